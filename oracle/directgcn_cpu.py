@@ -1,0 +1,120 @@
+"""ORACLE (test infrastructure only): fp32 CPU restatement of the reference DirectGCN path.
+
+Every function restates, op for op and in the same order, the reference code it cites, so that its
+results equal the reference's on the same inputs (bit-exact on the golden fixtures; see
+``tests/test_oracle_golden.py``). It runs on ATen CPU kernels, i.e. it IS the reference's CPU
+algorithm (index_select -> mul -> scatter_add_ per propagate), which is why ``bench.py`` times it as
+the ``cpu_baseline`` ("port").
+
+Parameters are passed as a dict keyed like the reference ``state_dict`` (e.g. ``lin_main_in.weight``,
+``C_in_vec``, ``constant``; model keys ``convs.{i}.*``, ``res_projs.{i}.*``, ``decoder_fc.{0,3}.*``,
+``pe_layer.weight``). Tensors may require grad: autograd through these functions gives the
+reference's gradients.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+
+# --------------------------------------------------------------------------------------------
+# PyG boundary (third-party, not vendored): MessagePassing(aggr='add').propagate, flow
+# source_to_target, PyG >= 2.3 sum path; message() = protgram_directgcn.py:137-140.
+# --------------------------------------------------------------------------------------------
+def propagate(edge_index: torch.Tensor, x: torch.Tensor, edge_weight: Optional[torch.Tensor]) -> torch.Tensor:
+    x_j = x.index_select(0, edge_index[0])
+    msg = x_j if edge_weight is None else edge_weight.view(-1, 1) * x_j
+    index = edge_index[1].view(-1, 1).expand_as(msg)
+    return msg.new_zeros((x.size(0), msg.size(1))).scatter_add_(0, index, msg)
+
+
+def linear(x, w, b=None):
+    return F.linear(x, w, b)
+
+
+# --------------------------------------------------------------------------------------------
+# DirectGCNLayer.forward -- src/models/protgram_directgcn.py:93-135
+# --------------------------------------------------------------------------------------------
+def layer_forward(p: dict, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices=None,
+                  use_vector_coeffs: bool = True, prefix: str = ""):
+    g = lambda k: p[prefix + k]  # noqa: E731
+    # the reference layer drops to scalar coefficients when num_nodes == 0 (:48-60)
+    use_vector_coeffs = use_vector_coeffs and (prefix + "C_in_vec") in p
+    # :101-103
+    h_main_in = propagate(ei_in, linear(x, g("lin_main_in.weight")), ew_in)
+    h_shared_in = propagate(ei_in, linear(x, g("lin_shared.weight")), ew_in)
+    ic = (h_main_in + g("bias_main_in")) + (h_shared_in + g("bias_directed_shared_in"))
+    # :106-108
+    h_main_out = propagate(ei_out, linear(x, g("lin_main_out.weight")), ew_out)
+    h_shared_out = propagate(ei_out, linear(x, g("lin_shared.weight")), ew_out)
+    oc = (h_main_out + g("bias_main_out")) + (h_shared_out + g("bias_directed_shared_out"))
+    # :111-113
+    h_main_u = propagate(ei_u, linear(x, g("lin_undirected.weight")), ew_u)
+    h_shared_u = propagate(ei_u, linear(x, g("lin_shared.weight")), ew_u)
+    uc = (h_main_u + g("bias_undirected")) + (h_shared_u + g("bias_undirected_shared"))
+    # :116-128
+    const = p.get(prefix + "constant")
+    if use_vector_coeffs and original_indices is not None:
+        oi = original_indices
+        c_in, c_out = g("C_in_vec")[oi], g("C_out_vec")[oi]
+        c_dir, c_u, c_all = g("C_directed_vec")[oi], g("C_undirected_vec")[oi], g("C_all_vec")[oi]
+        const_t = const[oi] if const is not None else 0
+    elif use_vector_coeffs:
+        c_in, c_out = g("C_in_vec"), g("C_out_vec")
+        c_dir, c_u, c_all = g("C_directed_vec"), g("C_undirected_vec"), g("C_all_vec")
+        const_t = const if const is not None else 0
+    else:
+        c_in, c_out, c_dir, c_u, c_all = g("C_in"), g("C_out"), g("C_directed"), g("C_undirected"), g("C_all")
+        const_t = 0
+    # :131-133
+    directed = c_dir * ((c_in * ic) + (c_out * oc))
+    undirected = c_u * uc
+    return (c_all * (undirected + directed)) + const_t
+
+
+def l2_normalize(x, eps=1e-12):
+    """EmbeddingProcessor.l2_normalize_torch, src/utils/models_utils.py:139-147 (eps added to the norm)."""
+    if x.ndim == 1:
+        return x / (torch.norm(x, p=2, keepdim=True) + eps)
+    return x / (torch.norm(x, p=2, dim=1, keepdim=True) + eps)
+
+
+def apply_pe(p: dict, x, n_gram_len: int, one_gram_dim: int):
+    """ProtGramDirectGCN._apply_pe, protgram_directgcn.py:182-193, written out-of-place (the reference's
+    in-place add raises under autograd when x does not require grad; values are identical)."""
+    w = p.get("pe_layer.weight")
+    if w is None:
+        return x
+    if n_gram_len > 0 and one_gram_dim > 0 and x.shape[1] == n_gram_len * one_gram_dim:
+        pos = min(n_gram_len, w.shape[0])
+        xr = x.view(-1, n_gram_len, one_gram_dim)
+        if pos > 0:
+            add = torch.zeros(n_gram_len, one_gram_dim, dtype=x.dtype)
+            add = torch.cat([w[:pos], add[pos:]], 0)
+            xr = xr + add.unsqueeze(0)
+        return xr.reshape(-1, n_gram_len * one_gram_dim)
+    return x
+
+
+def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices=None,
+                  n_gram_len: int = 0, one_gram_dim: int = 0, use_vector_coeffs: bool = True,
+                  training: bool = False, dropout: float = 0.5, l2_eps: float = 1e-12):
+    """ProtGramDirectGCN.forward, protgram_directgcn.py:195-222 (eval: dropout inactive)."""
+    h = apply_pe(p, x, n_gram_len, one_gram_dim)
+    for i in range(len(layer_dims) - 1):
+        h_res = h
+        out = layer_forward(p, h_res, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices,
+                            use_vector_coeffs, prefix=f"convs.{i}.")
+        if f"res_projs.{i}.weight" in p:
+            res = linear(h_res, p[f"res_projs.{i}.weight"], p[f"res_projs.{i}.bias"])
+        else:
+            res = h_res
+        h = F.leaky_relu(out + res)
+        h = F.dropout(h, p=dropout, training=training)
+    z = linear(h, p["decoder_fc.0.weight"], p["decoder_fc.0.bias"])
+    z = F.relu(z)
+    z = F.dropout(z, p=0.5, training=training)
+    logits = linear(z, p["decoder_fc.3.weight"], p["decoder_fc.3.bias"])
+    return F.log_softmax(logits, dim=-1), l2_normalize(h, eps=l2_eps)

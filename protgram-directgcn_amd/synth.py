@@ -1,0 +1,78 @@
+"""Seeded synthetic n-gram graphs, regenerable on the GPU box without fixtures.
+
+Two generators:
+
+* :func:`de_bruijn_edges` -- the complete n-gram transition graph B(20, n) in the reference's
+  node order. The reference numbers n-grams by the rank of the sorted n-gram strings
+  (``src/pipeline/data_builder.py:164,172-173``); with every n-gram present that rank is the
+  base-20 value of the string over the sorted alphabet ``ACDEFGHIKLMNPQRSTVWY``. Edge
+  ``s -> (20*s + c) mod 20**n`` (c = 0..19) is the window shift of ``data_builder.py:45-54``.
+  Raw transition count ``1 + splitmix64(0x5eed ^ (20*s + c)) mod 64``.
+* :func:`fasta_edges` -- random protein sequences cut into overlapping windows exactly as
+  ``data_builder.py:38-54`` does (no space padding), then grouped into unique
+  ``(source, target) -> count`` rows as ``data_builder.py:267-273`` does.
+
+Both return ``(num_nodes, src int64[E], dst int64[E], count float32[E])`` with unique
+``(src, dst)`` pairs sorted row-major, i.e. the content of the reference's edge parquet.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ALPHABET = "ACDEFGHIKLMNPQRSTVWY"
+SIGMA = 20
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """Vectorised splitmix64 finaliser on uint64 (wrap-around arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def de_bruijn_sizes(n: int) -> dict:
+    """|V|, E and shared-pattern nnz of the complete B(20, n) graph."""
+    N = SIGMA ** n
+    E = SIGMA ** (n + 1)
+    # 2*(non-loop transitions) - mutual pairs (the 380 two-periodic strings) + diagonal
+    nnz = 2 * (E - SIGMA) - SIGMA * (SIGMA - 1) + N
+    return {"N": N, "E": E, "nnz": nnz}
+
+
+def de_bruijn_edges(n: int, seed: int = 0x5EED):
+    N = SIGMA ** n
+    s = np.repeat(np.arange(N, dtype=np.int64), SIGMA)
+    c = np.tile(np.arange(SIGMA, dtype=np.int64), N)
+    eid = s * SIGMA + c
+    dst = eid % N
+    cnt = (splitmix64(np.uint64(seed) ^ eid.astype(np.uint64)) % np.uint64(64)).astype(np.float32) + 1.0
+    return N, s, dst, cnt
+
+
+def random_sequences(num_seqs: int, length: int, seed: int = 0) -> list[str]:
+    rng = np.random.default_rng(seed)
+    letters = np.array(list(ALPHABET))
+    return ["".join(letters[rng.integers(0, SIGMA, size=length)]) for _ in range(num_seqs)]
+
+
+def fasta_edges(n: int, sequences: list[str]):
+    """n-gram map (sorted unique strings -> rank) and unique transition counts."""
+    grams = set()
+    for seq in sequences:
+        for i in range(len(seq) - n + 1):
+            grams.add(seq[i:i + n])
+    ordered = sorted(grams)
+    ids = {g: i for i, g in enumerate(ordered)}
+    pairs: dict[tuple[int, int], int] = {}
+    for seq in sequences:
+        for i in range(len(seq) - n):
+            key = (ids[seq[i:i + n]], ids[seq[i + 1:i + 1 + n]])
+            pairs[key] = pairs.get(key, 0) + 1
+    keys = sorted(pairs)
+    src = np.array([k[0] for k in keys], dtype=np.int64)
+    dst = np.array([k[1] for k in keys], dtype=np.int64)
+    cnt = np.array([pairs[k] for k in keys], dtype=np.float32)
+    return len(ordered), src, dst, cnt, ordered

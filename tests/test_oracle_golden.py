@@ -1,0 +1,102 @@
+"""Pin the oracle (oracle/*.py) to the reference's own outputs (tests/golden).
+
+The oracle restates the reference op for op, so every comparison here is exact or at float32
+rounding-noise level (same ATen kernels, same order)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import CASES, graph, load, params, t
+from oracle import directgcn_cpu as oc
+from oracle import graph_cpu as og
+
+EXACT = dict(rtol=0, atol=0)
+TIGHT = dict(rtol=1e-6, atol=1e-7)
+
+MATRIX_CASES = ["f1_fasta2", "f1_debruijn2", "f2_edge", "f2_empty", "f5_fasta3", "f6_pe1"]
+
+
+@pytest.mark.parametrize("name", MATRIX_CASES)
+def test_oracle_matrices_match_reference(name):
+    fx = load(name)
+    m = og.build_matrices(int(fx["N"][0]), fx["src"], fx["dst"], fx["cnt"])
+    for k in ("in", "out", "und"):
+        idx, val = m[k]
+        np.testing.assert_array_equal(idx.numpy(), fx[f"{k}_idx"])
+        np.testing.assert_array_equal(val.numpy(), fx[f"{k}_val"])
+
+
+def test_oracle_matrices_debruijn3_checksums():
+    fx = load("f5_debruijn3")
+    import importlib
+    synth = importlib.import_module("protgram_directgcn_amd.synth")
+    N, s, d, c = synth.de_bruijn_edges(3)
+    m = og.build_matrices(N, s, d, c)
+    for k in ("in", "out", "und"):
+        idx, val = m[k]
+        assert val.numel() == fx[f"{k}_nnz"][0]
+        v64 = val.double()
+        np.testing.assert_allclose([v64.sum().item(), (v64 ** 2).sum().item()], fx[f"{k}_sum"], rtol=1e-12)
+        pick = fx[f"{k}_pick_idx"]
+        dense_pos = {(int(a), int(b)): i for i, (a, b) in enumerate(idx.t().tolist())}
+        got = np.array([val[dense_pos[(int(a), int(b))]].item() for a, b in pick.T], np.float32)
+        np.testing.assert_array_equal(got, fx[f"{k}_pick_val"])
+
+
+def _layer_prefixes(fx):
+    return sorted({k.split("_p:")[0] for k in fx if "_p:" in k and not k.startswith("M_")})
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c != "f5_debruijn3"])
+def test_oracle_layer_forward_and_grads(name):
+    fx = load(name)
+    ei, ew = graph(fx)
+    for tag in _layer_prefixes(fx):
+        if f"{tag}_y" not in fx:
+            continue
+        p = {k: v.requires_grad_(True) for k, v in params(fx, f"{tag}_p").items()}
+        x = t(fx[f"{tag}_x"]).requires_grad_(True)
+        orig = t(fx[f"{tag}_orig"]) if f"{tag}_orig" in fx else None
+        vec = bool(fx[f"{tag}_cfg"][3])
+        y = oc.layer_forward(p, x, ei["in"], ew["in"], ei["out"], ew["out"], ei["und"], ew["und"], orig, vec)
+        np.testing.assert_allclose(y.detach().numpy(), fx[f"{tag}_y"], **EXACT)
+        if f"{tag}_R" in fx:
+            (y * t(fx[f"{tag}_R"])).sum().backward()
+            np.testing.assert_allclose(x.grad.numpy(), fx[f"{tag}_gx"], **TIGHT)
+            for k, v in p.items():
+                g = v.grad.numpy() if v.grad is not None else np.zeros(v.shape, np.float32)
+                np.testing.assert_allclose(g, fx[f"{tag}_g:{k}"], **TIGHT, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["f1_fasta2", "f3_bench", "f6_pe1"])
+def test_oracle_model_forward_and_grads(name):
+    fx = load(name)
+    ei, ew = graph(fx)
+    cfg = fx["M_cfg"]
+    dims, (N, C, n, ogd) = list(cfg[:-4]), cfg[-4:]
+    p = {k: v.requires_grad_(True) for k, v in params(fx, "M_p").items()}
+    x = t(fx["M_x"]).requires_grad_(True)
+    lp, emb = oc.model_forward(p, dims, x, ei["in"], ew["in"], ei["out"], ew["out"], ei["und"], ew["und"],
+                               n_gram_len=int(n), one_gram_dim=int(ogd))
+    np.testing.assert_allclose(lp.detach().numpy(), fx["M_logp"], **EXACT)
+    np.testing.assert_allclose(emb.detach().numpy(), fx["M_emb"], **EXACT)
+    ((lp * t(fx["M_R1"])).sum() + (emb * t(fx["M_R2"])).sum()).backward()
+    np.testing.assert_allclose(x.grad.numpy(), fx["M_gx"], **TIGHT)
+    for k, v in p.items():
+        g = v.grad.numpy() if v.grad is not None else np.zeros(v.shape, np.float32)
+        np.testing.assert_allclose(g, fx[f"M_g:{k}"], **TIGHT, err_msg=k)
+
+
+def test_oracle_debruijn3_layer_samples():
+    fx = load("f5_debruijn3")
+    import importlib
+    synth = importlib.import_module("protgram_directgcn_amd.synth")
+    N, s, d, c = synth.de_bruijn_edges(3)
+    m = og.build_matrices(N, s, d, c)
+    p = params(fx, "L_p")
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234))
+    np.testing.assert_allclose([x.double().sum().item(), (x.double() ** 2).sum().item()], fx["L_xsum"], rtol=1e-12)
+    with torch.no_grad():
+        y = oc.layer_forward(p, x, *m["in"], *m["out"], *m["und"])
+    np.testing.assert_array_equal(y[t(fx["L_rows"])].numpy(), fx["L_y_rows"])
+    np.testing.assert_allclose(y.double().sum(0).numpy(), fx["L_colsum"], rtol=1e-12, atol=1e-9)

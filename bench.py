@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Bench: edges/sec propagated, DirectGCN forward on the 4-gram graph (BASELINE.json metric).
+
+Workload: complete n-gram graph B(20,4) in the reference's node order (N=160,000,
+E=3,200,000 transitions, 6,559,580 entries per adjacency, shared pattern), synthetic features
+X = randn(N, 128) (seed 1234), ProtGramDirectGCN with layer_dims [128,128,128] (2 DirectGCN layers,
+identity residuals), C=20 classes, eval mode, fp32. One step = one full model forward (both layers,
+decoder, log_softmax, L2-normalised embeddings), inputs resident in HBM.
+  edges/s = 3 * nnz * L / t_step   (each adjacency entry counted once per layer)
+
+--gpus N (torchrun, one process per GPU): node-range partition of the same graph across the N ranks,
+RCCL all-gather of the layer-1 output rows between the layers ("scaling": "strong": total work fixed).
+Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
+over ranks is reported. Rank 0 prints one JSON line.
+
+Extra fields: "roofline" for the dominant kernel (pg_spmm3_f32: algorithmic bytes per launch / its
+average duration from HIP events recorded on its launch stream inside the timed region) and
+"cpu_baseline" (the oracle = the reference's CPU algorithm, timed on this host, rank 0 at N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--ngram", type=int, default=4)
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--fused-norm", action="store_true", help="compute edge weights inside the SpMM")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-layers", type=int, default=1)
+    ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def log(*a):
+        if rank == 0:
+            print(*a, file=sys.stderr, flush=True)
+
+    n, Fd, L = args.ngram, args.feat, args.layers
+    sizes = pkg.synth.de_bruijn_sizes(n)
+    N = sizes["N"]
+    t0 = time.time()
+    s, d, c = pkg.synth.de_bruijn_edges(n)[1:]
+    g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm)
+    torch.cuda.synchronize()
+    log(f"[bench] graph B(20,{n}): N={N} E={s.size} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s")
+
+    torch.manual_seed(0)
+    dims = [Fd] * (L + 1)
+    C = 20
+    model = pkg.ProtGramDirectGCN(dims, N, C, n, 0, 512, 0.5, True)
+    with torch.no_grad():  # non-trivial gates/biases (the reference init has C=1, b=0)
+        gen = torch.Generator().manual_seed(11)
+        for name, p in model.named_parameters():
+            leaf = name.split(".")[-1]
+            if leaf.startswith("C_"):
+                p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+            elif "bias" in leaf:
+                p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+    model = model.to(dev).eval()
+    model.fused_norm = args.fused_norm
+    x = torch.randn(N, Fd, generator=torch.Generator().manual_seed(1234)).to(dev)
+    data = pkg.Data(x=x, graph=g)
+
+    part = shard.partition(g, rank, world) if world > 1 else None
+    gbufs = [torch.empty(part.per * world, Fd, device=dev) for _ in range(L - 1)] if part else None
+
+    def step():
+        with torch.no_grad():
+            if part is None:
+                return model(data)
+            return shard.sharded_forward(model, part, x, gather_buf=gbufs)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.SPMM_EVENTS = []
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
+    spmm_ms = [e0.elapsed_time(e1) for e0, e1 in events]
+    t_local = torch.tensor([elapsed, sum(spmm_ms) / max(1, len(spmm_ms))], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+    elapsed, spmm_avg_ms = float(t_local[0]), float(t_local[1])
+    ms_per_step = elapsed / args.steps * 1e3
+    edges_per_step = 3 * g.nnz * L
+    value = edges_per_step * args.steps / elapsed
+
+    # roofline of the dominant kernel (SURVEY §8d B_agg, per launch = this rank's rows)
+    if part is None:
+        launch_bytes = g.algorithmic_bytes(Fd)
+        launch_nnz, launch_rows = g.nnz, N
+    else:
+        launch_nnz, launch_rows = part.local.nnz, part.n_local
+        launch_bytes = 8 * (launch_rows + 1) + launch_nnz * (16 + 4 * Fd) + 3 * launch_rows * Fd * 4
+    achieved = launch_bytes / (spmm_avg_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", "traffic_r01.json")
+    if os.path.exists(tfile) and world == 1:
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("workload") == f"B(20,{n})/F{Fd}" and tj.get("kernel_bytes_per_launch"):
+                traffic = tj["kernel_bytes_per_launch"]
+        except (OSError, ValueError):
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": "pg_spmm3_f32" if not args.fused_norm else "pg_spmm3_fusednorm_f32",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": launch_bytes, "avg_launch_ms": round(spmm_avg_ms, 4),
+                "launches_timed": len(spmm_ms)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(g, model, x, args.cpu_sample_layers, log)
+
+    extra = {}
+    if args.extra and world == 1:
+        extra = extra_measurements(pkg, ops, g, model, x, data, log)
+
+    if rank == 0:
+        line = {
+            "metric": "edges/sec propagated, DirectGCN fwd on 4-gram graph, 1/2/4/8 MI355X",
+            "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"directgcn_fwd_B(20,{n})", "graph": f"complete n-gram de Bruijn B(20,{n})",
+                       "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
+                       "layers": L, "layer_dims": dims, "classes": C,
+                       "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
+                       "parallelism": f"node_range_x{world}" if world > 1 else "single"},
+            "nodes_per_sec": round(N * L * args.steps / elapsed, 1),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if extra:
+            line["extra"] = extra
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(g, model, x, layers, log):
+    """The reference algorithm on this host's CPU (oracle = op-for-op restatement of
+    protgram_directgcn.py:93-135 with PyG's propagate), on the same graph / weights / features:
+    ``layers`` DirectGCN layer forward(s) of the full graph (a bounded sample of the workload)."""
+    import numpy as np
+    import torch
+
+    from oracle import directgcn_cpu as oc
+
+    threads = torch.get_num_threads()
+    e = g.edges3.cpu().numpy()
+    N = g.n_rows
+    rows = torch.from_numpy(np.repeat(np.arange(N, dtype=np.int64), np.diff(g.rowptr.cpu().numpy())))
+    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
+    w = [torch.from_numpy(e[:, 1 + j].copy().view(np.float32)) for j in range(3)]
+    xc = x.cpu()
+    times = []
+    with torch.no_grad():
+        for i, conv in enumerate(model.convs[:layers]):
+            p = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
+            for rep in range(2):  # 1 warm-up + 1 timed per layer
+                t0 = time.perf_counter()
+                y = oc.layer_forward(p, xc, ei, w[0], ei, w[1], ei, w[2])
+                dt = time.perf_counter() - t0
+                if rep:
+                    times.append(dt)
+            xc = torch.nn.functional.leaky_relu(y + xc)
+    t = sum(times)
+    val = 3 * g.nnz * len(times) / t
+    log(f"[bench] cpu baseline: {len(times)} layer(s) in {t:.2f}s on {threads} threads -> {val:.3e} edges/s")
+    return {"value": round(val, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} DirectGCN layer forward(s) of the full graph (N={N}, 3x{g.nnz} entries), "
+                      f"oracle = reference CPU algorithm (6 Linear + 6 index_select/mul/scatter_add_), "
+                      f"torch {torch.__version__} CPU, {threads} threads, median-free single timed run per layer "
+                      f"after 1 warm-up",
+            "seconds": round(t, 3)}
+
+
+def extra_measurements(pkg, ops, g, model, x, data, log):
+    """Kernel-variant timings and a training step (diagnostics, stderr + 'extra' field)."""
+    import torch
+    res = {}
+
+    def timeit(fn, reps=20):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    Fd = x.size(1)
+    B = g.algorithmic_bytes(Fd)
+    for fl, name in ((0, "default"), (1, "no_xcd_remap"), (2, "edge_lds"), (4, "unroll4"), (6, "edge_lds+unroll4")):
+        ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
+        res[f"spmm3_{name}_ms"] = round(ms, 4)
+        res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)
+        if g.raw is not None:
+            ms = timeit(lambda: ops.spmm3(g, x, fused=True, flags=fl))
+            res[f"spmm3_fused_{name}_ms"] = round(ms, 4)
+    Z = ops.spmm3(g, x)
+    conv = model.convs[0]
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True))
+    flops = 2 * x.size(0) * 3 * Fd * conv.out_channels
+    res["dense_ms"] = round(ms, 4)
+    res["dense_TFLOPs"] = round(flops / ms / 1e9, 2)
+    G = torch.randn_like(Z)
+    ms = timeit(lambda: ops.spmm3_t(g, G))
+    res["spmm3t_ms"] = round(ms, 4)
+    # copy-kernel bandwidth reference
+    a = torch.empty(512 * 1024 * 1024 // 4, device=x.device)
+    b = torch.empty_like(a)
+    ms = timeit(lambda: b.copy_(a))
+    res["copy_GBs"] = round(2 * a.numel() * 4 / ms / 1e6, 1)
+    # training step (fwd + bwd + Adam)
+    model.train()
+    y = (torch.arange(x.size(0), device=x.device) // (20 ** 3)).clamp(max=19)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    import torch.nn.functional as F
+
+    def train_step():
+        opt.zero_grad()
+        lp, _ = model(data)
+        loss = F.nll_loss(lp, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters())
+        loss.backward()
+        opt.step()
+
+    res["train_step_ms"] = round(timeit(train_step, reps=5), 3)
+    model.eval()
+    log(f"[bench] extra: {json.dumps(res)}")
+    return res
+
+
+if __name__ == "__main__":
+    main()

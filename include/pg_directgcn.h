@@ -1,0 +1,149 @@
+/*
+ * pg_directgcn.h -- C ABI of the MI355X (gfx950) DirectGCN message-passing hot path.
+ *
+ * Replaces, per DirectGCN layer, the six PyG `MessagePassing.propagate` calls and the six
+ * `nn.Linear` calls of the reference (`src/models/protgram_directgcn.py:101-112`, propagate =
+ * gather x[ei[0]] * w -> scatter_add into ei[1], `:137-140` + PyG aggr='add' at `:27`), plus the
+ * gate/bias/constant combine (`:116-133`), the model's residual + leaky_relu (`:214-215`) and the
+ * propagation-matrix normalisation (`src/utils/graph_utils.py:160-273`) in fused form.
+ *
+ * Conventions
+ *  - Every pointer is DEVICE memory owned by the caller. The library never allocates or frees.
+ *  - Every call enqueues work on `stream` (a hipStream_t passed as void*; NULL = legacy default
+ *    stream) and returns without synchronising. Calls are stateless and re-entrant.
+ *  - Return value: PG_OK (0) or a negative PG_ERR_*; `pg_last_error()` gives a thread-local message.
+ *  - Sparse matrices are CSR keyed by DESTINATION row (the reference's ei[1]); `col` is the
+ *    SOURCE node (ei[0]). Within a row, entries are sorted by ascending col: this is the order in
+ *    which the reference's coalesced COO feeds scatter_add_, so accumulation order matches it.
+ *  - Dense matrices are row-major fp32 with an explicit leading dimension (in elements).
+ */
+#ifndef PG_DIRECTGCN_H
+#define PG_DIRECTGCN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_ABI_VERSION 1
+
+#define PG_OK 0
+#define PG_ERR_ARG (-1)
+#define PG_ERR_HIP (-2)
+#define PG_ERR_UNSUPPORTED (-3)
+
+/* Shared-pattern edge record, precomputed weights: one 16-byte load per pattern entry. The three
+ * weights are the values of mathcal_A_in, mathcal_A_out and A_undirected_norm at (col -> row)
+ * (graph_utils.py:275-287, :160-196). Absent weights (edge_weight=None) are stored as 1.0f. */
+typedef struct pg_edge3 {
+    int32_t col;
+    float w_in;
+    float w_out;
+    float w_und;
+} pg_edge3_t;
+
+/* Shared-pattern edge record, raw counts (fused-normalisation mode). For destination row i and
+ * source j = col: a_fwd = count of transition j->i (A_out_w[j,i]), a_bwd = count of i->j,
+ * m_und = multiplicity of the undirected entry (2 on a raw self-loop: PyG add_self_loops appends
+ * a second loop, graph_utils.py:180; else 1). a_fwd = a_bwd = 0 marks an identity-only diagonal. */
+typedef struct pg_edgeraw {
+    int32_t col;
+    float a_fwd;
+    float a_bwd;
+    float m_und;
+} pg_edgeraw_t;
+
+/* Single-adjacency edge record (non-shared patterns, e.g. gnn_benchmarker.py:297-305 wiring). */
+typedef struct pg_edge1 {
+    int32_t col;
+    float w;
+} pg_edge1_t;
+
+/* Per-node normalisation terms for fused mode, float4 per node:
+ *   x = 1/rowsum(A_out_w) (0 if the row is empty)   -- graph_utils.py:231-235 on A_out_w
+ *   y = 1/rowsum(A_in_w)  (0 if empty)              -- same on A_in_w = A_out_w^T
+ *   z = deg_und^-1/2 (0 if deg 0)                    -- graph_utils.py:187-189
+ *   w = 0 (padding) */
+
+/* Flags (bit field) accepted by the SpMM entry points. */
+#define PG_FLAG_NO_XCD_REMAP (1u << 0) /* keep hardware blockIdx order instead of XCD-contiguous rows */
+#define PG_FLAG_EDGE_LDS (1u << 1)     /* stage edge records through LDS (variant B) */
+#define PG_FLAG_UNROLL4 (1u << 2)      /* 4 gathers in flight per lane instead of 8 */
+
+const char* pg_last_error(void);
+int pg_abi_version(void);
+
+/* Z[i, 0:F] = sum_e w_in*X[col], Z[i, F:2F] = sum_e w_out*X[col], Z[i, 2F:3F] = sum_e w_und*X[col]
+ * over row i of the shared pattern. One pass: each X row gathered once per pattern entry.
+ * Replaces the 3 x 2 propagate calls of protgram_directgcn.py:101-112 (aggregate-then-transform).
+ * Requirements: ldx >= F, ldz >= 3F, n_rows rows in rowptr (n_rows+1 entries), col < rows(X). */
+int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges,
+                 const float* X, int64_t ldx, int64_t F,
+                 float* Z, int64_t ldz, uint32_t flags, void* stream);
+
+/* Same output as pg_spmm3_f32, with the three propagation weights computed in-kernel from raw counts
+ * (graph_utils.py:198-273 closed form; bit-exact to the reference's torch.sparse construction) and
+ * the per-node terms `node_norm` ([n_nodes, 4] as described above). eps = GCN_PROPAGATION_EPSILON. */
+int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* edges,
+                           const float* node_norm, float eps,
+                           const float* X, int64_t ldx, int64_t F,
+                           float* Z, int64_t ldz, uint32_t flags, void* stream);
+
+/* Materialise the precomputed-weight records from raw records (same closed form as fused mode). */
+int pg_edges_normalize_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* raw,
+                           const float* node_norm, float eps, pg_edge3_t* out, void* stream);
+
+/* Transposed propagation (backward of pg_spmm3_f32): dX[j, :] = sum_k sum_{e in row j of A_k^T}
+ * w_k * G[col, kF:(k+1)F]. `edges` is the CSR of the TRANSPOSED pattern (keyed by source), or the
+ * forward CSR itself when all three matrices are symmetric (n-gram graphs: SURVEY §8a A10).
+ * If accumulate != 0, dX += result. */
+int pg_spmm3t_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges,
+                  const float* G, int64_t ldg, int64_t F,
+                  float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+
+/* Single adjacency: Y[i, :] (+)= sum_e w * X[col, :]. Used for non-shared patterns (one call per
+ * adjacency writing its column block of Z) and their transposes. */
+int pg_spmm1_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge1_t* edges,
+                 const float* X, int64_t ldx, int64_t F,
+                 float* Y, int64_t ldy, int accumulate, uint32_t flags, void* stream);
+
+/* Dense DirectGCN contraction + combine on MFMA (v_mfma_f32_32x32x2_f32, exact fp32 products).
+ * Given the three aggregates Z = [A_in X | A_out X | A_und X] ([M, 3*F_in]), computes per row m
+ *   y[m] = s_in[m]  * (Z_in[m]  (W_main_in  + W_shared)^T + b_main_in  + b_dir_shared_in)
+ *        + s_out[m] * (Z_out[m] (W_main_out + W_shared)^T + b_main_out + b_dir_shared_out)
+ *        + s_und[m] * (Z_und[m] (W_undirected + W_shared)^T + b_undirected + b_undirected_shared)
+ *        + constant[r(m)]                                    (vector-coefficient mode only)
+ *   s_in = c_all*c_dir*c_in, s_out = c_all*c_dir*c_out, s_und = c_all*c_und,  c_x = C_x_vec[r(m)] or C_x[0]
+ *   r(m) = rows ? rows[m] : m                                 (original_indices, :116-120)
+ * which is protgram_directgcn.py:100-133 with A(xW) = (Ax)W. Optionally fused after it
+ * (ProtGramDirectGCN.forward :213-215): + residual (res_x[m] when W_res == NULL, else
+ * res_x[m] W_res^T + b_res as a 4th K segment), then leaky_relu(slope) when act != 0.
+ * All weights are nn.Linear layout [F_out, F_in] with leading dimension F_in (contiguous). */
+#define PG_GATES_VECTOR 0
+#define PG_GATES_SCALAR 1
+
+typedef struct pg_layer_args {
+    int64_t M, F_in, F_out;
+    const float* Z; int64_t ldz;
+    const float* W_main_in; const float* W_main_out; const float* W_undirected; const float* W_shared;
+    const float* b_main_in; const float* b_dir_shared_in;
+    const float* b_main_out; const float* b_dir_shared_out;
+    const float* b_undirected; const float* b_undirected_shared;
+    int32_t gate_mode;
+    const float* C_in; const float* C_out; const float* C_directed; const float* C_undirected; const float* C_all;
+    const int64_t* rows;
+    const float* constant; int64_t ld_const;
+    const float* res_x; int64_t ld_res;
+    const float* W_res; const float* b_res;
+    int32_t act; float slope;
+    float* Y; int64_t ldy;
+} pg_layer_args_t;
+
+int pg_directgcn_dense_f32(const pg_layer_args_t* args, uint32_t flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PG_DIRECTGCN_H */

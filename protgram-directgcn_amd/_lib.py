@@ -1,0 +1,96 @@
+"""ctypes binding of the in-tree C-ABI library ``libpgdgcn.so`` (include/pg_directgcn.h).
+
+There is no fallback: if the library is missing or fails to load, every op raises
+:class:`NativeLibraryError`. ``load_library()`` needs no GPU (dlopen + symbol check only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.environ.get("PG_DIRECTGCN_LIB", os.path.join(_HERE, "libpgdgcn.so"))
+
+PG_OK = 0
+PG_FLAG_NO_XCD_REMAP = 1 << 0
+PG_FLAG_EDGE_LDS = 1 << 1
+PG_FLAG_UNROLL4 = 1 << 2
+
+c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class LayerArgs(ctypes.Structure):
+    """pg_layer_args_t"""
+    _fields_ = [("M", c_i64), ("F_in", c_i64), ("F_out", c_i64),
+                ("Z", c_vp), ("ldz", c_i64),
+                ("W_main_in", c_vp), ("W_main_out", c_vp), ("W_undirected", c_vp), ("W_shared", c_vp),
+                ("b_main_in", c_vp), ("b_dir_shared_in", c_vp),
+                ("b_main_out", c_vp), ("b_dir_shared_out", c_vp),
+                ("b_undirected", c_vp), ("b_undirected_shared", c_vp),
+                ("gate_mode", c_i32),
+                ("C_in", c_vp), ("C_out", c_vp), ("C_directed", c_vp), ("C_undirected", c_vp), ("C_all", c_vp),
+                ("rows", c_vp),
+                ("constant", c_vp), ("ld_const", c_i64),
+                ("res_x", c_vp), ("ld_res", c_i64),
+                ("W_res", c_vp), ("b_res", c_vp),
+                ("act", c_i32), ("slope", c_f32),
+                ("Y", c_vp), ("ldy", c_i64)]
+
+
+# symbol -> (restype, argtypes); every symbol declared in include/pg_directgcn.h
+SIGNATURES = {
+    "pg_last_error": (ctypes.c_char_p, []),
+    "pg_abi_version": (ctypes.c_int, []),
+    "pg_spmm3_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                              c_u32, c_vp]),
+    "pg_edges_normalize_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32, c_vp]),
+    "pg_spmm1_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32, c_vp]),
+    "pg_directgcn_dense_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_u32, c_vp]),
+}
+
+_lib = None
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load_library():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise NativeLibraryError(
+            f"HIP library not found at {_LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback)")
+    try:
+        lib = ctypes.CDLL(_LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"failed to load {_LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            raise NativeLibraryError(f"{_LIB_PATH} does not export {name}")
+        fn.restype, fn.argtypes = res, args
+    if lib.pg_abi_version() != 1:
+        raise NativeLibraryError("ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != PG_OK:
+        msg = load_library().pg_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def default_flags() -> int:
+    """Kernel-variant flags (tuning knob; PG_SPMM_FLAGS env overrides)."""
+    v = os.environ.get("PG_SPMM_FLAGS")
+    return int(v, 0) if v else 0

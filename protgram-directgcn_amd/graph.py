@@ -1,0 +1,253 @@
+"""Device-resident CSR for the DirectGCN propagation (HBM layout of SURVEY §8b/§8d).
+
+Two ways in:
+
+* :func:`csr_from_coo` -- the drop-in boundary. Takes the reference's COO inputs exactly as the
+  trainer wires them (``edge_index_* = mathcal_A_*.indices()``, ``edge_weight_* = .values()``,
+  ``protgram_directgcn_trainer.py:362-367``; or the benchmarker's ``edge_weight=None`` wiring,
+  ``gnn_benchmarker.py:297-305``), detects whether the three adjacencies share one pattern, and
+  converts once to CSR keyed by destination (``ei[1]``). Results are cached per input tensors.
+* :func:`build_propagation_csr` -- builds the three n-gram propagation matrices directly from the raw
+  transition table (the reference's edge parquet, ``graph_utils.py:106-119``) in shared-pattern form,
+  with the normalisation (``graph_utils.py:160-273``) done on the GPU by ``pg_edges_normalize_f32``
+  or fused into the SpMM (``pg_spmm3_fusednorm_f32``).
+
+HBM layout, shared pattern (n-gram graphs):
+  rowptr  int64 [n+1]
+  edges3  int32 [nnz, 4] = {col, bits(w_in), bits(w_out), bits(w_und)}  -- 16 B per entry, one load
+  raw     int32 [nnz, 4] = {col, bits(a_fwd), bits(a_bwd), bits(m_und)}  (fused-norm mode)
+  node_norm f32 [n, 4]  = {1/dout, 1/din, deg_und^-1/2, 0}
+Non-shared patterns keep one ``{col, bits(w)}`` CSR (8 B per entry) per adjacency.
+Backward uses the transposed CSR; when all three matrices are symmetric (always true for the n-gram
+matrices) it aliases the forward CSR.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+_CACHE: "dict[tuple, CSRGraph]" = {}
+_CACHE_MAX = 8
+
+
+@dataclass
+class ShapedAdjacency:
+    """One adjacency in CSR-by-destination form with its transpose (CSR-by-source)."""
+    rowptr: torch.Tensor
+    edges: torch.Tensor  # int32 [nnz, 2] {col, bits(w)}
+    rowptr_t: torch.Tensor
+    edges_t: torch.Tensor
+    nnz: int
+
+
+@dataclass
+class CSRGraph:
+    n_rows: int
+    shared: bool
+    rowptr: Optional[torch.Tensor] = None
+    edges3: Optional[torch.Tensor] = None
+    rowptr_t: Optional[torch.Tensor] = None
+    edges3_t: Optional[torch.Tensor] = None
+    symmetric: bool = False
+    adj: list = field(default_factory=list)  # non-shared: [in, out, und] ShapedAdjacency
+    raw: Optional[torch.Tensor] = None
+    node_norm: Optional[torch.Tensor] = None
+    eps: float = 1e-9
+    nnz: int = 0
+
+    @property
+    def device(self):
+        t = self.rowptr if self.shared else self.adj[0].rowptr
+        return t.device
+
+    def nnz_total(self) -> int:
+        return 3 * self.nnz if self.shared else sum(a.nnz for a in self.adj)
+
+    def algorithmic_bytes(self, F: int, elem: int = 4) -> int:
+        """SURVEY §8d B_agg: rowptr + records + one X-row gather per entry + 3 output rows."""
+        n = self.n_rows
+        if self.shared:
+            return 8 * (n + 1) + self.nnz * (16 + F * elem) + 3 * n * F * elem
+        return sum(8 * (n + 1) + a.nnz * (8 + F * elem) + n * F * elem for a in self.adj)
+
+
+def _bits(w: torch.Tensor) -> torch.Tensor:
+    return w.contiguous().to(torch.float32).view(torch.int32)
+
+
+def _sort_by(primary: torch.Tensor, secondary: torch.Tensor, n_secondary: int) -> torch.Tensor:
+    key = primary * max(n_secondary, 1) + secondary
+    return torch.sort(key, stable=True).indices
+
+
+def _rowptr(rows: torch.Tensor, n: int) -> torch.Tensor:
+    counts = torch.bincount(rows, minlength=n) if rows.numel() else torch.zeros(n, dtype=torch.long,
+                                                                                   device=rows.device)
+    rp = torch.zeros(n + 1, dtype=torch.int64, device=rows.device)
+    rp[1:] = torch.cumsum(counts[:n], 0)
+    return rp
+
+
+def _validate(ei: torch.Tensor, n_rows: int, name: str):
+    if ei.dim() != 2 or ei.size(0) != 2:
+        raise ValueError(f"{name} must have shape [2, nnz], got {tuple(ei.shape)}")
+    if ei.numel():
+        lo, hi = int(ei.min()), int(ei.max())
+        if lo < 0 or hi >= n_rows:
+            raise IndexError(f"{name} holds node ids in [{lo}, {hi}] outside [0, {n_rows})")
+
+
+def _single(ei: torch.Tensor, ew: Optional[torch.Tensor], n: int) -> ShapedAdjacency:
+    ei = ei.to(torch.int64)
+    src, dst = ei[0], ei[1]
+    w = torch.ones(src.numel(), dtype=torch.float32, device=ei.device) if ew is None else ew.reshape(-1)
+    if w.numel() != src.numel():
+        raise ValueError("edge_weight length does not match edge_index")
+    p = _sort_by(dst, src, n)
+    e = torch.stack([src[p].to(torch.int32), _bits(w[p])], 1).contiguous()
+    pt = _sort_by(src, dst, n)
+    et = torch.stack([dst[pt].to(torch.int32), _bits(w[pt])], 1).contiguous()
+    return ShapedAdjacency(_rowptr(dst, n), e, _rowptr(src, n), et, int(src.numel()))
+
+
+def _key(*ts, n):
+    k = [n]
+    for t in ts:
+        if t is None:
+            k.append(None)
+        else:
+            k.append((t.data_ptr(), t._version, tuple(t.shape), t.dtype, str(t.device)))
+    return tuple(k)
+
+
+def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, cache: bool = True) -> CSRGraph:
+    """Convert the reference's three COO adjacencies to the device CSR (cached by tensor identity)."""
+    key = _key(ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, n=num_rows)
+    if cache and key in _CACHE:
+        return _CACHE[key]
+    n = int(num_rows)
+    for name, ei in (("edge_index_in", ei_in), ("edge_index_out", ei_out), ("edge_index_undirected", ei_und)):
+        _validate(ei, n, name)
+    shared = (ei_in.shape == ei_out.shape == ei_und.shape and ei_in.numel() > 0
+              and torch.equal(ei_in, ei_out) and torch.equal(ei_in, ei_und))
+    if shared:
+        ei = ei_in.to(torch.int64)
+        src, dst = ei[0], ei[1]
+        nnz = src.numel()
+        ones = None
+
+        def w(t):
+            nonlocal ones
+            if t is None:
+                if ones is None:
+                    ones = torch.ones(nnz, dtype=torch.float32, device=ei.device)
+                return ones
+            if t.numel() != nnz:
+                raise ValueError("edge_weight length does not match edge_index")
+            return t.reshape(-1)
+
+        wi, wo, wu = w(ew_in), w(ew_out), w(ew_und)
+        p = _sort_by(dst, src, n)
+        edges3 = torch.stack([src[p].to(torch.int32), _bits(wi[p]), _bits(wo[p]), _bits(wu[p])], 1).contiguous()
+        rowptr = _rowptr(dst, n)
+        pt = _sort_by(src, dst, n)
+        edges3_t = torch.stack([dst[pt].to(torch.int32), _bits(wi[pt]), _bits(wo[pt]), _bits(wu[pt])], 1).contiguous()
+        rowptr_t = _rowptr(src, n)
+        sym = torch.equal(rowptr, rowptr_t) and torch.equal(edges3, edges3_t)
+        if sym:
+            rowptr_t, edges3_t = rowptr, edges3
+        g = CSRGraph(n_rows=n, shared=True, rowptr=rowptr, edges3=edges3, rowptr_t=rowptr_t, edges3_t=edges3_t,
+                     symmetric=sym, nnz=nnz)
+    else:
+        g = CSRGraph(n_rows=n, shared=False,
+                     adj=[_single(ei_in, ew_in, n), _single(ei_out, ew_out, n), _single(ei_und, ew_und, n)])
+    if cache:
+        if len(_CACHE) >= _CACHE_MAX:
+            _CACHE.pop(next(iter(_CACHE)))
+        _CACHE[key] = g
+    return g
+
+
+def clear_cache():
+    _CACHE.clear()
+
+
+# ------------------------------------------------------------------------------------------------
+# n-gram propagation matrices straight from the raw transition table
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class RawNgramCSR:
+    n: int
+    rowptr: torch.Tensor     # int64 [n+1]
+    raw: torch.Tensor        # int32 [nnz, 4] {col, a_fwd, a_bwd, m_und}
+    node_norm: torch.Tensor  # f32 [n, 4]
+    nnz: int
+
+
+def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu") -> RawNgramCSR:
+    """Shared pattern of (A u A^T u I) with raw counts, plus per-node normalisation terms.
+
+    Integer work (pattern, grouping, sorting) runs with torch on ``device``; the O(n) float terms are
+    computed on the host with IEEE float32 ops so they equal the reference's torch CPU values bit for
+    bit: 1/rowsum (graph_utils.py:231-235) and deg^-1/2 (graph_utils.py:187-189)."""
+    n = int(num_nodes)
+    src_np = np.asarray(src, dtype=np.int64)
+    dst_np = np.asarray(dst, dtype=np.int64)
+    cnt_np = np.asarray(cnt, dtype=np.float32)
+    if src_np.size and (src_np.min() < 0 or max(src_np.max(), dst_np.max()) >= n):
+        raise IndexError("edge ids outside [0, num_nodes)")
+    dev = torch.device(device)
+    s = torch.from_numpy(src_np).to(dev)
+    d = torch.from_numpy(dst_np).to(dev)
+    c = torch.from_numpy(cnt_np).to(dev)
+    ar = torch.arange(n, dtype=torch.int64, device=dev)
+    zeros_e = torch.zeros_like(c)
+    rows = torch.cat([d, s, ar])
+    cols = torch.cat([s, d, ar])
+    a_fwd = torch.cat([c, zeros_e, torch.zeros(n, device=dev)])
+    a_bwd = torch.cat([zeros_e, c, torch.zeros(n, device=dev)])
+    key = rows * max(n, 1) + cols
+    uk, inv = torch.unique(key, sorted=True, return_inverse=True)
+    nnz = uk.numel()
+    af = torch.zeros(nnz, dtype=torch.float32, device=dev).index_add_(0, inv, a_fwd)
+    ab = torch.zeros(nnz, dtype=torch.float32, device=dev).index_add_(0, inv, a_bwd)
+    r_row = uk // max(n, 1)
+    r_col = uk % max(n, 1)
+    m = torch.where((r_row == r_col) & (af > 0), 2.0, 1.0).to(torch.float32)
+    rowptr = _rowptr(r_row, n)
+    raw = torch.stack([r_col.to(torch.int32), _bits(af), _bits(ab), _bits(m)], 1).contiguous()
+    # per-node terms (host, O(n))
+    dout = np.bincount(src_np, weights=cnt_np.astype(np.float64), minlength=n).astype(np.float32)
+    din = np.bincount(dst_np, weights=cnt_np.astype(np.float64), minlength=n).astype(np.float32)
+    one = np.float32(1.0)
+    with np.errstate(divide="ignore"):
+        dout_inv = np.where(dout != 0, one / np.where(dout != 0, dout, one), np.float32(0)).astype(np.float32)
+        din_inv = np.where(din != 0, one / np.where(din != 0, din, one), np.float32(0)).astype(np.float32)
+    deg = torch.bincount(r_row, weights=m.to(torch.float64), minlength=n).cpu().numpy().astype(np.float32)
+    with np.errstate(divide="ignore"):
+        r = (one / np.sqrt(deg)).astype(np.float32)
+    r[np.isinf(r)] = 0
+    nn_ = np.stack([dout_inv, din_inv, r, np.zeros(n, np.float32)], 1).astype(np.float32)
+    node_norm = torch.from_numpy(np.ascontiguousarray(nn_)).to(dev)
+    return RawNgramCSR(n, rowptr, raw, node_norm, int(nnz))
+
+
+def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,
+                          keep_raw: bool = True) -> CSRGraph:
+    """Shared-pattern device CSR of (mathcal_A_in, mathcal_A_out, A_undirected_norm) from raw counts.
+
+    Weights are materialised on the GPU by ``pg_edges_normalize_f32`` (bit-exact closed form of
+    graph_utils.py:198-273 / :160-196)."""
+    from . import ops
+
+    if int(num_nodes) > 0 and np.asarray(src).size == 0:
+        raise ValueError("graph without transitions: its mathcal_A_in/out are empty while A_undirected_norm "
+                         "holds self-loops (no shared pattern); use csr_from_coo on the reference matrices")
+    rc = ngram_raw_csr(num_nodes, src, dst, cnt, device=device)
+    edges3 = ops.edges_normalize(rc, eps)
+    return CSRGraph(n_rows=rc.n, shared=True, rowptr=rc.rowptr, edges3=edges3, rowptr_t=rc.rowptr,
+                    edges3_t=edges3, symmetric=True, raw=rc.raw if keep_raw else None,
+                    node_norm=rc.node_norm if keep_raw else None, eps=eps, nnz=rc.nnz)

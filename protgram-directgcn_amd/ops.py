@@ -1,0 +1,313 @@
+"""Torch-facing wrappers of the C-ABI kernels and their autograd rules.
+
+Forward passes run only in the HIP library (``libpgdgcn.so``) on the caller's current HIP stream.
+Backward passes use the same library for the sparse transposed propagation (``pg_spmm3t_f32`` /
+``pg_spmm1_f32``) and torch GPU ops for the small dense gradient products. CPU tensors are rejected:
+there is no CPU implementation of the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import LayerArgs, check, default_flags, load_library
+from .graph import CSRGraph, ShapedAdjacency
+
+LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
+
+# Optional live timing of the propagation kernel: when set to a list, spmm3 appends one
+# (start, end) pair of HIP events recorded on the launch stream around each propagation launch.
+SPMM_EVENTS: Optional[list] = None
+
+
+def _ev_start(x):
+    if SPMM_EVENTS is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record(torch.cuda.current_stream(x.device))
+    return e0
+
+
+def _ev_end(x, e0):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream(x.device))
+        SPMM_EVENTS.append((e0, e1))
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("protgram_directgcn_amd runs on the MI355X only: got a CPU tensor "
+                               "(move the model and data to 'cuda'; there is no CPU fallback)")
+        if t.dtype not in (torch.float32, torch.int32, torch.int64):
+            raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _f32c(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+# raw kernel calls
+# ------------------------------------------------------------------------------------------------
+def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
+          flags: Optional[int] = None) -> torch.Tensor:
+    """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels."""
+    lib = load_library()
+    x = _f32c(x)
+    _require_gpu(x)
+    N, F = g.n_rows, x.size(1)
+    if x.size(0) < N:
+        raise ValueError("x has fewer rows than the graph")
+    Z = out if out is not None else torch.empty(N, 3 * F, device=x.device, dtype=torch.float32)
+    fl = default_flags() if flags is None else flags
+    s = _stream(x)
+    ev = _ev_start(x)
+    if g.shared:
+        if fused:
+            if g.raw is None:
+                raise ValueError("graph has no raw-count records (build it with build_propagation_csr)")
+            check(lib.pg_spmm3_fusednorm_f32(N, _p(g.rowptr), _p(g.raw), _p(g.node_norm), g.eps, _p(x),
+                                             x.stride(0), F, _p(Z), Z.stride(0), fl, s), "pg_spmm3_fusednorm_f32")
+        else:
+            check(lib.pg_spmm3_f32(N, _p(g.rowptr), _p(g.edges3), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s),
+                  "pg_spmm3_f32")
+    else:
+        for k, a in enumerate(g.adj):
+            check(lib.pg_spmm1_f32(N, _p(a.rowptr), _p(a.edges), _p(x), x.stride(0), F, _p(Z[:, k * F:]),
+                                   Z.stride(0), 0, fl, s), "pg_spmm1_f32")
+    _ev_end(x, ev)
+    return Z
+
+
+def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
+    """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3)."""
+    lib = load_library()
+    G = _f32c(G)
+    _require_gpu(G)
+    N, F = g.n_rows, G.size(1) // 3
+    dX = torch.empty(N, F, device=G.device, dtype=torch.float32)
+    fl = default_flags() if flags is None else flags
+    s = _stream(G)
+    if g.shared:
+        check(lib.pg_spmm3t_f32(N, _p(g.rowptr_t), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0, fl,
+                                s), "pg_spmm3t_f32")
+    else:
+        for k, a in enumerate(g.adj):
+            check(lib.pg_spmm1_f32(N, _p(a.rowptr_t), _p(a.edges_t), _p(G[:, k * F:]), G.stride(0), F, _p(dX),
+                                   dX.stride(0), 1 if k else 0, fl, s), "pg_spmm1_f32")
+    return dX
+
+
+def spmm1(a: ShapedAdjacency, x: torch.Tensor, transpose: bool = False, flags: Optional[int] = None) -> torch.Tensor:
+    lib = load_library()
+    x = _f32c(x)
+    _require_gpu(x)
+    N = a.rowptr.numel() - 1
+    Y = torch.empty(N, x.size(1), device=x.device, dtype=torch.float32)
+    rp, e = (a.rowptr_t, a.edges_t) if transpose else (a.rowptr, a.edges)
+    fl = default_flags() if flags is None else flags
+    check(lib.pg_spmm1_f32(N, _p(rp), _p(e), _p(x), x.stride(0), x.size(1), _p(Y), Y.stride(0), 0, fl, _stream(x)),
+          "pg_spmm1_f32")
+    return Y
+
+
+def edges_normalize(rc, eps: float) -> torch.Tensor:
+    """Precomputed {col, w_in, w_out, w_und} records from raw-count records, on the GPU."""
+    lib = load_library()
+    _require_gpu(rc.raw)
+    out = torch.empty_like(rc.raw)
+    check(lib.pg_edges_normalize_f32(rc.n, _p(rc.rowptr), _p(rc.raw), _p(rc.node_norm), eps, _p(out),
+                                     _stream(rc.raw)), "pg_edges_normalize_f32")
+    return out
+
+
+def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
+                act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
+    """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header)."""
+    lib = load_library()
+    _require_gpu(Z)
+    M, F_in = Z.size(0), Z.size(1) // 3
+    F_out = prm["W_main_in"].size(0)
+    Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
+    keep = []
+
+    def c(t):
+        if t is None:
+            return None
+        t = _f32c(t) if t.dtype != torch.int64 else t.contiguous()
+        keep.append(t)
+        return _p(t)
+
+    a = LayerArgs()
+    a.M, a.F_in, a.F_out = M, F_in, F_out
+    Zc = _f32c(Z)
+    a.Z, a.ldz = c(Zc), Zc.stride(0)
+    a.W_main_in, a.W_main_out = c(prm["W_main_in"]), c(prm["W_main_out"])
+    a.W_undirected, a.W_shared = c(prm["W_undirected"]), c(prm["W_shared"])
+    a.b_main_in, a.b_dir_shared_in = c(prm["b_main_in"]), c(prm["b_dir_shared_in"])
+    a.b_main_out, a.b_dir_shared_out = c(prm["b_main_out"]), c(prm["b_dir_shared_out"])
+    a.b_undirected, a.b_undirected_shared = c(prm["b_undirected"]), c(prm["b_undirected_shared"])
+    a.gate_mode = gate_mode
+    a.C_in, a.C_out, a.C_directed = c(prm["C_in"]), c(prm["C_out"]), c(prm["C_directed"])
+    a.C_undirected, a.C_all = c(prm["C_undirected"]), c(prm["C_all"])
+    a.rows = c(rows)
+    if constant is not None:
+        a.constant, a.ld_const = c(constant), constant.size(1)
+    if res_x is not None:
+        rx = _f32c(res_x)
+        keep.append(rx)
+        a.res_x, a.ld_res = _p(rx), rx.stride(0)
+    a.W_res, a.b_res = c(W_res), c(b_res)
+    a.act, a.slope = int(bool(act)), float(slope)
+    a.Y, a.ldy = _p(Y), Y.stride(0)
+    fl = default_flags() if flags is None else flags
+    check(lib.pg_directgcn_dense_f32(ctypes.byref(a), fl, _stream(Z)), "pg_directgcn_dense_f32")
+    return Y
+
+
+# ------------------------------------------------------------------------------------------------
+# autograd
+# ------------------------------------------------------------------------------------------------
+class Propagate3(torch.autograd.Function):
+    """x [N, F] -> Z [N, 3F] = [A_in x | A_out x | A_und x]; backward = transposed propagation."""
+
+    @staticmethod
+    def forward(ctx, x, g: CSRGraph, fused: bool = False):
+        ctx.g = g
+        return spmm3(g, x, fused=fused)
+
+    @staticmethod
+    def backward(ctx, dZ):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None
+        return spmm3_t(ctx.g, dZ), None, None
+
+
+class Propagate1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a: ShapedAdjacency):
+        ctx.a = a
+        return spmm1(a, x)
+
+    @staticmethod
+    def backward(ctx, dY):
+        return spmm1(ctx.a, dY, transpose=True), None
+
+
+_DENSE_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in", "b_dir_shared_in",
+               "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared",
+               "C_in", "C_out", "C_directed", "C_undirected", "C_all")
+
+
+class LayerDense(torch.autograd.Function):
+    """Y = act(sum_k s_k (Z_k W_k'^T + b_k') + constant[rows] + residual) (pg_directgcn_dense_f32).
+
+    Backward (GPU torch ops; dX of the propagation is handled by Propagate3):
+      G = dpre [W_in' | W_out' | W_und']  ->  dZ_k = s_k G_k,  ds_k = <G_k, Z_k> + <dpre, b_k'>
+      dW_k' = (s_k dpre)^T Z_k,  db_k' = sum_m s_k dpre,  and the chain rule through s_k(c)."""
+
+    @staticmethod
+    def forward(ctx, Z, res_x, constant, W_res, b_res, rows, gate_mode, act, slope, *params):
+        prm = dict(zip(_DENSE_KEYS, params))
+        Y = layer_dense(Z, prm, gate_mode, rows=rows, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
+                        act=act, slope=slope)
+        ctx.gate_mode, ctx.act, ctx.slope = gate_mode, act, slope
+        ctx.has_res, ctx.has_const = res_x is not None, constant is not None
+        ctx.save_for_backward(Z, res_x if res_x is not None else Z.new_empty(0),
+                              constant if constant is not None else Z.new_empty(0),
+                              W_res if W_res is not None else Z.new_empty(0),
+                              rows if rows is not None else Z.new_empty(0, dtype=torch.int64), Y, *params)
+        ctx.has_wres, ctx.has_rows = W_res is not None, rows is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        Z, res_x, constant, W_res, rows, Y, *params = ctx.saved_tensors
+        prm = dict(zip(_DENSE_KEYS, params))
+        res_x = res_x if ctx.has_res else None
+        constant = constant if ctx.has_const else None
+        W_res = W_res if ctx.has_wres else None
+        rows = rows if ctx.has_rows else None
+        M = Z.size(0)
+        F_in = Z.size(1) // 3
+        dpre = dY * torch.where(Y > 0, 1.0, ctx.slope) if ctx.act else dY
+
+        # gates
+        def gate(name):
+            v = prm[name]
+            if ctx.gate_mode == 1:
+                return v.reshape(1, 1).expand(M, 1)
+            idx = rows if rows is not None else None
+            return (v[idx] if idx is not None else v[:M]).reshape(M, 1)
+
+        ci, co, cd, cu, ca = (gate(k) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"))
+        cad = ca * cd
+        s = [cad * ci, cad * co, ca * cu]
+        Wp = [prm["W_main_in"] + prm["W_shared"], prm["W_main_out"] + prm["W_shared"],
+              prm["W_undirected"] + prm["W_shared"]]
+        bp = [prm["b_main_in"] + prm["b_dir_shared_in"], prm["b_main_out"] + prm["b_dir_shared_out"],
+              prm["b_undirected"] + prm["b_undirected_shared"]]
+        Zk = [Z[:, k * F_in:(k + 1) * F_in] for k in range(3)]
+        dZ = torch.empty_like(Z)
+        ds, dWp, dbp = [], [], []
+        for k in range(3):
+            Gk = dpre @ Wp[k]  # [M, F_in]
+            dZ[:, k * F_in:(k + 1) * F_in] = s[k] * Gk
+            ds.append((Gk * Zk[k]).sum(1, keepdim=True) + dpre @ bp[k].reshape(-1, 1))
+            sd = s[k] * dpre
+            dWp.append(sd.t() @ Zk[k])
+            dbp.append(sd.sum(0))
+        g = {}
+        g["W_main_in"], g["W_main_out"], g["W_undirected"] = dWp
+        g["W_shared"] = dWp[0] + dWp[1] + dWp[2]
+        g["b_main_in"] = g["b_dir_shared_in"] = dbp[0]
+        g["b_main_out"] = g["b_dir_shared_out"] = dbp[1]
+        g["b_undirected"] = g["b_undirected_shared"] = dbp[2]
+        dci = ds[0] * cad
+        dco = ds[1] * cad
+        dcd = ds[0] * ca * ci + ds[1] * ca * co
+        dcu = ds[2] * ca
+        dca = ds[0] * cd * ci + ds[1] * cd * co + ds[2] * cu
+        for name, dv in (("C_in", dci), ("C_out", dco), ("C_directed", dcd), ("C_undirected", dcu), ("C_all", dca)):
+            v = prm[name]
+            if ctx.gate_mode == 1:
+                g[name] = dv.sum().reshape(v.shape)
+            else:
+                full = torch.zeros_like(v)
+                if rows is not None:
+                    full.index_add_(0, rows, dv)
+                else:
+                    full[:M] += dv
+                g[name] = full
+        d_const = None
+        if constant is not None and ctx.needs_input_grad[2]:
+            d_const = torch.zeros_like(constant)
+            if rows is not None:
+                d_const.index_add_(0, rows, dpre)
+            else:
+                d_const[:M] += dpre
+        d_res = d_wres = d_bres = None
+        if res_x is not None:
+            if W_res is None:
+                d_res = dpre
+            else:
+                d_res = dpre @ W_res
+                d_wres = dpre.t() @ res_x
+                d_bres = dpre.sum(0)
+        grads = [g[k] if ctx.needs_input_grad[9 + i] else None for i, k in enumerate(_DENSE_KEYS)]
+        return (dZ, d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)

@@ -1,0 +1,254 @@
+"""GPU parity: the HIP path (through the C-ABI library) against the oracle and the reference's golden
+vectors. Tolerances:
+  * propagation kernels (pg_spmm3/pg_spmm1/fused-norm): BIT-EXACT vs the oracle's propagate(), which
+    is the reference's index_select -> mul -> scatter_add_ (same operation order, see pg_spmm.hip)
+  * GPU-built weights (pg_edges_normalize_f32): bit-exact vs the IEEE closed form; <= 1 ulp vs the
+    reference matrices (torch CPU sqrt is MKL's, not correctly rounded; tests/test_host.py)
+  * layer / model outputs and gradients (reassociated A(xW) = (Ax)W + MFMA accumulation order):
+    |d| <= 1e-5 + 1e-5*|ref| elementwise (BASELINE.json north_star: fp32 within 1e-5)
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import graph, load, params, t
+from oracle import directgcn_cpu as oc
+from oracle import graph_cpu as og
+
+pytestmark = pytest.mark.gpu
+RTOL = ATOL = 1e-5
+FLAG_VARIANTS = [0, 1, 2, 4, 6]  # default, no XCD remap, LDS edge staging, unroll 4, LDS+unroll4
+
+
+def assert_close(got, ref, what, rtol=RTOL, atol=ATOL):
+    got = got.detach().float().cpu()
+    ref = torch.as_tensor(ref).float()
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    err = (got - ref).abs()
+    bad = err > atol + rtol * ref.abs()
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} elements out of tolerance, max |d| {err.max().item():.3e}"
+
+
+def dev_graph(ei, ew, dev):
+    return ({k: v.to(dev) for k, v in ei.items()}, {k: (v.to(dev) if v is not None else None) for k, v in ew.items()})
+
+
+# ---------------------------------------------------------------------------------------------
+# propagation kernels
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,F", [("f1_fasta2", 32), ("f1_debruijn2", 128), ("f2_edge", 16), ("f5_fasta3", 64),
+                                    ("f5_fasta3", 256), ("f3_bench", 48), ("f2_empty", 8), ("f4_cluster", 20)])
+def test_spmm3_bitexact(pkg, cuda, name, F):
+    from protgram_directgcn_amd import ops
+    fx = load(name)
+    ei, ew = graph(fx)
+    N = int(fx["N"][0]) if name != "f4_cluster" else int(fx["subset"].size)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(3))
+    ref = [oc.propagate(ei[k], x, ew[k]) for k in ("in", "out", "und")]
+    dei, dew = dev_graph(ei, ew, cuda)
+    g = pkg.graph.csr_from_coo(N, dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"])
+    for fl in FLAG_VARIANTS:
+        Z = ops.spmm3(g, x.to(cuda), flags=fl).cpu()
+        for k in range(3):
+            assert torch.equal(Z[:, k * F:(k + 1) * F], ref[k]), (name, F, fl, k)
+
+
+@pytest.mark.parametrize("name", ["f1_fasta2", "f1_debruijn2", "f2_edge", "f5_fasta3", "f6_pe1"])
+def test_gpu_weights_and_fusednorm(pkg, cuda, name):
+    """GPU-built propagation weights and the fused-normalisation SpMM."""
+    from protgram_directgcn_amd import ops
+    fx = load(name)
+    N = int(fx["N"][0])
+    g = pkg.build_propagation_csr(N, fx["src"], fx["dst"], fx["cnt"], device=cuda)
+    e = g.edges3.cpu().numpy()
+    rows = np.repeat(np.arange(N), np.diff(g.rowptr.cpu().numpy()))
+    key = e[:, 0].astype(np.int64) * N + rows
+    order = np.argsort(key)
+    for j, k in enumerate(("in", "out", "und")):
+        idx = fx[f"{k}_idx"]
+        np.testing.assert_array_equal(key[order], idx[0] * N + idx[1])
+        ulp = np.abs(e[order, 1 + j].astype(np.int64) - fx[f"{k}_val"].view(np.int32).astype(np.int64))
+        assert ulp.max() <= (0 if k == "und" else 1), (k, ulp.max())
+    # fused-norm SpMM == SpMM over the materialised weights, bit for bit; == oracle on those weights
+    F = 32
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(4)).to(cuda)
+    for fl in FLAG_VARIANTS:
+        Z0 = ops.spmm3(g, x, flags=fl)
+        Z1 = ops.spmm3(g, x, fused=True, flags=fl)
+        assert torch.equal(Z0, Z1), fl
+    src_idx = torch.from_numpy(e[:, 0].astype(np.int64))
+    ei = torch.stack([src_idx, torch.from_numpy(rows)])
+    for j in range(3):
+        w = torch.from_numpy(e[:, 1 + j].copy().view(np.float32))
+        ref = oc.propagate(ei, x.cpu(), w)
+        assert torch.equal(Z0[:, j * F:(j + 1) * F].cpu(), ref)
+
+
+@pytest.mark.parametrize("name,F", [("f1_fasta2", 32), ("f3_bench", 16), ("f5_fasta3", 64)])
+def test_spmm3_transpose_matches_autograd(pkg, cuda, name, F):
+    from protgram_directgcn_amd import ops
+    fx = load(name)
+    ei, ew = graph(fx)
+    N = int(fx["N"][0])
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(5), requires_grad=True)
+    Gs = torch.randn(N, 3 * F, generator=torch.Generator().manual_seed(6))
+    Z = torch.cat([oc.propagate(ei[k], x, ew[k]) for k in ("in", "out", "und")], 1)
+    (Z * Gs).sum().backward()
+    dei, dew = dev_graph(ei, ew, cuda)
+    g = pkg.graph.csr_from_coo(N, dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"])
+    for fl in FLAG_VARIANTS:
+        dX = ops.spmm3_t(g, Gs.to(cuda), flags=fl)
+        assert_close(dX, x.grad, f"{name} dX flags={fl}", rtol=1e-6, atol=1e-6)
+
+
+def test_spmm_deterministic(pkg, cuda):
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, device=cuda)
+    Z0 = ops.spmm3(g, x)
+    for _ in range(3):
+        assert torch.equal(ops.spmm3(g, x), Z0)
+    G = torch.randn(N, 192, device=cuda)
+    assert torch.equal(ops.spmm3_t(g, G), ops.spmm3_t(g, G))
+
+
+# ---------------------------------------------------------------------------------------------
+# layer and model vs the reference's golden vectors
+# ---------------------------------------------------------------------------------------------
+def _layer_from_fixture(pkg, fx, tag, dev):
+    fin, fout, nn_, vec = (int(v) for v in fx[f"{tag}_cfg"])
+    layer = pkg.DirectGCNLayer(fin, fout, nn_, bool(vec))
+    layer.load_state_dict(params(fx, f"{tag}_p"))
+    return layer.to(dev)
+
+
+@pytest.mark.parametrize("name,tag", [("f1_fasta2", "L"), ("f1_debruijn2", "L"), ("f2_edge", "L"), ("f2_edge", "L2"),
+                                      ("f2_empty", "L"), ("f3_bench", "L"), ("f4_cluster", "L"), ("f4_cluster", "S"),
+                                      ("f4_cluster", "V"), ("f5_fasta3", "L")])
+def test_layer_forward_backward_vs_reference(pkg, cuda, name, tag):
+    fx = load(name)
+    ei, ew = graph(fx)
+    dei, dew = dev_graph(ei, ew, cuda)
+    layer = _layer_from_fixture(pkg, fx, tag, cuda)
+    x = t(fx[f"{tag}_x"]).to(cuda).requires_grad_(True)
+    orig = t(fx[f"{tag}_orig"]).to(cuda) if f"{tag}_orig" in fx else None
+    y = layer(x, dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"], orig)
+    assert_close(y, fx[f"{tag}_y"], f"{name}/{tag} y")
+    if f"{tag}_R" in fx:
+        (y * t(fx[f"{tag}_R"]).to(cuda)).sum().backward()
+        assert_close(x.grad, fx[f"{tag}_gx"], f"{name}/{tag} grad x")
+        for k, p in layer.named_parameters():
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            assert_close(g, fx[f"{tag}_g:{k}"], f"{name}/{tag} grad {k}", rtol=1e-4, atol=1e-5)
+
+
+def _model_from_fixture(pkg, fx, dev, prefix="M_p"):
+    cfg = fx["M_cfg"]
+    dims, (N, C, n, ogd) = [int(v) for v in cfg[:-4]], [int(v) for v in cfg[-4:]]
+    m = pkg.ProtGramDirectGCN(dims, N, C, n, ogd, 512, 0.5, True)
+    m.load_state_dict(params(fx, prefix))
+    return m.to(dev), dims, N, n, ogd
+
+
+@pytest.mark.parametrize("name", ["f1_fasta2", "f3_bench", "f6_pe1"])
+def test_model_forward_backward_vs_reference(pkg, cuda, name):
+    fx = load(name)
+    ei, ew = graph(fx)
+    dei, dew = dev_graph(ei, ew, cuda)
+    m, dims, N, n, ogd = _model_from_fixture(pkg, fx, cuda)
+    m.eval()
+    x = t(fx["M_x"]).to(cuda).requires_grad_(True)
+    data = pkg.Data(x=x, edge_index_in=dei["in"], edge_weight_in=dew["in"], edge_index_out=dei["out"],
+                    edge_weight_out=dew["out"], edge_index_undirected_norm=dei["und"],
+                    edge_weight_undirected_norm=dew["und"])
+    lp, emb = m(data)
+    assert_close(lp, fx["M_logp"], f"{name} log_probs")
+    assert_close(emb, fx["M_emb"], f"{name} embeddings")
+    ((lp * t(fx["M_R1"]).to(cuda)).sum() + (emb * t(fx["M_R2"]).to(cuda)).sum()).backward()
+    assert_close(x.grad, fx["M_gx"], f"{name} grad x", rtol=1e-4, atol=1e-5)
+    for k, p in m.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        assert_close(g, fx[f"M_g:{k}"], f"{name} grad {k}", rtol=1e-4, atol=1e-5)
+
+
+def test_training_steps_vs_reference(pkg, cuda):
+    """Two steps of the reference's full-batch loop (trainer :91-100; eval-mode dropout, see fixture)."""
+    import torch.nn.functional as F
+    fx = load("f1_fasta2")
+    ei, ew = graph(fx)
+    dei, dew = dev_graph(ei, ew, cuda)
+    m, dims, N, n, ogd = _model_from_fixture(pkg, fx, cuda)
+    m.eval()
+    data = pkg.Data(x=t(fx["M_x"]).to(cuda), edge_index_in=dei["in"], edge_weight_in=dew["in"],
+                    edge_index_out=dei["out"], edge_weight_out=dew["out"], edge_index_undirected_norm=dei["und"],
+                    edge_weight_undirected_norm=dew["und"])
+    y = t(fx["M_train_y"]).to(cuda)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=0.0)
+    losses = []
+    for _ in range(len(fx["M_train_loss"])):
+        opt.zero_grad()
+        out, _ = m(data=data)
+        loss = F.nll_loss(out, y) + 1e-7 * sum(p.norm(2).pow(2) for p in m.parameters() if p.requires_grad)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, fx["M_train_loss"], rtol=1e-5)
+    ref = params(fx, "M_train_p")
+    for k, v in m.state_dict().items():
+        assert_close(v, ref[k], f"param after 2 steps {k}", rtol=1e-4, atol=1e-5)
+
+
+def test_debruijn3_layer_samples(pkg, cuda):
+    fx = load("f5_debruijn3")
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    layer = pkg.DirectGCNLayer(64, 64, N, True)
+    layer.load_state_dict(params(fx, "L_p"))
+    layer = layer.to(cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    with torch.no_grad():
+        y = layer.fused_forward(x, g)
+        y_f = layer.fused_forward(x, g, fused_norm=True)
+    assert torch.equal(y, y_f)
+    assert_close(y[t(fx["L_rows"]).to(cuda)], fx["L_y_rows"], "3-gram sampled rows")
+    np.testing.assert_allclose(y.double().sum(0).cpu().numpy(), fx["L_colsum"], rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,F", [(4, 128)])
+def test_full_size_4gram_layer_vs_oracle(pkg, cuda, n, F):
+    """BASELINE config size (4-gram, F=128): full forward vs the oracle on the same inputs, plus
+    size-independent properties (linearity of the propagation, CSR-vs-fused identity)."""
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    torch.manual_seed(0)
+    layer = pkg.DirectGCNLayer(F, F, N, True)
+    with torch.no_grad():
+        for name, p in layer.named_parameters():
+            if name.startswith("C_"):
+                p.uniform_(0.5, 1.5)
+            elif "bias" in name:
+                p.uniform_(-0.1, 0.1)
+    layer = layer.to(cuda)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(1234))
+    xd = x.to(cuda)
+    with torch.no_grad():
+        y = layer.fused_forward(xd, g)
+        a, b = torch.randn(2).tolist()
+        x2 = torch.randn(N, F, device=cuda)
+        Z1, Z2 = ops.spmm3(g, xd), ops.spmm3(g, x2)
+        Z12 = ops.spmm3(g, a * xd + b * x2)
+        assert_close(Z12, a * Z1 + b * Z2, "linearity", rtol=1e-4, atol=1e-4)
+    # oracle on the reference-order matrices rebuilt from our (GPU) weights: equal up to sqrt ulps
+    e = g.edges3.cpu().numpy()
+    rows = torch.from_numpy(np.repeat(np.arange(N), np.diff(g.rowptr.cpu().numpy())))
+    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
+    w = [torch.from_numpy(e[:, 1 + j].copy().view(np.float32)) for j in range(3)]
+    p = {k: v.detach().cpu() for k, v in layer.state_dict().items()}
+    with torch.no_grad():
+        y_ref = oc.layer_forward(p, x, ei, w[0], ei, w[1], ei, w[2])
+    assert_close(y, y_ref, "4-gram layer")
+    Z = ops.spmm3(g, xd)
+    for j in range(3):
+        assert torch.equal(Z[:, j * F:(j + 1) * F].cpu(), oc.propagate(ei, x, w[j])), j

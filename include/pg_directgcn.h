@@ -140,7 +140,18 @@ typedef struct pg_layer_args {
     float* Y; int64_t ldy;
 } pg_layer_args_t;
 
-int pg_directgcn_dense_f32(const pg_layer_args_t* args, uint32_t flags, void* stream);
+/* Number of floats of the packed operand: B = [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] as [F_out, K]
+ * (K = 3*F_in, or 4*F_in with a projected residual) followed by the bias sums [4, F_out]
+ * (b_main_k + b_shared_k for k = in, out, und; then b_res or 0). */
+int64_t pg_directgcn_packed_floats(int64_t F_in, int64_t F_out, int has_res_proj);
+
+/* Pack the weights/biases named in `args` (W_*, b_*, W_res, b_res) into `packed` (device memory of
+ * pg_directgcn_packed_floats() floats). Re-run only when the parameters change. */
+int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stream);
+
+/* The contraction + epilogue. Reads weights/biases from `packed` (the W_* / b_* fields of args are not
+ * read); W_res != NULL selects the projected residual. */
+int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

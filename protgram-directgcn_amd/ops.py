@@ -136,11 +136,47 @@ def edges_normalize(rc, eps: float) -> torch.Tensor:
     return out
 
 
+_PACK_CACHE: dict = {}
+
+
+def _version_key(ts):
+    return tuple(None if t is None else (t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
+
+
+def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
+    """pg_directgcn_pack_f32: [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] + bias sums, cached while the
+    parameters are unchanged (keyed on storage pointer + in-place version counter)."""
+    srcs = [prm[k] for k in _PACK_KEYS] + [W_res, b_res]
+    key = _version_key(srcs)
+    hit = _PACK_CACHE.get(key)
+    if hit is not None:
+        return hit
+    lib = load_library()
+    F_out, F_in = prm["W_main_in"].shape
+    n = lib.pg_directgcn_packed_floats(F_in, F_out, 1 if W_res is not None else 0)
+    out = torch.empty(n, device=prm["W_main_in"].device, dtype=torch.float32)
+    keep = [_f32c(t.detach()) if t is not None else None for t in srcs]
+    a = LayerArgs()
+    a.F_in, a.F_out = F_in, F_out
+    (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
+     a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared, a.W_res, a.b_res) = [_p(t) for t in keep]
+    check(lib.pg_directgcn_pack_f32(ctypes.byref(a), _p(out), _stream(out)), "pg_directgcn_pack_f32")
+    if len(_PACK_CACHE) >= 32:
+        _PACK_CACHE.pop(next(iter(_PACK_CACHE)))
+    _PACK_CACHE[key] = out
+    return out
+
+
+_PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in", "b_dir_shared_in",
+              "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared")
+
+
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
                 act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
     """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header)."""
     lib = load_library()
     _require_gpu(Z)
+    packed = pack_weights(prm, W_res, b_res)
     M, F_in = Z.size(0), Z.size(1) // 3
     F_out = prm["W_main_in"].size(0)
     Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
@@ -149,7 +185,7 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     def c(t):
         if t is None:
             return None
-        t = _f32c(t) if t.dtype != torch.int64 else t.contiguous()
+        t = _f32c(t.detach()) if t.dtype != torch.int64 else t.contiguous()
         keep.append(t)
         return _p(t)
 
@@ -157,11 +193,6 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     a.M, a.F_in, a.F_out = M, F_in, F_out
     Zc = _f32c(Z)
     a.Z, a.ldz = c(Zc), Zc.stride(0)
-    a.W_main_in, a.W_main_out = c(prm["W_main_in"]), c(prm["W_main_out"])
-    a.W_undirected, a.W_shared = c(prm["W_undirected"]), c(prm["W_shared"])
-    a.b_main_in, a.b_dir_shared_in = c(prm["b_main_in"]), c(prm["b_dir_shared_in"])
-    a.b_main_out, a.b_dir_shared_out = c(prm["b_main_out"]), c(prm["b_dir_shared_out"])
-    a.b_undirected, a.b_undirected_shared = c(prm["b_undirected"]), c(prm["b_undirected_shared"])
     a.gate_mode = gate_mode
     a.C_in, a.C_out, a.C_directed = c(prm["C_in"]), c(prm["C_out"]), c(prm["C_directed"])
     a.C_undirected, a.C_all = c(prm["C_undirected"]), c(prm["C_all"])
@@ -169,14 +200,14 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     if constant is not None:
         a.constant, a.ld_const = c(constant), constant.size(1)
     if res_x is not None:
-        rx = _f32c(res_x)
+        rx = _f32c(res_x.detach())
         keep.append(rx)
         a.res_x, a.ld_res = _p(rx), rx.stride(0)
-    a.W_res, a.b_res = c(W_res), c(b_res)
+    a.W_res = c(W_res)
     a.act, a.slope = int(bool(act)), float(slope)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
-    check(lib.pg_directgcn_dense_f32(ctypes.byref(a), fl, _stream(Z)), "pg_directgcn_dense_f32")
+    check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
     return Y
 
 

@@ -16,7 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_header_symbol(pkg):
     lib = pkg.load_library()
     hdr = open(os.path.join(REPO, "include", "pg_directgcn.h")).read()
-    names = set(re.findall(r"^\s*(?:int|const char\*)\s+(pg_\w+)\s*\(", hdr, re.M))
+    names = set(re.findall(r"^\s*(?:int64_t|int|const char\*)\s+(pg_\w+)\s*\(", hdr, re.M))
     assert {"pg_spmm3_f32", "pg_spmm3_fusednorm_f32", "pg_spmm3t_f32", "pg_spmm1_f32",
             "pg_directgcn_dense_f32", "pg_edges_normalize_f32", "pg_last_error", "pg_abi_version"} <= names
     for n in names:

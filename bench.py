@@ -241,7 +241,12 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
 
     Fd = x.size(1)
     B = g.algorithmic_bytes(Fd)
-    for fl, name in ((0, "default"), (1, "no_xcd_remap"), (2, "edge_lds"), (4, "unroll4"), (6, "edge_lds+unroll4")):
+    import dataclasses
+    g0 = dataclasses.replace(g, row_order=None)
+    for fl, name in ((0, "nosched"), (4, "nosched_unroll4"), (6, "nosched_lds_unroll4")):
+        ms = timeit(lambda: ops.spmm3(g0, x, flags=fl))
+        res[f"spmm3_{name}_ms"] = round(ms, 4)
+    for fl, name in ((0, "default"), (1, "no_xcd_remap"), (4, "unroll4"), (5, "unroll4_no_xcd_remap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)

@@ -71,6 +71,12 @@ typedef struct pg_edge1 {
 #define PG_FLAG_EDGE_LDS (1u << 1)     /* stage edge records through LDS (variant B) */
 #define PG_FLAG_UNROLL4 (1u << 2)      /* 4 gathers in flight per lane instead of 8 */
 
+/* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
+ * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
+ * only the schedule -- which rows run concurrently on one XCD and share its L2 -- never the result.
+ * The n-gram builder orders rows by (min out-neighbour, min in-neighbour), which groups the rows that
+ * share their out-neighbour set (same (n-1)-suffix) and in-neighbour set (same (n-1)-prefix). */
+
 const char* pg_last_error(void);
 int pg_abi_version(void);
 
@@ -78,14 +84,15 @@ int pg_abi_version(void);
  * over row i of the shared pattern. One pass: each X row gathered once per pattern entry.
  * Replaces the 3 x 2 propagate calls of protgram_directgcn.py:101-112 (aggregate-then-transform).
  * Requirements: ldx >= F, ldz >= 3F, n_rows rows in rowptr (n_rows+1 entries), col < rows(X). */
-int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges,
+int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
                  const float* X, int64_t ldx, int64_t F,
                  float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Same output as pg_spmm3_f32, with the three propagation weights computed in-kernel from raw counts
  * (graph_utils.py:198-273 closed form; bit-exact to the reference's torch.sparse construction) and
  * the per-node terms `node_norm` ([n_nodes, 4] as described above). eps = GCN_PROPAGATION_EPSILON. */
-int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* edges,
+int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order,
+                           const pg_edgeraw_t* edges,
                            const float* node_norm, float eps,
                            const float* X, int64_t ldx, int64_t F,
                            float* Z, int64_t ldz, uint32_t flags, void* stream);
@@ -98,13 +105,13 @@ int pg_edges_normalize_f32(int64_t n_rows, const int64_t* rowptr, const pg_edger
  * w_k * G[col, kF:(k+1)F]. `edges` is the CSR of the TRANSPOSED pattern (keyed by source), or the
  * forward CSR itself when all three matrices are symmetric (n-gram graphs: SURVEY §8a A10).
  * If accumulate != 0, dX += result. */
-int pg_spmm3t_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges,
+int pg_spmm3t_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
                   const float* G, int64_t ldg, int64_t F,
                   float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Single adjacency: Y[i, :] (+)= sum_e w * X[col, :]. Used for non-shared patterns (one call per
  * adjacency writing its column block of Z) and their transposes. */
-int pg_spmm1_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge1_t* edges,
+int pg_spmm1_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge1_t* edges,
                  const float* X, int64_t ldx, int64_t F,
                  float* Y, int64_t ldy, int accumulate, uint32_t flags, void* stream);
 

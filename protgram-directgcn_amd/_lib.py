@@ -45,12 +45,14 @@ class LayerArgs(ctypes.Structure):
 SIGNATURES = {
     "pg_last_error": (ctypes.c_char_p, []),
     "pg_abi_version": (ctypes.c_int, []),
-    "pg_spmm3_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
-    "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
+    "pg_spmm3_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
                                               c_u32, c_vp]),
     "pg_edges_normalize_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp]),
-    "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32, c_vp]),
-    "pg_spmm1_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32, c_vp]),
+    "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
+                                     c_vp]),
+    "pg_spmm1_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
+                                    c_vp]),
     "pg_directgcn_packed_floats": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "pg_directgcn_pack_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp]),
     "pg_directgcn_dense_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_u32, c_vp]),

@@ -42,6 +42,7 @@ struct DenseP {
     const float* res_x;
     int64_t ld_res;
     int proj_res;  // residual is the 4th K segment (+ b_res in bsum row 3)
+    int vec_out;   // float4 epilogue (F_out, ldy, ld_const, ld_res multiples of 4; 16-B aligned)
     int act;
     float slope;
     float* Y;
@@ -70,9 +71,14 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
     constexpr int A_F4 = BM * BK / 4 / 256;
     constexpr int B_F4 = BN * BK / 4 / 256;
 
-    __shared__ __attribute__((aligned(16))) float As[2][BM * LDSW];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDSW];
-    __shared__ float Sg[BM * 4];
+    constexpr int TLD = BN + 4;  // epilogue tile row (floats), 16-B aligned, conflict-free float4 reads
+    constexpr int MAIN_FLOATS = 2 * BM * LDSW + 2 * BN * LDSW;
+    constexpr int SMEM_FLOATS = MAIN_FLOATS > BM * TLD ? MAIN_FLOATS : BM * TLD;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM_FLOATS];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ int64_t Crow[BM];  // constant row per tile row (original_indices), -1 past M
+    float (*As)[BM * LDSW] = reinterpret_cast<float (*)[BM * LDSW]>(smem);
+    float (*Bs)[BN * LDSW] = reinterpret_cast<float (*)[BN * LDSW]>(smem + 2 * BM * LDSW);
 
     const int64_t n_mblk = (p.M + BM - 1) / BM;
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
@@ -98,6 +104,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
         Sg[tid * 4 + 1] = s1;
         Sg[tid * 4 + 2] = s2;
         Sg[tid * 4 + 3] = 1.f;
+        Crow[tid] = m < p.M ? (p.rows ? p.rows[m] : m) : -1;
     }
     __syncthreads();
 
@@ -207,31 +214,97 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
         __syncthreads();
     }
 
-    // Epilogue. C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-    const bool full_rows = m0 + BM <= p.M;
-    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
-    const bool id_res = p.res_x && !p.proj_res;
+    // Epilogue: park the accumulator tile in LDS (C/D map of the 32x32 MFMA: col = lane&31,
+    // row = (r&3) + 8*(r>>2) + 4*(lane>>5)), then sweep it row-major with float4 per thread so the
+    // constant / residual loads and the Y stores are 16-B coalesced, all loads of a batch in flight.
+    float* T = smem;  // the K loop ended with a barrier: the staging buffers are free
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * TN * 32 + j * 32 + li;
-        const bool ncol = n < p.F_out;
-        const int nn = ncol ? n : 0;
-        const float b0 = p.bsum[nn], b1 = p.bsum[p.F_out + nn], b2 = p.bsum[2 * p.F_out + nn];
-        const float br = p.proj_res ? p.bsum[3 * p.F_out + nn] : 0.f;
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int rl = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const int64_t m = m0 + rl;
-                if (!ncol || (!full_rows && m >= p.M)) continue;
-                const float* sg = &Sg[rl * 4];
-                float v = acc[i][j][r] + (sg[0] * b0 + sg[1] * b1 + sg[2] * b2) + br;
-                if (has_const) v += p.constant[(p.rows ? p.rows[m] : m) * p.ld_const + n];
-                if (id_res) v += p.res_x[m * p.ld_res + n];
-                if (p.act) v = v > 0.f ? v : v * p.slope;
-                p.Y[m * p.ldy + n] = v;
+                T[rl * TLD + wn * TN * 32 + j * 32 + li] = acc[i][j][r];
             }
+    __syncthreads();
+
+    constexpr int C4 = BN / 4;            // float4 per tile row
+    constexpr int ITER = BM * C4 / 256;   // float4 per thread
+    constexpr int BATCH = 4;
+    const int c4 = tid % C4;              // fixed column group per thread
+    const int nb = n0 + 4 * c4;
+    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
+    const bool id_res = p.res_x && !p.proj_res;
+    const bool vec_out = p.vec_out;
+    float4 b[3], br = make_float4(0.f, 0.f, 0.f, 0.f);
+    {
+        auto ldb = [&](const float* v) {
+            float4 o;
+            o.x = nb + 0 < p.F_out ? v[nb + 0] : 0.f;
+            o.y = nb + 1 < p.F_out ? v[nb + 1] : 0.f;
+            o.z = nb + 2 < p.F_out ? v[nb + 2] : 0.f;
+            o.w = nb + 3 < p.F_out ? v[nb + 3] : 0.f;
+            return o;
+        };
+        b[0] = ldb(p.bsum);
+        b[1] = ldb(p.bsum + p.F_out);
+        b[2] = ldb(p.bsum + 2 * p.F_out);
+        if (p.proj_res) br = ldb(p.bsum + 3 * p.F_out);
+    }
+    for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+        float4 cv[BATCH], rv[BATCH];
+        int rl[BATCH];
+        int64_t mm[BATCH];
+        bool ok[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            rl[u] = (tid + 256 * (it0 + u)) / C4;
+            mm[u] = m0 + rl[u];
+            ok[u] = Crow[rl[u]] >= 0 && nb < p.F_out;
+            cv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ok[u] && vec_out) {
+                if (has_const) cv[u] = ld4(p.constant + Crow[rl[u]] * p.ld_const + nb);
+                if (id_res) rv[u] = ld4(p.res_x + mm[u] * p.ld_res + nb);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            if (!ok[u]) continue;
+            const float* sg = &Sg[rl[u] * 4];
+            float4 v = ld4(&T[rl[u] * TLD + 4 * c4]);
+            float o[4] = {v.x, v.y, v.z, v.w};
+            const float bb0[4] = {b[0].x, b[0].y, b[0].z, b[0].w};
+            const float bb1[4] = {b[1].x, b[1].y, b[1].z, b[1].w};
+            const float bb2[4] = {b[2].x, b[2].y, b[2].z, b[2].w};
+            const float bbr[4] = {br.x, br.y, br.z, br.w};
+            float cc[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
+            float rr[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+            if (!vec_out) {  // ragged / unaligned output: element loads with column bounds
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int n = nb + e;
+                    if (n < p.F_out) {
+                        if (has_const) cc[e] = p.constant[Crow[rl[u]] * p.ld_const + n];
+                        if (id_res) rr[e] = p.res_x[mm[u] * p.ld_res + n];
+                    }
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float y = o[e] + (sg[0] * bb0[e] + sg[1] * bb1[e] + sg[2] * bb2[e]) + bbr[e] + cc[e] + rr[e];
+                if (p.act) y = y > 0.f ? y : y * p.slope;
+                o[e] = y;
+            }
+            if (vec_out) {
+                *reinterpret_cast<float4*>(p.Y + mm[u] * p.ldy + nb) = make_float4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (nb + e < p.F_out) p.Y[mm[u] * p.ldy + nb + e] = o[e];
+            }
+        }
     }
 }
 
@@ -328,6 +401,9 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.Y = a->Y;
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    p.vec_out = (a->F_out % 4 == 0) && (a->ldy % 4 == 0) && pg::aligned16(a->Y) &&
+                (!a->constant || (a->ld_const % 4 == 0 && pg::aligned16(a->constant))) &&
+                (!a->res_x || a->W_res || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)));
     bool vec = (a->F_in % 4 == 0) && (a->ldz % 4 == 0) && pg::aligned16(a->Z) && pg::aligned16(packed);
     if (a->res_x) vec = vec && pg::aligned16(a->res_x) && (a->ld_res % 4 == 0);
     const bool wide = a->F_out > 64;

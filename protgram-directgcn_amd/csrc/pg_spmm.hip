@@ -24,6 +24,7 @@ enum : int { M3 = 0, M3RAW = 1, M3T = 2, M1 = 3 };
 struct SpmmParams {
     int64_t n_rows;
     const int64_t* rowptr;
+    const int32_t* row_order;  // processing position -> row (NULL = identity)
     const void* edges;
     const float* X;
     int64_t ldx;
@@ -105,8 +106,9 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
     const int64_t row0 = lb * RPB;
     const int grp = threadIdx.x / LPR;
     const int t = threadIdx.x % LPR;
-    const int64_t row = row0 + grp;
-    const bool live = row < p.n_rows;
+    const int64_t pos = row0 + grp;
+    const bool live = pos < p.n_rows;
+    const int64_t row = (live && p.row_order) ? (int64_t)p.row_order[pos] : pos;
 
     const R* __restrict__ E = reinterpret_cast<const R*>(p.edges);
     const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.X);
@@ -243,9 +245,10 @@ __global__ __launch_bounds__(256) void spmm_scalar_kernel(SpmmParams p) {
     constexpr int NACC = Shape<MODE>::NACC;
     constexpr int NSLICE = Shape<MODE>::NSLICE;
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
-    const int64_t row = lb * 4 + threadIdx.x / 64;
+    const int64_t pos = lb * 4 + threadIdx.x / 64;
     const int lane = threadIdx.x % 64;
-    if (row >= p.n_rows) return;
+    if (pos >= p.n_rows) return;
+    const int64_t row = p.row_order ? (int64_t)p.row_order[pos] : pos;
     const R* __restrict__ E = reinterpret_cast<const R*>(p.edges);
     const int64_t beg = p.rowptr[row], end = p.rowptr[row + 1];
     float4 ni = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(256) void spmm_scalar_kernel(SpmmParams p) {
 // Materialise precomputed weights from raw records (pg_edges_normalize_f32): one thread per entry.
 __global__ __launch_bounds__(256) void normalize_kernel(int64_t n_rows, const int64_t* rowptr, const int4* raw,
                                                         const float4* node_norm, float eps, int4* out) {
-    const int64_t row = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const int64_t row = (int64_t)blockIdx.x * 4 + threadIdx.x / 64;  // CSR order (no schedule needed)
     if (row >= n_rows) return;
     const float4 ni = node_norm[row];
     for (int64_t e = rowptr[row] + (threadIdx.x % 64); e < rowptr[row + 1]; e += 64) {
@@ -310,7 +313,7 @@ void launch_vec(const SpmmParams& p, hipStream_t s) {
 
 template <int MODE, int LPR, int NV>
 void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
-    const bool lds = flags & PG_FLAG_EDGE_LDS;
+    const bool lds = (flags & PG_FLAG_EDGE_LDS) && p.row_order == nullptr;  // staging needs contiguous rows
     const bool u4 = flags & PG_FLAG_UNROLL4;
     if (lds) {
         if (u4) launch_vec<MODE, LPR, NV, 4, true>(p, s);
@@ -361,37 +364,40 @@ int common_checks(int64_t n_rows, const int64_t* rowptr, const void* edges, cons
 
 extern "C" {
 
-int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, const float* X, int64_t ldx,
-                 int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream) {
+int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                 const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream) {
     int rc = common_checks(n_rows, rowptr, edges, X, ldx, F, Z, ldz, 3 * F, F);
     if (rc) return rc;
-    SpmmParams p{n_rows, rowptr, edges, X, ldx, Z, ldz, nullptr, 0.f, (int)F, 0, 1};
+    SpmmParams p{n_rows, rowptr, row_order, edges, X, ldx, Z, ldz, nullptr, 0.f, (int)F, 0, 1};
     return dispatch<M3>(p, flags, (hipStream_t)stream, "pg_spmm3_f32");
 }
 
-int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* edges, const float* node_norm,
-                           float eps, const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, uint32_t flags,
-                           void* stream) {
+int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edgeraw_t* edges,
+                           const float* node_norm, float eps, const float* X, int64_t ldx, int64_t F, float* Z,
+                           int64_t ldz, uint32_t flags, void* stream) {
     int rc = common_checks(n_rows, rowptr, edges, X, ldx, F, Z, ldz, 3 * F, F);
     if (rc) return rc;
     PG_REQUIRE(n_rows == 0 || (node_norm && pg::aligned16(node_norm)), "node_norm must be 16-byte aligned [n,4]");
-    SpmmParams p{n_rows, rowptr, edges, X, ldx, Z, ldz, reinterpret_cast<const float4*>(node_norm), eps, (int)F, 0, 1};
+    SpmmParams p{n_rows, rowptr, row_order, edges, X, ldx, Z, ldz, reinterpret_cast<const float4*>(node_norm), eps,
+                 (int)F, 0, 1};
     return dispatch<M3RAW>(p, flags, (hipStream_t)stream, "pg_spmm3_fusednorm_f32");
 }
 
-int pg_spmm3t_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, const float* G, int64_t ldg,
-                  int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+int pg_spmm3t_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                  const float* G, int64_t ldg, int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags,
+                  void* stream) {
     int rc = common_checks(n_rows, rowptr, edges, G, ldg, F, dX, lddx, F, 3 * F);
     if (rc) return rc;
-    SpmmParams p{n_rows, rowptr, edges, G, ldg, dX, lddx, nullptr, 0.f, (int)F, accumulate ? 1 : 0, 1};
+    SpmmParams p{n_rows, rowptr, row_order, edges, G, ldg, dX, lddx, nullptr, 0.f, (int)F, accumulate ? 1 : 0, 1};
     return dispatch<M3T>(p, flags, (hipStream_t)stream, "pg_spmm3t_f32");
 }
 
-int pg_spmm1_f32(int64_t n_rows, const int64_t* rowptr, const pg_edge1_t* edges, const float* X, int64_t ldx,
-                 int64_t F, float* Y, int64_t ldy, int accumulate, uint32_t flags, void* stream) {
+int pg_spmm1_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge1_t* edges,
+                 const float* X, int64_t ldx, int64_t F, float* Y, int64_t ldy, int accumulate, uint32_t flags,
+                 void* stream) {
     int rc = common_checks(n_rows, rowptr, edges, X, ldx, F, Y, ldy, F, F);
     if (rc) return rc;
-    SpmmParams p{n_rows, rowptr, edges, X, ldx, Y, ldy, nullptr, 0.f, (int)F, accumulate ? 1 : 0, 1};
+    SpmmParams p{n_rows, rowptr, row_order, edges, X, ldx, Y, ldy, nullptr, 0.f, (int)F, accumulate ? 1 : 0, 1};
     return dispatch<M1>(p, flags, (hipStream_t)stream, "pg_spmm1_f32");
 }
 

@@ -57,6 +57,7 @@ class CSRGraph:
     node_norm: Optional[torch.Tensor] = None
     eps: float = 1e-9
     nnz: int = 0
+    row_order: Optional[torch.Tensor] = None  # int32 processing schedule of destination rows (None = 0..n-1)
 
     @property
     def device(self):
@@ -78,9 +79,11 @@ def _bits(w: torch.Tensor) -> torch.Tensor:
     return w.contiguous().to(torch.float32).view(torch.int32)
 
 
-def _sort_by(primary: torch.Tensor, secondary: torch.Tensor, n_secondary: int) -> torch.Tensor:
-    key = primary * max(n_secondary, 1) + secondary
-    return torch.sort(key, stable=True).indices
+def _sort_by(primary: torch.Tensor) -> torch.Tensor:
+    """Stable sort by row only: within a row the entries keep their COO order, which is the order in
+    which the reference's scatter_add_ accumulates them (so sums round identically). For a coalesced
+    COO this is ascending column order."""
+    return torch.sort(primary, stable=True).indices
 
 
 def _rowptr(rows: torch.Tensor, n: int) -> torch.Tensor:
@@ -106,9 +109,9 @@ def _single(ei: torch.Tensor, ew: Optional[torch.Tensor], n: int) -> ShapedAdjac
     w = torch.ones(src.numel(), dtype=torch.float32, device=ei.device) if ew is None else ew.reshape(-1)
     if w.numel() != src.numel():
         raise ValueError("edge_weight length does not match edge_index")
-    p = _sort_by(dst, src, n)
+    p = _sort_by(dst)
     e = torch.stack([src[p].to(torch.int32), _bits(w[p])], 1).contiguous()
-    pt = _sort_by(src, dst, n)
+    pt = _sort_by(src)
     et = torch.stack([dst[pt].to(torch.int32), _bits(w[pt])], 1).contiguous()
     return ShapedAdjacency(_rowptr(dst, n), e, _rowptr(src, n), et, int(src.numel()))
 
@@ -150,10 +153,10 @@ def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, ca
             return t.reshape(-1)
 
         wi, wo, wu = w(ew_in), w(ew_out), w(ew_und)
-        p = _sort_by(dst, src, n)
+        p = _sort_by(dst)
         edges3 = torch.stack([src[p].to(torch.int32), _bits(wi[p]), _bits(wo[p]), _bits(wu[p])], 1).contiguous()
         rowptr = _rowptr(dst, n)
-        pt = _sort_by(src, dst, n)
+        pt = _sort_by(src)
         edges3_t = torch.stack([dst[pt].to(torch.int32), _bits(wi[pt]), _bits(wo[pt]), _bits(wu[pt])], 1).contiguous()
         rowptr_t = _rowptr(src, n)
         sym = torch.equal(rowptr, rowptr_t) and torch.equal(edges3, edges3_t)
@@ -185,9 +188,27 @@ class RawNgramCSR:
     raw: torch.Tensor        # int32 [nnz, 4] {col, a_fwd, a_bwd, m_und}
     node_norm: torch.Tensor  # f32 [n, 4]
     nnz: int
+    row_order: Optional[torch.Tensor] = None
 
 
-def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu") -> RawNgramCSR:
+def locality_schedule(n: int, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """Row processing order that makes concurrently scheduled rows share neighbour rows in L2.
+
+    Key = (min out-neighbour, min in-neighbour). In an n-gram transition graph the out-neighbours of
+    s_1..s_n are s_2..s_n c (a function of the (n-1)-suffix) and the in-neighbours are c s_1..s_{n-1}
+    (a function of the prefix), so sorting by the key groups the rows with identical out-neighbour
+    sets, and consecutive groups share the middle s_2..s_{n-1}: a run of 400 rows then touches only
+    ~800 distinct feature rows (vs ~16,400 gathers). For graphs without that structure it is just a
+    deterministic permutation. Changes the schedule only, never the result."""
+    dev = src.device
+    big = torch.full((n,), n, dtype=torch.int64, device=dev)
+    min_out = big.clone().scatter_reduce_(0, src, dst, reduce="amin") if src.numel() else big.clone()
+    min_in = big.clone().scatter_reduce_(0, dst, src, reduce="amin") if src.numel() else big.clone()
+    key = min_out * (n + 1) + min_in
+    return torch.sort(key, stable=True).indices.to(torch.int32)
+
+
+def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu", schedule: bool = True) -> RawNgramCSR:
     """Shared pattern of (A u A^T u I) with raw counts, plus per-node normalisation terms.
 
     Integer work (pattern, grouping, sorting) runs with torch on ``device``; the O(n) float terms are
@@ -232,11 +253,12 @@ def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu") -> RawNgramCSR:
     r[np.isinf(r)] = 0
     nn_ = np.stack([dout_inv, din_inv, r, np.zeros(n, np.float32)], 1).astype(np.float32)
     node_norm = torch.from_numpy(np.ascontiguousarray(nn_)).to(dev)
-    return RawNgramCSR(n, rowptr, raw, node_norm, int(nnz))
+    order = locality_schedule(n, s, d) if schedule else None
+    return RawNgramCSR(n, rowptr, raw, node_norm, int(nnz), order)
 
 
 def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,
-                          keep_raw: bool = True) -> CSRGraph:
+                          keep_raw: bool = True, schedule: bool = True) -> CSRGraph:
     """Shared-pattern device CSR of (mathcal_A_in, mathcal_A_out, A_undirected_norm) from raw counts.
 
     Weights are materialised on the GPU by ``pg_edges_normalize_f32`` (bit-exact closed form of
@@ -246,8 +268,8 @@ def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: flo
     if int(num_nodes) > 0 and np.asarray(src).size == 0:
         raise ValueError("graph without transitions: its mathcal_A_in/out are empty while A_undirected_norm "
                          "holds self-loops (no shared pattern); use csr_from_coo on the reference matrices")
-    rc = ngram_raw_csr(num_nodes, src, dst, cnt, device=device)
+    rc = ngram_raw_csr(num_nodes, src, dst, cnt, device=device, schedule=schedule)
     edges3 = ops.edges_normalize(rc, eps)
     return CSRGraph(n_rows=rc.n, shared=True, rowptr=rc.rowptr, edges3=edges3, rowptr_t=rc.rowptr,
                     edges3_t=edges3, symmetric=True, raw=rc.raw if keep_raw else None,
-                    node_norm=rc.node_norm if keep_raw else None, eps=eps, nnz=rc.nnz)
+                    node_norm=rc.node_norm if keep_raw else None, eps=eps, nnz=rc.nnz, row_order=rc.row_order)

@@ -81,14 +81,14 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
         if fused:
             if g.raw is None:
                 raise ValueError("graph has no raw-count records (build it with build_propagation_csr)")
-            check(lib.pg_spmm3_fusednorm_f32(N, _p(g.rowptr), _p(g.raw), _p(g.node_norm), g.eps, _p(x),
+            check(lib.pg_spmm3_fusednorm_f32(N, _p(g.rowptr), _p(g.row_order), _p(g.raw), _p(g.node_norm), g.eps, _p(x),
                                              x.stride(0), F, _p(Z), Z.stride(0), fl, s), "pg_spmm3_fusednorm_f32")
         else:
-            check(lib.pg_spmm3_f32(N, _p(g.rowptr), _p(g.edges3), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s),
-                  "pg_spmm3_f32")
+            check(lib.pg_spmm3_f32(N, _p(g.rowptr), _p(g.row_order), _p(g.edges3), _p(x), x.stride(0), F, _p(Z),
+                                   Z.stride(0), fl, s), "pg_spmm3_f32")
     else:
         for k, a in enumerate(g.adj):
-            check(lib.pg_spmm1_f32(N, _p(a.rowptr), _p(a.edges), _p(x), x.stride(0), F, _p(Z[:, k * F:]),
+            check(lib.pg_spmm1_f32(N, _p(a.rowptr), None, _p(a.edges), _p(x), x.stride(0), F, _p(Z[:, k * F:]),
                                    Z.stride(0), 0, fl, s), "pg_spmm1_f32")
     _ev_end(x, ev)
     return Z
@@ -104,11 +104,12 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     fl = default_flags() if flags is None else flags
     s = _stream(G)
     if g.shared:
-        check(lib.pg_spmm3t_f32(N, _p(g.rowptr_t), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0, fl,
-                                s), "pg_spmm3t_f32")
+        ro = g.row_order if g.symmetric else None
+        check(lib.pg_spmm3t_f32(N, _p(g.rowptr_t), _p(ro), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,
+                                fl, s), "pg_spmm3t_f32")
     else:
         for k, a in enumerate(g.adj):
-            check(lib.pg_spmm1_f32(N, _p(a.rowptr_t), _p(a.edges_t), _p(G[:, k * F:]), G.stride(0), F, _p(dX),
+            check(lib.pg_spmm1_f32(N, _p(a.rowptr_t), None, _p(a.edges_t), _p(G[:, k * F:]), G.stride(0), F, _p(dX),
                                    dX.stride(0), 1 if k else 0, fl, s), "pg_spmm1_f32")
     return dX
 
@@ -121,8 +122,8 @@ def spmm1(a: ShapedAdjacency, x: torch.Tensor, transpose: bool = False, flags: O
     Y = torch.empty(N, x.size(1), device=x.device, dtype=torch.float32)
     rp, e = (a.rowptr_t, a.edges_t) if transpose else (a.rowptr, a.edges)
     fl = default_flags() if flags is None else flags
-    check(lib.pg_spmm1_f32(N, _p(rp), _p(e), _p(x), x.stride(0), x.size(1), _p(Y), Y.stride(0), 0, fl, _stream(x)),
-          "pg_spmm1_f32")
+    check(lib.pg_spmm1_f32(N, _p(rp), None, _p(e), _p(x), x.stride(0), x.size(1), _p(Y), Y.stride(0), 0, fl,
+                           _stream(x)), "pg_spmm1_f32")
     return Y
 
 

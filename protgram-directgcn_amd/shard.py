@@ -51,8 +51,12 @@ def partition(g: CSRGraph, rank: int, world: int) -> NodeRangePartition:
     r1 = min(n, r0 + per)
     rp = g.rowptr
     e0, e1 = int(rp[r0]), int(rp[r1])
+    order = None
+    if g.row_order is not None:  # keep the global schedule's relative order of the owned rows
+        ro = g.row_order.to(torch.int64)
+        order = (ro[(ro >= r0) & (ro < r1)] - r0).to(torch.int32)
     local = CSRGraph(n_rows=r1 - r0, shared=True, rowptr=(rp[r0:r1 + 1] - e0).contiguous(), edges3=g.edges3[e0:e1],
-                     rowptr_t=None, edges3_t=None, symmetric=False, nnz=e1 - e0)
+                     rowptr_t=None, edges3_t=None, symmetric=False, nnz=e1 - e0, row_order=order)
     rows = torch.arange(r0, r1, dtype=torch.int64, device=rp.device)
     return NodeRangePartition(rank, world, n, per, r0, r1, local, rows)
 

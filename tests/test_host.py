@@ -29,11 +29,11 @@ def test_library_exports_every_header_symbol(pkg):
 def test_abi_argument_errors_without_gpu(pkg):
     lib = pkg.load_library()
     # argument validation happens before any HIP call
-    rc = lib.pg_spmm3_f32(-1, None, None, None, 4, 4, None, 12, 0, None)
+    rc = lib.pg_spmm3_f32(-1, None, None, None, None, 4, 4, None, 12, 0, None)
     assert rc == -1 and b"n_rows" in lib.pg_last_error()
-    rc = lib.pg_spmm3_f32(10, None, None, None, 4, 4, None, 12, 0, None)
+    rc = lib.pg_spmm3_f32(10, None, None, None, None, 4, 4, None, 12, 0, None)
     assert rc == -1
-    rc = lib.pg_spmm3_f32(0, None, None, None, 4, 4, None, 8, 0, None)
+    rc = lib.pg_spmm3_f32(0, None, None, None, None, 4, 4, None, 8, 0, None)
     assert rc == -1 and b"ldz" in lib.pg_last_error()
 
 
@@ -76,6 +76,18 @@ def test_ngram_csr_closed_form_matches_reference_matrices(pkg, name):
         # closed form here (and in the HIP kernel) uses the correctly rounded sqrt.
         ulp = np.abs(w[k][order].view(np.int32).astype(np.int64) - fx[f"{k}_val"].view(np.int32).astype(np.int64))
         assert ulp.max() <= (0 if k == "und" else 1), (k, ulp.max())
+
+
+def test_locality_schedule_is_a_permutation_grouping_suffixes(pkg):
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    order = pkg.graph.locality_schedule(N, torch.from_numpy(s), torch.from_numpy(d)).long()
+    assert torch.equal(torch.sort(order).values, torch.arange(N))
+    # consecutive runs of 20 rows share their (n-1)-suffix (identical out-neighbour sets)
+    suffix = order % (20 ** 2)
+    assert bool((suffix.view(-1, 20) == suffix.view(-1, 20)[:, :1]).all())
+    # and runs of 400 rows share the middle letter
+    middle = (order // 20) % 20
+    assert bool((middle.view(-1, 400) == middle.view(-1, 400)[:, :1]).all())
 
 
 def test_debruijn_sizes_formula(pkg):

@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-layers", type=int, default=1)
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
+    ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     return ap.parse_args()
 
 
@@ -61,10 +63,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if args.one_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     def log(*a):
         if rank == 0:
@@ -256,10 +262,14 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     Z = ops.spmm3(g, x)
     conv = model.convs[0]
     prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
-    ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True))
     flops = 2 * x.size(0) * 3 * Fd * conv.out_channels
-    res["dense_ms"] = round(ms, 4)
-    res["dense_TFLOPs"] = round(flops / ms / 1e9, 2)
+    for fl, name in ((0, "dense"), (8, "dense_bm64"), (16, "dense_bm128")):
+        ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True, flags=fl))
+        res[f"{name}_ms"] = round(ms, 4)
+        res[f"{name}_TFLOPs"] = round(flops / ms / 1e9, 2)
+    dec = model.decoder_fc
+    res["head_ms"] = round(timeit(lambda: ops.head(x, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias,
+                                                   1e-12)), 4)
     G = torch.randn_like(Z)
     ms = timeit(lambda: ops.spmm3_t(g, G))
     res["spmm3t_ms"] = round(ms, 4)

@@ -70,6 +70,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_NO_XCD_REMAP (1u << 0) /* keep hardware blockIdx order instead of XCD-contiguous rows */
 #define PG_FLAG_EDGE_LDS (1u << 1)     /* stage edge records through LDS (variant B) */
 #define PG_FLAG_UNROLL4 (1u << 2)      /* 4 gathers in flight per lane instead of 8 */
+#define PG_FLAG_DENSE_BM64 (1u << 3)   /* dense kernel: force 64-row tiles */
+#define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -159,6 +161,14 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stre
 /* The contraction + epilogue. Reads weights/biases from `packed` (the W_* / b_* fields of args are not
  * read); W_res != NULL selects the projected residual. */
 int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
+
+/* Fused prediction head (protgram_directgcn.py:218-222, eval mode): per row m of h [M, F]
+ *   logp[m] = log_softmax(W2 relu(W1 h[m] + b1) + b2)      W1 [H, F], W2 [C, H] (nn.Linear layout)
+ *   emb[m]  = h[m] / (||h[m]||_2 + eps)                      (models_utils.py:139-147)
+ * One read of h; both products on fp32 MFMA for F <= 256, H <= 128, C <= 64, else a VALU kernel. */
+int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, int64_t ldh,
+                          const float* W1, const float* b1, const float* W2, const float* b2, float eps,
+                          float* logp, int64_t ldp, float* emb, int64_t lde, void* stream);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,8 @@ SIGNATURES = {
     "pg_directgcn_packed_floats": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "pg_directgcn_pack_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp]),
     "pg_directgcn_dense_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_u32, c_vp]),
+    "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                             c_vp, c_i64, c_vp, c_i64, c_vp]),
 }
 
 _lib = None

@@ -23,7 +23,6 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int LDSW = 36;  // padded LDS row (floats)
 
@@ -62,10 +61,11 @@ __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_
     return p.res_x[m * p.ld_res + (k - 3 * p.F_in)];
 }
 
-template <int BN, bool VEC>
+template <int BM, int BN, bool VEC>
 __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
-    constexpr int WN = (BN == 128) ? 2 : 1;
+    constexpr int WN = (BN == 128 || BM == 64) ? 2 : 1;
     constexpr int WM = 4 / WN;
+    static_assert(BM / WM >= 32 && BN / WN >= 32, "wave tile too small");
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
     constexpr int A_F4 = BM * BK / 4 / 256;
@@ -408,15 +408,28 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     if (a->res_x) vec = vec && pg::aligned16(a->res_x) && (a->ld_res % 4 == 0);
     const bool wide = a->F_out > 64;
     const int64_t BN = wide ? 128 : 64;
-    const int64_t nb = ((a->M + BM - 1) / BM) * ((a->F_out + BN - 1) / BN);
+    // BM=64 row tiles double the grid (fewer idle CUs in the last wave of blocks); BM=128 halves the
+    // B-tile re-reads. PG_FLAG_DENSE_BM64 / PG_FLAG_DENSE_BM128 force one; default picks by grid size.
+    const int64_t nb128 = ((a->M + 127) / 128) * ((a->F_out + BN - 1) / BN);
+    bool bm64 = nb128 < 4 * 512;
+    if (flags & PG_FLAG_DENSE_BM64) bm64 = true;
+    if (flags & PG_FLAG_DENSE_BM128) bm64 = false;
+    const int64_t BMv = bm64 ? 64 : 128;
+    const int64_t nb = ((a->M + BMv - 1) / BMv) * ((a->F_out + BN - 1) / BN);
     hipStream_t s = (hipStream_t)stream;
-    if (wide) {
-        if (vec) hipLaunchKernelGGL((dense_kernel<128, true>), dim3((unsigned)nb), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((dense_kernel<128, false>), dim3((unsigned)nb), dim3(256), 0, s, p);
+#define PG_LAUNCH(BMx, BNx)                                                                             \
+    do {                                                                                                 \
+        if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, true>), dim3((unsigned)nb), dim3(256), 0, s, p); \
+        else hipLaunchKernelGGL((dense_kernel<BMx, BNx, false>), dim3((unsigned)nb), dim3(256), 0, s, p);    \
+    } while (0)
+    if (bm64) {
+        if (wide) PG_LAUNCH(64, 128);
+        else PG_LAUNCH(64, 64);
     } else {
-        if (vec) hipLaunchKernelGGL((dense_kernel<64, true>), dim3((unsigned)nb), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((dense_kernel<64, false>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        if (wide) PG_LAUNCH(128, 128);
+        else PG_LAUNCH(128, 64);
     }
+#undef PG_LAUNCH
     return pg::check_launch("pg_directgcn_dense_f32");
 }
 

@@ -1,0 +1,228 @@
+// Fused prediction head of ProtGramDirectGCN (src/models/protgram_directgcn.py:218-222):
+//   logits = W2 relu(W1 h + b1) + b2            (decoder_fc: Linear -> ReLU -> Dropout(eval) -> Linear)
+//   logp   = log_softmax(logits)                (F.log_softmax(.., dim=-1))
+//   emb    = h / (||h||_2 + eps)                (EmbeddingProcessor.l2_normalize_torch, models_utils.py:139-147)
+// One pass over h: a block stages 64 rows of h in LDS, writes their embeddings, runs both decoder
+// products on fp32 MFMA (v_mfma_f32_32x32x2_f32, B operands straight from the L1/L2-resident
+// weights), and finishes the row softmax in LDS. Replaces 6+ framework launches and two re-reads of h.
+// Fast path: F <= 256, H <= 128, C <= 64 (F, H multiples of 4); other shapes use a one-wave-per-row
+// fallback kernel.
+#include "pg_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int HB = 64;  // rows per block
+
+struct HeadP {
+    int64_t M;
+    int F, H, C;
+    const float* h;
+    int64_t ldh;
+    const float *W1, *b1, *W2, *b2;
+    float eps;
+    float* logp;
+    int64_t ldp;
+    float* emb;
+    int64_t lde;
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int FMAX, int HMAX, int CMAX>
+__global__ __launch_bounds__(256) void head_kernel(HeadP p) {
+    constexpr int HLD = FMAX + 4, ZLD = HMAX + 4, LLD = CMAX + 1;
+    __shared__ __attribute__((aligned(16))) float Hs[HB * HLD];
+    __shared__ __attribute__((aligned(16))) float Zs[HB * ZLD];
+    __shared__ float Ls[HB * LLD];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int li = lane & 31, lh = lane >> 5;
+    const int64_t m0 = (int64_t)blockIdx.x * HB;
+    const int F4 = p.F >> 2;
+
+    // 1. stage h rows (float4, coalesced; rows past M are zero)
+    for (int idx = tid; idx < HB * F4; idx += 256) {
+        const int r = idx / F4, c4 = idx % F4;
+        const int64_t m = m0 + r;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < p.M) v = ld4(p.h + m * p.ldh + 4 * c4);
+        *reinterpret_cast<float4*>(&Hs[r * HLD + 4 * c4]) = v;
+    }
+    __syncthreads();
+
+    // 2. embeddings: 4 lanes... one 16-lane group per row, 16 rows per wave pass
+    {
+        const int g = lane >> 4, t = lane & 15;
+        for (int r = wave * 4 + g; r < HB; r += 16) {
+            float ss = 0.f;
+            for (int c4 = t; c4 < F4; c4 += 16) {
+                const float4 v = ld4(&Hs[r * HLD + 4 * c4]);
+                ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+            }
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+            const int64_t m = m0 + r;
+            if (m < p.M) {
+                const float inv = 1.0f / (sqrtf(ss) + p.eps);
+                for (int c4 = t; c4 < F4; c4 += 16) {
+                    float4 v = ld4(&Hs[r * HLD + 4 * c4]);
+                    v = make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+                    *reinterpret_cast<float4*>(p.emb + m * p.lde + 4 * c4) = v;
+                }
+            }
+        }
+    }
+
+    // 3. z = relu(h W1^T + b1): (HB/32) x (H/32) tiles of 32x32, K = F. Lane feeds A from LDS and
+    //    B (= W1 rows) from global, 4 k at a time with the K permutation of pg_dense.hip.
+    {
+        const int ntile_n = (p.H + 31) / 32;
+        for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
+            const int tm = tile / ntile_n, tn = tile % ntile_n;
+            const int j = tn * 32 + li;
+            const bool jok = j < p.H;
+            const float* w1row = p.W1 + (int64_t)(jok ? j : 0) * p.F;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+            for (int k0 = 0; k0 < p.F; k0 += 8) {
+                const int k = k0 + 4 * lh;
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+                if (k < p.F) {
+                    a = ld4(&Hs[(tm * 32 + li) * HLD + k]);
+                    if (jok) b = ld4(w1row + k);
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+            }
+            const float bj = jok ? p.b1[j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float z = acc[r] + bj;
+                if (j < ZLD - 4) Zs[row * ZLD + j] = jok ? (z > 0.f ? z : 0.f) : 0.f;
+            }
+        }
+    }
+    __syncthreads();
+
+    // 4. logits = z W2^T + b2: (HB/32) x (C/32) tiles, K = H
+    {
+        const int ntile_n = (p.C + 31) / 32;
+        for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
+            const int tm = tile / ntile_n, tn = tile % ntile_n;
+            const int c = tn * 32 + li;
+            const bool cok = c < p.C;
+            const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * p.H;
+            f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+            for (int k0 = 0; k0 < p.H; k0 += 8) {
+                const int k = k0 + 4 * lh;
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+                if (k < p.H) {
+                    a = ld4(&Zs[(tm * 32 + li) * ZLD + k]);
+                    if (cok) b = ld4(w2row + k);
+                }
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+            }
+            const float bc = cok ? p.b2[c] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (cok) Ls[row * LLD + c] = acc[r] + bc;
+            }
+        }
+    }
+    __syncthreads();
+
+    // 5. log_softmax per row (max-shifted, as torch): 4 lanes per row
+    {
+        const int r = tid >> 2, t = tid & 3;
+        const int64_t m = m0 + r;
+        float mx = -INFINITY;
+        for (int c = t; c < p.C; c += 4) mx = fmaxf(mx, Ls[r * LLD + c]);
+        mx = fmaxf(mx, __shfl_xor(mx, 1, 4));
+        mx = fmaxf(mx, __shfl_xor(mx, 2, 4));
+        float se = 0.f;
+        for (int c = t; c < p.C; c += 4) se += expf(Ls[r * LLD + c] - mx);
+        se += __shfl_xor(se, 1, 4);
+        se += __shfl_xor(se, 2, 4);
+        const float lse = mx + logf(se);
+        if (m < p.M)
+            for (int c = t; c < p.C; c += 4) p.logp[m * p.ldp + c] = Ls[r * LLD + c] - lse;
+    }
+}
+
+// General shapes: one wave per row, VALU.
+__global__ __launch_bounds__(256) void head_generic_kernel(HeadP p) {
+    extern __shared__ float sm[];  // per wave: F + H + C floats
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + wave;
+    float* hs = sm + wave * (p.F + p.H + p.C);
+    float* zs = hs + p.F;
+    float* ls = zs + p.H;
+    if (m >= p.M) return;
+    float ss = 0.f;
+    for (int f = lane; f < p.F; f += 64) {
+        const float v = p.h[m * p.ldh + f];
+        hs[f] = v;
+        ss += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    const float inv = 1.0f / (sqrtf(ss) + p.eps);
+    for (int f = lane; f < p.F; f += 64) p.emb[m * p.lde + f] = hs[f] * inv;
+    __builtin_amdgcn_wave_barrier();
+    for (int j = lane; j < p.H; j += 64) {
+        float z = p.b1[j];
+        for (int f = 0; f < p.F; ++f) z += p.W1[(int64_t)j * p.F + f] * hs[f];
+        zs[j] = z > 0.f ? z : 0.f;
+    }
+    __builtin_amdgcn_wave_barrier();
+    float mx = -INFINITY;
+    for (int c = lane; c < p.C; c += 64) {
+        float l = p.b2[c];
+        for (int k = 0; k < p.H; ++k) l += p.W2[(int64_t)c * p.H + k] * zs[k];
+        ls[c] = l;
+        mx = fmaxf(mx, l);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    __builtin_amdgcn_wave_barrier();
+    float se = 0.f;
+    for (int c = lane; c < p.C; c += 64) se += expf(ls[c] - mx);
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const float lse = mx + logf(se);
+    for (int c = lane; c < p.C; c += 64) p.logp[m * p.ldp + c] = ls[c] - lse;
+}
+
+}  // namespace
+
+extern "C" int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, int64_t ldh,
+                                     const float* W1, const float* b1, const float* W2, const float* b2, float eps,
+                                     float* logp, int64_t ldp, float* emb, int64_t lde, void* stream) {
+    PG_REQUIRE(M >= 0 && F > 0 && H > 0 && C > 0 && F < (1 << 16) && H < (1 << 16) && C < (1 << 16), "bad shape");
+    if (M == 0) return PG_OK;
+    PG_REQUIRE(h && W1 && b1 && W2 && b2 && logp && emb, "null pointer");
+    PG_REQUIRE(ldh >= F && lde >= F && ldp >= C, "bad leading dimension");
+    HeadP p{M, (int)F, (int)H, (int)C, h, ldh, W1, b1, W2, b2, eps, logp, ldp, emb, lde};
+    hipStream_t s = (hipStream_t)stream;
+    const bool vec = F % 4 == 0 && H % 4 == 0 && ldh % 4 == 0 && lde % 4 == 0 && pg::aligned16(h) &&
+                     pg::aligned16(emb) && pg::aligned16(W1) && pg::aligned16(W2);
+    const unsigned nb = (unsigned)((M + HB - 1) / HB);
+    if (vec && F <= 128 && H <= 64 && C <= 32) {
+        hipLaunchKernelGGL((head_kernel<128, 64, 32>), dim3(nb), dim3(256), 0, s, p);
+    } else if (vec && F <= 256 && H <= 128 && C <= 64) {
+        hipLaunchKernelGGL((head_kernel<256, 128, 64>), dim3(nb), dim3(256), 0, s, p);
+    } else {
+        const size_t shm = 4 * (size_t)(F + H + C) * sizeof(float);
+        PG_REQUIRE(shm <= 160 * 1024, "head too wide for the generic kernel");
+        hipLaunchKernelGGL(head_generic_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), shm, s, p);
+    }
+    return pg::check_launch("pg_directgcn_head_f32");
+}

@@ -235,6 +235,14 @@ class ProtGramDirectGCN(nn.Module):
             else:
                 h = conv.fused_forward(h, g, original_indices, res_x=h, act=True, fused_norm=self.fused_norm)
             h = F.dropout(h, p=self.dropout, training=self.training)
-        logits = self.decoder_fc(h)
+        return self.head(h)
+
+    def head(self, h):
+        """decoder_fc -> log_softmax, and l2_normalize (protgram_directgcn.py:218-222). Inference (eval, no
+        autograd) runs the fused pg_directgcn_head_f32 kernel; training keeps torch's autograd."""
+        dec = self.decoder_fc
+        if not self.training and not torch.is_grad_enabled() and h.is_cuda:
+            return ops.head(h, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias, self.l2_eps)
+        logits = dec(h)
         emb = h / (torch.norm(h, p=2, dim=1, keepdim=True) + self.l2_eps)  # models_utils.py:139-147
         return F.log_softmax(logits, dim=-1), emb

@@ -212,6 +212,22 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     return Y
 
 
+def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
+    """Fused decoder + log_softmax + L2-normalised embedding (eval-mode forward, no autograd)."""
+    lib = load_library()
+    h = _f32c(h.detach())
+    _require_gpu(h)
+    M, F = h.shape
+    H, C = W1.size(0), W2.size(0)
+    W1, b1, W2, b2 = (_f32c(t.detach()) for t in (W1, b1, W2, b2))
+    logp = torch.empty(M, C, device=h.device, dtype=torch.float32)
+    emb = torch.empty(M, F, device=h.device, dtype=torch.float32)
+    check(lib.pg_directgcn_head_f32(M, F, H, C, _p(h), h.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), float(eps),
+                                    _p(logp), logp.stride(0), _p(emb), emb.stride(0), _stream(h)),
+          "pg_directgcn_head_f32")
+    return logp, emb
+
+
 # ------------------------------------------------------------------------------------------------
 # autograd
 # ------------------------------------------------------------------------------------------------

@@ -88,9 +88,7 @@ def sharded_forward(model, part: NodeRangePartition, x_full: torch.Tensor, group
                 h_full = all_gather_rows(h_local, part, group, buf)
             else:
                 h_full = h_local
-    logits = model.decoder_fc(h_local)
-    emb = h_local / (torch.norm(h_local, p=2, dim=1, keepdim=True) + model.l2_eps)
-    return F.log_softmax(logits, dim=-1), emb
+    return model.head(h_local)
 
 
 def all_gather_rows(h_local: torch.Tensor, part: NodeRangePartition, group=None, out=None) -> torch.Tensor:
@@ -102,5 +100,8 @@ def all_gather_rows(h_local: torch.Tensor, part: NodeRangePartition, group=None,
         h_local = pad
     if out is None:
         out = h_local.new_empty(part.per * part.world, Fd)
-    dist.all_gather_into_tensor(out, h_local.contiguous(), group=group)
+    if dist.get_backend(group) == "gloo":  # rehearsal backend (CPU tests, one-GPU dry runs)
+        dist.all_gather(list(out.view(part.world, part.per, Fd).unbind(0)), h_local.contiguous(), group=group)
+    else:
+        dist.all_gather_into_tensor(out, h_local.contiguous(), group=group)
     return out[:part.n]

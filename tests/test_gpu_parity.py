@@ -277,3 +277,38 @@ def test_full_size_4gram_layer_vs_oracle(pkg, cuda, n, F):
     Z = ops.spmm3(g, xd)
     for j in range(3):
         assert torch.equal(Z[:, j * F:(j + 1) * F].cpu(), oc.propagate(ei, x, w[j])), j
+
+
+@pytest.mark.parametrize("F,H,C", [(128, 64, 20), (32, 16, 5), (256, 128, 50), (16, 8, 400), (34, 17, 3), (12, 6, 1)])
+def test_head_kernel_vs_torch(pkg, cuda, F, H, C):
+    import torch.nn.functional as Fn
+    from protgram_directgcn_amd import ops
+    g = torch.Generator().manual_seed(F * 1000 + C)
+    M = 1000
+    h = torch.randn(M, F, generator=g)
+    h[5] = 0.0  # zero row: emb = 0 / (0 + eps)
+    W1, b1 = torch.randn(H, F, generator=g) * 0.2, torch.randn(H, generator=g) * 0.1
+    W2, b2 = torch.randn(C, H, generator=g) * 0.2, torch.randn(C, generator=g) * 0.1
+    z = Fn.relu(h @ W1.t() + b1)
+    lp_ref = Fn.log_softmax(z @ W2.t() + b2, dim=-1)
+    emb_ref = h / (torch.norm(h, p=2, dim=1, keepdim=True) + 1e-12)
+    lp, emb = ops.head(h.to(cuda), W1.to(cuda), b1.to(cuda), W2.to(cuda), b2.to(cuda), 1e-12)
+    assert_close(lp, lp_ref, "log_probs")
+    assert_close(emb, emb_ref, "emb")
+
+
+@pytest.mark.parametrize("name", ["f1_fasta2", "f3_bench", "f6_pe1"])
+def test_model_inference_path_vs_reference(pkg, cuda, name):
+    """eval + no_grad: the extract_gcn_node_embeddings path (models_utils.py:265-273), fused head kernel."""
+    fx = load(name)
+    ei, ew = graph(fx)
+    dei, dew = dev_graph(ei, ew, cuda)
+    m, dims, N, n, ogd = _model_from_fixture(pkg, fx, cuda)
+    m.eval()
+    data = pkg.Data(x=t(fx["M_x"]).to(cuda), edge_index_in=dei["in"], edge_weight_in=dew["in"],
+                    edge_index_out=dei["out"], edge_weight_out=dew["out"], edge_index_undirected_norm=dei["und"],
+                    edge_weight_undirected_norm=dew["und"])
+    with torch.no_grad():
+        lp, emb = m(data)
+    assert_close(lp, fx["M_logp"], f"{name} log_probs (no_grad)")
+    assert_close(emb, fx["M_emb"], f"{name} embeddings (no_grad)")

@@ -83,16 +83,22 @@ __global__ __launch_bounds__(256) void head_kernel(HeadP p) {
             const int j = tn * 32 + li;
             const bool jok = j < p.H;
             const float* w1row = p.W1 + (int64_t)(jok ? j : 0) * p.F;
+            // all B fragments of this tile issued up front (FMAX/8 float4 per lane), then the MFMA chain
+            constexpr int KG = FMAX / 8;
+            float4 bf[KG];
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int k = g * 8 + 4 * lh;
+                bf[g] = (jok && k < p.F) ? ld4(w1row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             f32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-            for (int k0 = 0; k0 < p.F; k0 += 8) {
-                const int k = k0 + 4 * lh;
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-                if (k < p.F) {
-                    a = ld4(&Hs[(tm * 32 + li) * HLD + k]);
-                    if (jok) b = ld4(w1row + k);
-                }
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int k = g * 8 + 4 * lh;
+                const float4 a = k < p.F ? ld4(&Hs[(tm * 32 + li) * HLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 b = bf[g];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
@@ -117,16 +123,21 @@ __global__ __launch_bounds__(256) void head_kernel(HeadP p) {
             const int c = tn * 32 + li;
             const bool cok = c < p.C;
             const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * p.H;
+            constexpr int KG = HMAX / 8;
+            float4 bf[KG];
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int k = g * 8 + 4 * lh;
+                bf[g] = (cok && k < p.H) ? ld4(w2row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             f32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-            for (int k0 = 0; k0 < p.H; k0 += 8) {
-                const int k = k0 + 4 * lh;
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-                if (k < p.H) {
-                    a = ld4(&Zs[(tm * 32 + li) * ZLD + k]);
-                    if (cok) b = ld4(w2row + k);
-                }
+#pragma unroll
+            for (int g = 0; g < KG; ++g) {
+                const int k = g * 8 + 4 * lh;
+                const float4 a = k < p.H ? ld4(&Zs[(tm * 32 + li) * ZLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 b = bf[g];
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);

@@ -252,7 +252,8 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     for fl, name in ((0, "nosched"), (4, "nosched_unroll4"), (6, "nosched_lds_unroll4")):
         ms = timeit(lambda: ops.spmm3(g0, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
-    for fl, name in ((0, "default"), (1, "no_xcd_remap"), (4, "unroll4"), (5, "unroll4_no_xcd_remap")):
+    for fl, name in ((64, "untiled"), (64 | 4, "untiled_unroll4"), (0, "tiled_fc32_u8"), (4, "tiled_fc32_u4"),
+                     (32, "tiled_fc64_u8"), (36, "tiled_fc64_u4"), (1, "tiled_fc32_noremap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)

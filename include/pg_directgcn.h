@@ -72,6 +72,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_UNROLL4 (1u << 2)      /* 4 gathers in flight per lane instead of 8 */
 #define PG_FLAG_DENSE_BM64 (1u << 3)   /* dense kernel: force 64-row tiles */
 #define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
+#define PG_FLAG_TILED_FC64 (1u << 5)   /* tiled SpMM: 64-float feature chunks (default 32) */
+#define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -98,6 +100,28 @@ int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const int32_t*
                            const float* node_norm, float eps,
                            const float* X, int64_t ldx, int64_t F,
                            float* Z, int64_t ldz, uint32_t flags, void* stream);
+
+/* Row tiles for the LDS-staged SpMM (built once per graph, graph.py build_tiles). Tile t owns the rows
+ * tile_rows[tile_rowptr[t] .. tile_rowptr[t+1]) and stages the sorted unique source rows
+ * tile_ucols[tile_uptr[t] .. tile_uptr[t+1]) in LDS; erow_ptr/entries list each tile-ordered row's
+ * entries in CSR order with `col` replaced by the LDS slot (0 .. U_t-1). */
+typedef struct pg_tiles {
+    const int32_t* tile_rowptr;  /* [n_tiles+1] */
+    const int32_t* tile_rows;    /* [n_rows]    */
+    const int64_t* erow_ptr;     /* [n_rows+1]  */
+    const pg_edge3_t* entries;   /* [nnz]       */
+    const int32_t* tile_uptr;    /* [n_tiles+1] */
+    const int32_t* tile_ucols;   /* [sum U_t]   */
+    int64_t n_tiles;
+    int32_t max_rows;
+    int32_t max_ucols;
+} pg_tiles_t;
+
+/* Same output as pg_spmm3_f32 (bit for bit) through the LDS-staged tiles: each unique source row chunk is
+ * read from L2 once per tile instead of once per entry. F % 32 == 0; max_ucols <= 320 (288 with
+ * PG_FLAG_TILED_FC64); PG_ERR_UNSUPPORTED otherwise (callers then use pg_spmm3_f32). */
+int pg_spmm3_tiled_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
+                       float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Materialise the precomputed-weight records from raw records (same closed form as fused mode). */
 int pg_edges_normalize_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* raw,

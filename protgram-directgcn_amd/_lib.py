@@ -15,6 +15,10 @@ PG_OK = 0
 PG_FLAG_NO_XCD_REMAP = 1 << 0
 PG_FLAG_EDGE_LDS = 1 << 1
 PG_FLAG_UNROLL4 = 1 << 2
+PG_FLAG_DENSE_BM64 = 1 << 3
+PG_FLAG_DENSE_BM128 = 1 << 4
+PG_FLAG_TILED_FC64 = 1 << 5
+PG_FLAG_UNTILED = 1 << 6
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -41,6 +45,13 @@ class LayerArgs(ctypes.Structure):
                 ("Y", c_vp), ("ldy", c_i64)]
 
 
+class TilesArgs(ctypes.Structure):
+    """pg_tiles_t"""
+    _fields_ = [("tile_rowptr", c_vp), ("tile_rows", c_vp), ("erow_ptr", c_vp), ("entries", c_vp),
+                ("tile_uptr", c_vp), ("tile_ucols", c_vp), ("n_tiles", c_i64), ("max_rows", c_i32),
+                ("max_ucols", c_i32)]
+
+
 # symbol -> (restype, argtypes); every symbol declared in include/pg_directgcn.h
 SIGNATURES = {
     "pg_last_error": (ctypes.c_char_p, []),
@@ -48,6 +59,7 @@ SIGNATURES = {
     "pg_spmm3_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
                                               c_u32, c_vp]),
+    "pg_spmm3_tiled_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_edges_normalize_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
                                      c_vp]),

@@ -1,0 +1,149 @@
+// LDS-staged tiled variant of the fused three-adjacency SpMM (same result as pg_spmm3_f32, bit for bit).
+//
+// Why: pg_spmm3_f32 gathers one F-wide source row per pattern entry from L2 (~41 per destination row at
+// 4-gram); it runs at the chip's L2->CU gather rate while >90% of those rows are L2 hits. In an n-gram
+// graph the rows that share an (n-1)-prefix share their in-neighbours and the rows that share an
+// (n-1)-suffix share their out-neighbours, so a K x L tile of the (prefix x suffix) grid needs only
+// 20K + 20L + KL distinct source rows for 41KL entries (4.6x fewer at K=4, L=8). The host builds such
+// tiles once per graph (graph.py build_tiles: per tile the sorted unique source rows + entries re-indexed
+// to LDS slots, each row's entries kept in CSR order).
+//
+// Kernel: one workgroup per (tile, FC-wide feature chunk). Phase 1 gathers the tile's unique source-row
+// chunks into LDS (every lane's loads issued before any LDS write). Phase 2: each row group of FC/4
+// lanes accumulates one destination row from LDS -- same separately rounded mul/add sequence in the
+// same order as the reference's scatter_add_ -- and writes its three output chunks.
+#include "pg_common.h"
+
+namespace {
+
+struct TiledP {
+    const int32_t* tile_rowptr;
+    const int32_t* tile_rows;
+    const int64_t* erow_ptr;
+    const int4* entries;
+    const int32_t* tile_uptr;
+    const int32_t* tile_ucols;
+    int64_t n_tiles;
+    const float* X;
+    int64_t ldx;
+    int F;
+    float* Z;
+    int64_t ldz;
+    int remap;
+};
+
+__device__ __forceinline__ float fb(int v) { return __int_as_float(v); }
+__device__ __forceinline__ float4 axpy4(float4 acc, float w, float4 x) {
+    acc.x = __fadd_rn(acc.x, __fmul_rn(w, x.x));
+    acc.y = __fadd_rn(acc.y, __fmul_rn(w, x.y));
+    acc.z = __fadd_rn(acc.z, __fmul_rn(w, x.z));
+    acc.w = __fadd_rn(acc.w, __fmul_rn(w, x.w));
+    return acc;
+}
+
+template <int FC, int UMAX, int U>
+__global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
+    constexpr int LPR = FC / 4;           // lanes per row chunk (one float4 each)
+    constexpr int GROUPS = 256 / LPR;     // row groups per block
+    constexpr int SLD = FC + 4;           // padded LDS row (floats)
+    constexpr int PASSES = (UMAX + GROUPS - 1) / GROUPS;
+    __shared__ __attribute__((aligned(16))) float Xs[UMAX * SLD];
+
+    const int nchunk = p.F / FC;
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int64_t tile = lb / nchunk;
+    const int chunk = (int)(lb % nchunk);
+    const int grp = threadIdx.x / LPR, t = threadIdx.x % LPR;
+    const int fo = chunk * FC + 4 * t;  // feature offset of this lane
+
+    // phase 1: stage the unique source-row chunks
+    const int u0 = p.tile_uptr[tile];
+    const int nu = p.tile_uptr[tile + 1] - u0;
+    {
+        float4 v[PASSES];
+#pragma unroll
+        for (int k = 0; k < PASSES; ++k) {
+            const int slot = grp + k * GROUPS;
+            v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (slot < nu) {
+                const int64_t col = p.tile_ucols[u0 + slot];
+                v[k] = *reinterpret_cast<const float4*>(p.X + col * p.ldx + fo);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < PASSES; ++k) {
+            const int slot = grp + k * GROUPS;
+            if (slot < nu) *reinterpret_cast<float4*>(&Xs[slot * SLD + 4 * t]) = v[k];
+        }
+    }
+    __syncthreads();
+
+    // phase 2: destination rows of the tile
+    const int r0 = p.tile_rowptr[tile];
+    const int nr = p.tile_rowptr[tile + 1] - r0;
+    for (int ri = grp; ri < nr; ri += GROUPS) {
+        const int64_t pos = r0 + ri;
+        const int64_t row = p.tile_rows[pos];
+        const int64_t e0 = p.erow_ptr[pos], e1 = p.erow_ptr[pos + 1];
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
+        int64_t e = e0;
+        for (; e + U <= e1; e += U) {
+            int4 r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = p.entries[e + u];
+            float4 xv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) xv[u] = *reinterpret_cast<const float4*>(&Xs[r[u].x * SLD + 4 * t]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                a0 = axpy4(a0, fb(r[u].y), xv[u]);
+                a1 = axpy4(a1, fb(r[u].z), xv[u]);
+                a2 = axpy4(a2, fb(r[u].w), xv[u]);
+            }
+        }
+        for (; e < e1; ++e) {
+            const int4 r = p.entries[e];
+            const float4 xv = *reinterpret_cast<const float4*>(&Xs[r.x * SLD + 4 * t]);
+            a0 = axpy4(a0, fb(r.y), xv);
+            a1 = axpy4(a1, fb(r.z), xv);
+            a2 = axpy4(a2, fb(r.w), xv);
+        }
+        float* z = p.Z + row * p.ldz + fo;
+        *reinterpret_cast<float4*>(z) = a0;
+        *reinterpret_cast<float4*>(z + p.F) = a1;
+        *reinterpret_cast<float4*>(z + 2 * p.F) = a2;
+    }
+}
+
+template <int FC, int UMAX>
+void launch(const TiledP& p, uint32_t flags, hipStream_t s) {
+    const int64_t nb = p.n_tiles * (p.F / FC);
+    if (flags & PG_FLAG_UNROLL4)
+        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, 4>), dim3((unsigned)nb), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, 8>), dim3((unsigned)nb), dim3(256), 0, s, p);
+}
+
+}  // namespace
+
+extern "C" int pg_spmm3_tiled_f32(const pg_tiles_t* tl, const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz,
+                                  uint32_t flags, void* stream) {
+    PG_REQUIRE(tl != nullptr, "null tiles");
+    if (tl->n_tiles == 0) return PG_OK;
+    PG_REQUIRE(tl->n_tiles > 0 && tl->tile_rowptr && tl->tile_rows && tl->erow_ptr && tl->entries && tl->tile_uptr &&
+                   tl->tile_ucols,
+               "incomplete tiles");
+    PG_REQUIRE(X && Z && F > 0 && ldx >= F && ldz >= 3 * F, "bad X/Z");
+    PG_REQUIRE(F % 32 == 0 && ldx % 4 == 0 && ldz % 4 == 0 && pg::aligned16(X) && pg::aligned16(Z),
+               "tiled kernel needs F % 32 == 0 and 16-B aligned rows");
+    const bool wide = (flags & PG_FLAG_TILED_FC64) && F % 64 == 0;
+    const int64_t umax = wide ? 288 : 320;
+    if (tl->max_ucols > umax)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "tile stages %d source rows (> %lld)", tl->max_ucols, (long long)umax);
+    TiledP p{tl->tile_rowptr, tl->tile_rows, tl->erow_ptr, reinterpret_cast<const int4*>(tl->entries), tl->tile_uptr,
+             tl->tile_ucols, tl->n_tiles, X, ldx, (int)F, Z, ldz, (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1};
+    hipStream_t s = (hipStream_t)stream;
+    if (wide) launch<64, 288>(p, flags, s);
+    else launch<32, 320>(p, flags, s);
+    return pg::check_launch("pg_spmm3_tiled_f32");
+}

@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import LayerArgs, check, default_flags, load_library
+from ._lib import PG_FLAG_UNTILED, LayerArgs, TilesArgs, check, default_flags, load_library
 from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
@@ -77,6 +77,16 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     fl = default_flags() if flags is None else flags
     s = _stream(x)
     ev = _ev_start(x)
+    tl = g.tiles
+    if g.shared and not fused and tl is not None and F % 32 == 0 and not (fl & PG_FLAG_UNTILED):
+        a = TilesArgs(_p(tl.tile_rowptr), _p(tl.tile_rows), _p(tl.erow_ptr), _p(tl.entries), _p(tl.tile_uptr),
+                      _p(tl.tile_ucols), tl.n_tiles, tl.max_rows, tl.max_ucols)
+        rc = lib.pg_spmm3_tiled_f32(ctypes.byref(a), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s)
+        if rc == 0:
+            _ev_end(x, ev)
+            return Z
+        if rc != -3:  # PG_ERR_UNSUPPORTED -> the untiled kernel below
+            check(rc, "pg_spmm3_tiled_f32")
     if g.shared:
         if fused:
             if g.raw is None:

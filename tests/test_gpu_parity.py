@@ -312,3 +312,36 @@ def test_model_inference_path_vs_reference(pkg, cuda, name):
         lp, emb = m(data)
     assert_close(lp, fx["M_logp"], f"{name} log_probs (no_grad)")
     assert_close(emb, fx["M_emb"], f"{name} embeddings (no_grad)")
+
+
+@pytest.mark.parametrize("graph_kind", ["debruijn3", "fasta3", "random"])
+@pytest.mark.parametrize("F", [32, 64, 128, 256])
+def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
+    """pg_spmm3_tiled_f32 == pg_spmm3_f32 == oracle propagate, bit for bit, all variants."""
+    from protgram_directgcn_amd import ops
+    from protgram_directgcn_amd._lib import PG_FLAG_TILED_FC64, PG_FLAG_UNROLL4, PG_FLAG_UNTILED
+    if graph_kind == "debruijn3":
+        N, s, d, c = pkg.synth.de_bruijn_edges(3)
+        max_u = 320
+    elif graph_kind == "fasta3":
+        fx = load("f5_fasta3")
+        N, s, d, c = int(fx["N"][0]), fx["src"], fx["dst"], fx["cnt"]
+        max_u = 320
+    else:
+        rng = np.random.default_rng(7)
+        N = 2000
+        k = np.unique(rng.integers(0, N, 30000) * N + rng.integers(0, N, 30000))
+        s, d, c = k // N, k % N, rng.integers(1, 9, k.size).astype(np.float32)
+        max_u = 96  # forces the row-split path of the tiler
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda, tiles=False)
+    rc = pkg.graph.ngram_raw_csr(N, s, d, c, device=cuda)
+    g.tiles = pkg.graph.build_tiles(g, *rc.class_keys, max_ucols=max_u)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda)
+    ref = ops.spmm3(g, x, flags=PG_FLAG_UNTILED)
+    for fl in (0, PG_FLAG_UNROLL4, PG_FLAG_TILED_FC64, PG_FLAG_TILED_FC64 | PG_FLAG_UNROLL4, 1):
+        assert torch.equal(ops.spmm3(g, x, flags=fl), ref), fl
+    e = g.edges3.cpu().numpy()
+    rows = torch.from_numpy(np.repeat(np.arange(N), np.diff(g.rowptr.cpu().numpy())))
+    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
+    w = torch.from_numpy(e[:, 1].copy().view(np.float32))
+    assert torch.equal(ref[:, :F].cpu(), oc.propagate(ei, x.cpu(), w))

@@ -81,7 +81,7 @@ def main():
     N = sizes["N"]
     t0 = time.time()
     s, d, c = pkg.synth.de_bruijn_edges(n)[1:]
-    g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm)
+    g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm or args.extra)
     torch.cuda.synchronize()
     log(f"[bench] graph B(20,{n}): N={N} E={s.size} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s")
 
@@ -230,6 +230,8 @@ def cpu_baseline(g, model, x, layers, log):
 
 def extra_measurements(pkg, ops, g, model, x, data, log):
     """Kernel-variant timings and a training step (diagnostics, stderr + 'extra' field)."""
+    import math
+
     import torch
     res = {}
 
@@ -252,8 +254,15 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     for fl, name in ((0, "nosched"), (4, "nosched_unroll4"), (6, "nosched_lds_unroll4")):
         ms = timeit(lambda: ops.spmm3(g0, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
+    if g.tiles is not None and g.raw is not None:
+        # alternative tile shape: 4x4 tiles (<=176 staged rows: fits the 64-float chunk kernel)
+        kin, kout = pkg.graph.class_keys(g.n_rows, *[torch.from_numpy(a).to(x.device) for a in
+                                                      pkg.synth.de_bruijn_edges(round(math.log(g.n_rows, 20)))[1:3]])
+        g44 = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout, K=4, L=4, max_ucols=192))
+        for fl, name in ((0, "tiles44_fc32_u8"), (4, "tiles44_fc32_u4"), (32, "tiles44_fc64_u8"), (36, "tiles44_fc64_u4")):
+            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(g44, x, flags=fl)), 4)
     for fl, name in ((64, "untiled"), (64 | 4, "untiled_unroll4"), (0, "tiled_fc32_u8"), (4, "tiled_fc32_u4"),
-                     (32, "tiled_fc64_u8"), (36, "tiled_fc64_u4"), (1, "tiled_fc32_noremap")):
+                     (1, "tiled_fc32_noremap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)

@@ -115,11 +115,13 @@ typedef struct pg_tiles {
     int64_t n_tiles;
     int32_t max_rows;
     int32_t max_ucols;
+    int32_t max_entries;
 } pg_tiles_t;
 
 /* Same output as pg_spmm3_f32 (bit for bit) through the LDS-staged tiles: each unique source row chunk is
- * read from L2 once per tile instead of once per entry. F % 32 == 0; max_ucols <= 320 (288 with
- * PG_FLAG_TILED_FC64); PG_ERR_UNSUPPORTED otherwise (callers then use pg_spmm3_f32). */
+ * read from L2 once per tile instead of once per entry. F % 32 == 0; max_ucols <= 320 (192 with
+ * PG_FLAG_TILED_FC64) and max_entries <= 1344; PG_ERR_UNSUPPORTED otherwise (callers then use
+ * pg_spmm3_f32). */
 int pg_spmm3_tiled_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
                        float* Z, int64_t ldz, uint32_t flags, void* stream);
 

@@ -49,7 +49,7 @@ class TilesArgs(ctypes.Structure):
     """pg_tiles_t"""
     _fields_ = [("tile_rowptr", c_vp), ("tile_rows", c_vp), ("erow_ptr", c_vp), ("entries", c_vp),
                 ("tile_uptr", c_vp), ("tile_ucols", c_vp), ("n_tiles", c_i64), ("max_rows", c_i32),
-                ("max_ucols", c_i32)]
+                ("max_ucols", c_i32), ("max_entries", c_i32)]
 
 
 # symbol -> (restype, argtypes); every symbol declared in include/pg_directgcn.h

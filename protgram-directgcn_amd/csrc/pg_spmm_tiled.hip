@@ -41,13 +41,15 @@ __device__ __forceinline__ float4 axpy4(float4 acc, float w, float4 x) {
     return acc;
 }
 
-template <int FC, int UMAX, int U>
+template <int FC, int UMAX, int EMAX, int U>
 __global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
     constexpr int LPR = FC / 4;           // lanes per row chunk (one float4 each)
     constexpr int GROUPS = 256 / LPR;     // row groups per block
     constexpr int SLD = FC + 4;           // padded LDS row (floats)
     constexpr int PASSES = (UMAX + GROUPS - 1) / GROUPS;
+    constexpr int EPASSES = (EMAX + 255) / 256;
     __shared__ __attribute__((aligned(16))) float Xs[UMAX * SLD];
+    __shared__ __attribute__((aligned(16))) int4 Rs[EMAX];  // the tile's entry records
 
     const int nchunk = p.F / FC;
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
@@ -56,10 +58,21 @@ __global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
     const int grp = threadIdx.x / LPR, t = threadIdx.x % LPR;
     const int fo = chunk * FC + 4 * t;  // feature offset of this lane
 
-    // phase 1: stage the unique source-row chunks
+    // phase 1: stage the unique source-row chunks and the tile's entry records (all loads in flight
+    // before the first LDS write)
     const int u0 = p.tile_uptr[tile];
     const int nu = p.tile_uptr[tile + 1] - u0;
+    const int r0 = p.tile_rowptr[tile];
+    const int nr = p.tile_rowptr[tile + 1] - r0;
+    const int64_t E0 = p.erow_ptr[r0];
+    const int ne = (int)(p.erow_ptr[r0 + nr] - E0);
     {
+        int4 rv[EPASSES];
+#pragma unroll
+        for (int k = 0; k < EPASSES; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            rv[k] = i < ne ? p.entries[E0 + i] : make_int4(0, 0, 0, 0);
+        }
         float4 v[PASSES];
 #pragma unroll
         for (int k = 0; k < PASSES; ++k) {
@@ -75,22 +88,25 @@ __global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
             const int slot = grp + k * GROUPS;
             if (slot < nu) *reinterpret_cast<float4*>(&Xs[slot * SLD + 4 * t]) = v[k];
         }
+#pragma unroll
+        for (int k = 0; k < EPASSES; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            if (i < ne) Rs[i] = rv[k];
+        }
     }
     __syncthreads();
 
-    // phase 2: destination rows of the tile
-    const int r0 = p.tile_rowptr[tile];
-    const int nr = p.tile_rowptr[tile + 1] - r0;
+    // phase 2: destination rows of the tile, from LDS only
     for (int ri = grp; ri < nr; ri += GROUPS) {
         const int64_t pos = r0 + ri;
         const int64_t row = p.tile_rows[pos];
-        const int64_t e0 = p.erow_ptr[pos], e1 = p.erow_ptr[pos + 1];
+        const int e0 = (int)(p.erow_ptr[pos] - E0), e1 = (int)(p.erow_ptr[pos + 1] - E0);
         float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0;
-        int64_t e = e0;
+        int e = e0;
         for (; e + U <= e1; e += U) {
             int4 r[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) r[u] = p.entries[e + u];
+            for (int u = 0; u < U; ++u) r[u] = Rs[e + u];
             float4 xv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) xv[u] = *reinterpret_cast<const float4*>(&Xs[r[u].x * SLD + 4 * t]);
@@ -102,7 +118,7 @@ __global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
             }
         }
         for (; e < e1; ++e) {
-            const int4 r = p.entries[e];
+            const int4 r = Rs[e];
             const float4 xv = *reinterpret_cast<const float4*>(&Xs[r.x * SLD + 4 * t]);
             a0 = axpy4(a0, fb(r.y), xv);
             a1 = axpy4(a1, fb(r.z), xv);
@@ -115,13 +131,13 @@ __global__ __launch_bounds__(256) void spmm3_tiled_kernel(TiledP p) {
     }
 }
 
-template <int FC, int UMAX>
+template <int FC, int UMAX, int EMAX>
 void launch(const TiledP& p, uint32_t flags, hipStream_t s) {
     const int64_t nb = p.n_tiles * (p.F / FC);
     if (flags & PG_FLAG_UNROLL4)
-        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, 4>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, EMAX, 4>), dim3((unsigned)nb), dim3(256), 0, s, p);
     else
-        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, 8>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((spmm3_tiled_kernel<FC, UMAX, EMAX, 8>), dim3((unsigned)nb), dim3(256), 0, s, p);
 }
 
 }  // namespace
@@ -137,13 +153,14 @@ extern "C" int pg_spmm3_tiled_f32(const pg_tiles_t* tl, const float* X, int64_t 
     PG_REQUIRE(F % 32 == 0 && ldx % 4 == 0 && ldz % 4 == 0 && pg::aligned16(X) && pg::aligned16(Z),
                "tiled kernel needs F % 32 == 0 and 16-B aligned rows");
     const bool wide = (flags & PG_FLAG_TILED_FC64) && F % 64 == 0;
-    const int64_t umax = wide ? 288 : 320;
-    if (tl->max_ucols > umax)
-        return pg::set_error(PG_ERR_UNSUPPORTED, "tile stages %d source rows (> %lld)", tl->max_ucols, (long long)umax);
+    const int64_t umax = wide ? 192 : 320;
+    if (tl->max_ucols > umax || tl->max_entries > 1344)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "tile stages %d source rows / %d entries (> %lld / 1344)",
+                             tl->max_ucols, tl->max_entries, (long long)umax);
     TiledP p{tl->tile_rowptr, tl->tile_rows, tl->erow_ptr, reinterpret_cast<const int4*>(tl->entries), tl->tile_uptr,
              tl->tile_ucols, tl->n_tiles, X, ldx, (int)F, Z, ldz, (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1};
     hipStream_t s = (hipStream_t)stream;
-    if (wide) launch<64, 288>(p, flags, s);
-    else launch<32, 320>(p, flags, s);
+    if (wide) launch<64, 192, 1344>(p, flags, s);
+    else launch<32, 320, 1344>(p, flags, s);
     return pg::check_launch("pg_spmm3_tiled_f32");
 }

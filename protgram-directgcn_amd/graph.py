@@ -196,6 +196,7 @@ class RowTiles:
     n_tiles: int
     max_rows: int
     max_ucols: int
+    max_entries: int
     reuse: float               # entries / staged rows
 
 
@@ -251,7 +252,7 @@ def _rank_within(class_comp, class_of_row):
 
 
 def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4, L: int = 8,
-                max_ucols: int = 320) -> RowTiles:
+                max_ucols: int = 320, max_entries: int = 1344) -> RowTiles:
     """Tile the shared-pattern CSR for the LDS-staged kernel (tiles over max_ucols unique source rows are
     split by rows). Pure index work; the entries keep each row's CSR order (bit-identical sums)."""
     import numpy as np
@@ -266,24 +267,27 @@ def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4
     ekey = np.repeat(tile_id, lens0) * (n + 1) + e[np.repeat(rp[order], lens0) +
                                                 (np.arange(lens0.sum()) - np.repeat(np.cumsum(lens0) - lens0, lens0)), 0]
     uk = np.unique(ekey)
-    ucount = np.bincount(uk // (n + 1), minlength=int(tile_id[-1]) + 1 if tile_id.size else 0)
+    ntile0 = int(tile_id[-1]) + 1 if tile_id.size else 0
+    ucount = np.bincount(uk // (n + 1), minlength=ntile0)
+    ecount = np.bincount(tile_id, weights=lens0, minlength=ntile0)
     new_tile = np.empty_like(tile_id)
     t_next = 0
     bounds = np.flatnonzero(np.diff(np.concatenate([[-1], tile_id, [-2]])) != 0)
     for t, (s0, s1) in enumerate(zip(bounds[:-1], bounds[1:])):
-        if ucount[t] <= max_ucols:
+        if ucount[t] <= max_ucols and ecount[t] <= max_entries:
             new_tile[s0:s1] = t_next
             t_next += 1
             continue
         rows = order[s0:s1]
-        cur, start = set(), s0
+        cur, start, ne = set(), s0, 0
         for j, r in enumerate(rows):
             cols = e[rp[r]:rp[r + 1], 0]
-            if cur and len(cur.union(cols.tolist())) > max_ucols:
+            if cur and (len(cur.union(cols.tolist())) > max_ucols or ne + cols.size > max_entries):
                 new_tile[start:s0 + j] = t_next
                 t_next += 1
-                cur, start = set(), s0 + j
+                cur, start, ne = set(), s0 + j, 0
             cur.update(cols.tolist())
+            ne += cols.size
         new_tile[start:s1] = t_next
         t_next += 1
     T = t_next
@@ -307,6 +311,7 @@ def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4
         erow_ptr=torch.from_numpy(erow_ptr).to(dev), entries=torch.from_numpy(np.ascontiguousarray(ent)).to(dev),
         tile_uptr=torch.from_numpy(tile_uptr).to(dev), tile_ucols=torch.from_numpy(ucols).to(dev),
         n_tiles=T, max_rows=int(np.diff(tile_rowptr).max()) if T else 0, max_ucols=int(usz.max()) if T else 0,
+        max_entries=int(np.diff(erow_ptr[tile_rowptr.astype(np.int64)]).max()) if T else 0,
         reuse=float(erow_ptr[-1] / max(1, usz.sum())))
 
 

@@ -254,15 +254,28 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     for fl, name in ((0, "nosched"), (4, "nosched_unroll4"), (6, "nosched_lds_unroll4")):
         ms = timeit(lambda: ops.spmm3(g0, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
-    if g.tiles is not None and g.raw is not None:
-        # alternative tile shape: 4x4 tiles (<=176 staged rows: fits the 64-float chunk kernel)
+    if g.raw is not None:
         kin, kout = pkg.graph.class_keys(g.n_rows, *[torch.from_numpy(a).to(x.device) for a in
                                                       pkg.synth.de_bruijn_edges(round(math.log(g.n_rows, 20)))[1:3]])
+        gt = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout))
+        for fl, name in ((0, "tiled_fc32_u8"), (4, "tiled_fc32_u4")):
+            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(gt, x, flags=fl)), 4)
+        # alternative tile shape: 4x4 tiles (<=176 staged rows: fits the 64-float chunk kernel)
         g44 = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout, K=4, L=4, max_ucols=192))
-        for fl, name in ((0, "tiles44_fc32_u8"), (4, "tiles44_fc32_u4"), (32, "tiles44_fc64_u8"), (36, "tiles44_fc64_u4")):
+        for fl, name in ((32, "tiles44_fc64_u8"),):
             res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(g44, x, flags=fl)), 4)
-    for fl, name in ((64, "untiled"), (64 | 4, "untiled_unroll4"), (0, "tiled_fc32_u8"), (4, "tiled_fc32_u4"),
-                     (1, "tiled_fc32_noremap")):
+        # untiled kernel driven by 2-D tile orders (L1 reuse inside a block of 8 rows)
+        import numpy as np
+        for K, L, bmajor in ((4, 8, False), (4, 8, True), (2, 4, True), (4, 2, False), (8, 4, True), (20, 20, True)):
+            order, tid = pkg.graph.tile_schedule(kin, kout, K, L)
+            if bmajor:  # inside each tile sort by (out-class, in-class) instead of (in-class, out-class)
+                kin_np, kout_np = kin.cpu().numpy(), kout.cpu().numpy()
+                o2 = np.lexsort((kin_np[order], kout_np[order], tid))
+                order = order[o2]
+            ro = torch.from_numpy(order.astype(np.int32)).to(x.device)
+            gk = dataclasses.replace(g, tiles=None, row_order=ro)
+            res[f"spmm3_order_{K}x{L}{'_b' if bmajor else '_a'}_ms"] = round(timeit(lambda: ops.spmm3(gk, x)), 4)
+    for fl, name in ((0, "default"), (4, "unroll4"), (1, "no_xcd_remap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)

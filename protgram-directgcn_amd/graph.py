@@ -394,7 +394,7 @@ def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu", schedule: bool = 
 
 
 def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,
-                          keep_raw: bool = True, schedule: bool = True, tiles: bool = True) -> CSRGraph:
+                          keep_raw: bool = True, schedule: bool = True, tiles: bool = False) -> CSRGraph:
     """Shared-pattern device CSR of (mathcal_A_in, mathcal_A_out, A_undirected_norm) from raw counts.
 
     Weights are materialised on the GPU by ``pg_edges_normalize_f32`` (bit-exact closed form of

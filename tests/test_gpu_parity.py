@@ -333,7 +333,7 @@ def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
         k = np.unique(rng.integers(0, N, 30000) * N + rng.integers(0, N, 30000))
         s, d, c = k // N, k % N, rng.integers(1, 9, k.size).astype(np.float32)
         max_u = 96  # forces the row-split path of the tiler
-    g = pkg.build_propagation_csr(N, s, d, c, device=cuda, tiles=False)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
     rc = pkg.graph.ngram_raw_csr(N, s, d, c, device=cuda)
     g.tiles = pkg.graph.build_tiles(g, *rc.class_keys, max_ucols=max_u)
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda)

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Run selected hot-path kernels on the 4-gram workload a few times (target for rocprofv3 --pmc passes).
+usage: python tools/kprobe.py [reps]"""
+import dataclasses
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+from __graft_entry__ import load_package  # noqa: E402
+
+pkg = load_package()
+from protgram_directgcn_amd import ops  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+dev = torch.device("cuda:0")
+N, s, d, c = pkg.synth.de_bruijn_edges(4)
+g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+kin, kout = pkg.graph.class_keys(N, torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev))
+gt = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout))
+x = torch.randn(N, 128, device=dev)
+torch.manual_seed(0)
+layer = pkg.DirectGCNLayer(128, 128, N).to(dev)
+prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
+for _ in range(reps):
+    Z = ops.spmm3(g, x)                 # spmm_vec_kernel (untiled)
+    ops.spmm3(gt, x)                    # spmm3_tiled_kernel
+    ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)
+torch.cuda.synchronize()
+print("ok")

@@ -275,7 +275,7 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
             ro = torch.from_numpy(order.astype(np.int32)).to(x.device)
             gk = dataclasses.replace(g, tiles=None, row_order=ro)
             res[f"spmm3_order_{K}x{L}{'_b' if bmajor else '_a'}_ms"] = round(timeit(lambda: ops.spmm3(gk, x)), 4)
-    for fl, name in ((0, "default"), (4, "unroll4"), (1, "no_xcd_remap")):
+    for fl, name in ((0, "window_u8"), (4, "window_u4"), (128, "bcast_u8"), (132, "bcast_u4"), (1, "window_noremap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)

@@ -74,6 +74,7 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
 #define PG_FLAG_TILED_FC64 (1u << 5)   /* tiled SpMM: 64-float feature chunks (default 32) */
 #define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
+#define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record (old default) */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

@@ -237,6 +237,164 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
         }
 }
 
+// Variant C (default for F = 4*LPR, LPR in {8,16,32,64}): records through a per-row-group LDS window.
+// Counters on gfx950 (tools/pmc_passes.sh) show the broadcast record load of variants A/B costing as much
+// L1->VGPR (TD) bandwidth as the feature gathers themselves: every lane of a row group loads the same 16-B
+// record, i.e. a 1 KiB wave-instruction for LPR-fold duplicated data, and TD is busy ~94% of the kernel.
+// Here the LPR lanes of a group load LPR *consecutive* records (one each, coalesced), park them in the
+// group's own LDS window, and read them back as LDS broadcasts: the TD only carries the feature gathers.
+// A window is private to one row group inside one wave, so wave-local ordering (the compiler's
+// lgkmcnt waits + a wave barrier) replaces block barriers. Same accumulation order: still bit-exact.
+template <int LPR, int NV, int U, int MODE>
+__global__ __launch_bounds__(256) void spmm_win_kernel(SpmmParams p) {
+    using R = typename Rec<MODE>::T;
+    constexpr int RPB = 256 / LPR;
+    constexpr int NACC = Shape<MODE>::NACC;
+    constexpr int NSLICE = Shape<MODE>::NSLICE;
+    constexpr int WIN = LPR;  // records per window (one per lane)
+    __shared__ __attribute__((aligned(16))) R win[RPB][WIN];
+
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int grp = threadIdx.x / LPR;
+    const int t = threadIdx.x % LPR;
+    const int64_t pos = lb * RPB + grp;
+    const bool live = pos < p.n_rows;
+    const int64_t row = (live && p.row_order) ? (int64_t)p.row_order[pos] : pos;
+    const R* __restrict__ E = reinterpret_cast<const R*>(p.edges);
+    const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.X);
+    const int64_t ldx4 = p.ldx >> 2;
+    const int F4 = p.F >> 2;
+    int64_t beg = 0, end = 0;
+    if (live) {
+        beg = p.rowptr[row];
+        end = p.rowptr[row + 1];
+    }
+    float4 ni = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (MODE == M3RAW) {
+        if (live) ni = p.node_norm[row];
+    }
+    float4 acc[NACC][NV];
+#pragma unroll
+    for (int a = 0; a < NACC; ++a)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[a][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    R* mywin = win[grp];
+    // prefetch the first window into registers
+    R nxt = (beg + t < end) ? E[beg + t] : R{};
+    for (int64_t w0 = beg; w0 < end; w0 += WIN) {
+        __builtin_amdgcn_wave_barrier();  // previous window fully consumed by this group's lanes
+        mywin[t] = nxt;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t wn = w0 + WIN;
+        if (wn + t < end) nxt = E[wn + t];  // next window in flight while this one is consumed
+        const int n = (int)((end - w0) < WIN ? (end - w0) : WIN);
+        int j = 0;
+        for (; j + U <= n; j += U) {
+            R r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = mywin[j + u];
+            float4 xv[U][NSLICE][NV];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float4* src = X4 + (int64_t)r[u].x * ldx4 + t;
+#pragma unroll
+                for (int s = 0; s < NSLICE; ++s)
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) xv[u][s][v] = src[s * F4 + v * LPR];
+            }
+            float4 nj[U];
+            if constexpr (MODE == M3RAW) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) nj[u] = p.node_norm[r[u].x];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (MODE == M3) {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        acc[0][v] = axpy4(acc[0][v], fb(r[u].y), xv[u][0][v]);
+                        acc[1][v] = axpy4(acc[1][v], fb(r[u].z), xv[u][0][v]);
+                        acc[2][v] = axpy4(acc[2][v], fb(r[u].w), xv[u][0][v]);
+                    }
+                } else if constexpr (MODE == M3RAW) {
+                    const W3 w = fused_weights(fb(r[u].y), fb(r[u].z), fb(r[u].w), nj[u], ni, (int64_t)r[u].x == row,
+                                               p.eps);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        acc[0][v] = axpy4(acc[0][v], w.in, xv[u][0][v]);
+                        acc[1][v] = axpy4(acc[1][v], w.out, xv[u][0][v]);
+                        acc[2][v] = axpy4(acc[2][v], w.und, xv[u][0][v]);
+                    }
+                } else if constexpr (MODE == M3T) {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        float4 a = acc[0][v];
+                        a = axpy4(a, fb(r[u].y), xv[u][0][v]);
+                        a = axpy4(a, fb(r[u].z), xv[u][1][v]);
+                        a = axpy4(a, fb(r[u].w), xv[u][2][v]);
+                        acc[0][v] = a;
+                    }
+                } else {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) acc[0][v] = axpy4(acc[0][v], fb(r[u].y), xv[u][0][v]);
+                }
+            }
+        }
+        for (; j < n; ++j) {
+            const R r = mywin[j];
+            const float4* src = X4 + (int64_t)r.x * ldx4 + t;
+            float4 xv[NSLICE][NV];
+#pragma unroll
+            for (int s = 0; s < NSLICE; ++s)
+#pragma unroll
+                for (int v = 0; v < NV; ++v) xv[s][v] = src[s * F4 + v * LPR];
+            if constexpr (MODE == M3) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    acc[0][v] = axpy4(acc[0][v], fb(r.y), xv[0][v]);
+                    acc[1][v] = axpy4(acc[1][v], fb(r.z), xv[0][v]);
+                    acc[2][v] = axpy4(acc[2][v], fb(r.w), xv[0][v]);
+                }
+            } else if constexpr (MODE == M3RAW) {
+                const W3 w = fused_weights(fb(r.y), fb(r.z), fb(r.w), p.node_norm[r.x], ni, (int64_t)r.x == row, p.eps);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    acc[0][v] = axpy4(acc[0][v], w.in, xv[0][v]);
+                    acc[1][v] = axpy4(acc[1][v], w.out, xv[0][v]);
+                    acc[2][v] = axpy4(acc[2][v], w.und, xv[0][v]);
+                }
+            } else if constexpr (MODE == M3T) {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    float4 a = acc[0][v];
+                    a = axpy4(a, fb(r.y), xv[0][v]);
+                    a = axpy4(a, fb(r.z), xv[1][v]);
+                    a = axpy4(a, fb(r.w), xv[2][v]);
+                    acc[0][v] = a;
+                }
+            } else {
+#pragma unroll
+                for (int v = 0; v < NV; ++v) acc[0][v] = axpy4(acc[0][v], fb(r.y), xv[0][v]);
+            }
+        }
+    }
+    if (!live) return;
+    float4* Z4 = reinterpret_cast<float4*>(p.Z) + row * (p.ldz >> 2) + t;
+#pragma unroll
+    for (int a = 0; a < NACC; ++a)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            float4* dst = Z4 + a * F4 + v * LPR;
+            float4 val = acc[a][v];
+            if (p.accumulate) {
+                const float4 old = *dst;
+                val = make_float4(add(old.x, val.x), add(old.y, val.y), add(old.z, val.z), add(old.w, val.w));
+            }
+            *dst = val;
+        }
+}
+
 // Fallback for feature widths that are not a multiple of 4 (or too wide for the vector path):
 // one wave per row, features in chunks of 64 (one per lane), records re-read per chunk.
 template <int MODE>
@@ -313,6 +471,15 @@ void launch_vec(const SpmmParams& p, hipStream_t s) {
 
 template <int MODE, int LPR, int NV>
 void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
+    if (!(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS)) && LPR >= 8) {
+        constexpr int RPB = 256 / LPR;
+        const int64_t nb = (p.n_rows + RPB - 1) / RPB;
+        if (flags & PG_FLAG_UNROLL4)
+            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 8, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        return;
+    }
     const bool lds = (flags & PG_FLAG_EDGE_LDS) && p.row_order == nullptr;  // staging needs contiguous rows
     const bool u4 = flags & PG_FLAG_UNROLL4;
     if (lds) {

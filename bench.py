@@ -275,7 +275,7 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
             ro = torch.from_numpy(order.astype(np.int32)).to(x.device)
             gk = dataclasses.replace(g, tiles=None, row_order=ro)
             res[f"spmm3_order_{K}x{L}{'_b' if bmajor else '_a'}_ms"] = round(timeit(lambda: ops.spmm3(gk, x)), 4)
-    for fl, name in ((0, "window_u8"), (4, "window_u4"), (128, "bcast_u8"), (132, "bcast_u4"), (1, "window_noremap")):
+    for fl, name in ((0, "window_u4"), (4, "window_u8"), (128, "bcast_u8"), (1, "window_u4_noremap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)
@@ -294,8 +294,8 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     res["head_ms"] = round(timeit(lambda: ops.head(x, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias,
                                                    1e-12)), 4)
     G = torch.randn_like(Z)
-    ms = timeit(lambda: ops.spmm3_t(g, G))
-    res["spmm3t_ms"] = round(ms, 4)
+    for fl, name in ((0, "bcast_u8"), (4, "bcast_u4"), (256, "window_u4"), (260, "window_u8")):
+        res[f"spmm3t_{name}_ms"] = round(timeit(lambda: ops.spmm3_t(g, G, flags=fl)), 4)
     # copy-kernel bandwidth reference
     a = torch.empty(512 * 1024 * 1024 // 4, device=x.device)
     b = torch.empty_like(a)

@@ -471,13 +471,17 @@ void launch_vec(const SpmmParams& p, hipStream_t s) {
 
 template <int MODE, int LPR, int NV>
 void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
-    if (!(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS)) && LPR >= 8) {
+    // Default: variant C (record window) with 4 gathers in flight for the single-slice modes; the
+    // three-slice transpose (M3T) keeps variant A (its 3x wider gathers need the registers).
+    // PG_FLAG_WINDOW forces C for any mode; PG_FLAG_UNROLL4 toggles C to 8 gathers in flight.
+    const bool win = ((MODE != M3T) || (flags & PG_FLAG_WINDOW)) && !(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS));
+    if (win && LPR >= 8) {
         constexpr int RPB = 256 / LPR;
         const int64_t nb = (p.n_rows + RPB - 1) / RPB;
         if (flags & PG_FLAG_UNROLL4)
-            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
-        else
             hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 8, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
         return;
     }
     const bool lds = (flags & PG_FLAG_EDGE_LDS) && p.row_order == nullptr;  // staging needs contiguous rows

@@ -75,6 +75,7 @@ typedef struct pg_edge1 {
 #define PG_FLAG_TILED_FC64 (1u << 5)   /* tiled SpMM: 64-float feature chunks (default 32) */
 #define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
+#define PG_FLAG_DENSE_8WAVES (1u << 9)  /* dense kernel: 8 waves per 128x128 tile (32x64 per wave) */
 #define PG_FLAG_WINDOW (1u << 8)        /* SpMM variant C (per-row-group LDS record window) also for the transpose */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which

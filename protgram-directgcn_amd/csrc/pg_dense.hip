@@ -61,15 +61,16 @@ __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_
     return p.res_x[m * p.ld_res + (k - 3 * p.F_in)];
 }
 
-template <int BM, int BN, bool VEC>
-__global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
-    constexpr int WN = (BN == 128 || BM == 64) ? 2 : 1;
-    constexpr int WM = 4 / WN;
+template <int BM, int BN, int NW, bool VEC>
+__global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
+    constexpr int NT = 64 * NW;  // threads
+    constexpr int WN = (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
+    constexpr int WM = NW / WN;
     static_assert(BM / WM >= 32 && BN / WN >= 32, "wave tile too small");
     constexpr int TM = BM / WM / 32;
     constexpr int TN = BN / WN / 32;
-    constexpr int A_F4 = BM * BK / 4 / 256;
-    constexpr int B_F4 = BN * BK / 4 / 256;
+    constexpr int A_F4 = BM * BK / 4 / NT;
+    constexpr int B_F4 = BN * BK / 4 / NT;
 
     constexpr int TLD = BN + 4;  // epilogue tile row (floats), 16-B aligned, conflict-free float4 reads
     constexpr int MAIN_FLOATS = 2 * BM * LDSW + 2 * BN * LDSW;
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
     __shared__ __attribute__((aligned(16))) float smem[SMEM_FLOATS];
     __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
     __shared__ int64_t Crow[BM];  // constant row per tile row (original_indices), -1 past M
+    static_assert(BM <= NT, "gate prologue assumes one thread per tile row");
     float (*As)[BM * LDSW] = reinterpret_cast<float (*)[BM * LDSW]>(smem);
     float (*Bs)[BN * LDSW] = reinterpret_cast<float (*)[BN * LDSW]>(smem + 2 * BM * LDSW);
 
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
-            const int idx = tid + 256 * q;
+            const int idx = tid + NT * q;
             const int64_t m = min(m0 + (idx >> 3), mlast);
             const int k = k0 + 4 * (idx & 7);
             if (VEC) {
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
         }
 #pragma unroll
         for (int q = 0; q < B_F4; ++q) {
-            const int idx = tid + 256 * q;
+            const int idx = tid + NT * q;
             const int n = min(n0 + (idx >> 3), p.F_out - 1);
             const int k = k0 + 4 * (idx & 7);
             const float* src = p.Bp + (int64_t)n * p.K;
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
     auto stash = [&](int buf, int k0) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
-            const int idx = tid + 256 * q;
+            const int idx = tid + NT * q;
             float4 v = ra[q];
             if (VEC) {
                 const int k = k0 + 4 * (idx & 7);
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
         }
 #pragma unroll
         for (int q = 0; q < B_F4; ++q) {
-            const int idx = tid + 256 * q;
+            const int idx = tid + NT * q;
             float4 v = rb[q];
             if (VEC) {
                 const int k = k0 + 4 * (idx & 7);
@@ -230,8 +232,8 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
     __syncthreads();
 
     constexpr int C4 = BN / 4;            // float4 per tile row
-    constexpr int ITER = BM * C4 / 256;   // float4 per thread
-    constexpr int BATCH = 4;
+    constexpr int ITER = BM * C4 / NT;    // float4 per thread
+    constexpr int BATCH = ITER < 4 ? ITER : 4;
     const int c4 = tid % C4;              // fixed column group per thread
     const int nb = n0 + 4 * c4;
     const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void dense_kernel(DenseP p) {
         bool ok[BATCH];
 #pragma unroll
         for (int u = 0; u < BATCH; ++u) {
-            rl[u] = (tid + 256 * (it0 + u)) / C4;
+            rl[u] = (tid + NT * (it0 + u)) / C4;
             mm[u] = m0 + rl[u];
             ok[u] = Crow[rl[u]] >= 0 && nb < p.F_out;
             cv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -411,23 +413,28 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     // BM=64 row tiles double the grid (fewer idle CUs in the last wave of blocks); BM=128 halves the
     // B-tile re-reads. PG_FLAG_DENSE_BM64 / PG_FLAG_DENSE_BM128 force one; default picks by grid size.
     const int64_t nb128 = ((a->M + 127) / 128) * ((a->F_out + BN - 1) / BN);
-    bool bm64 = nb128 < 4 * 512;
+    bool bm64 = false;
+    (void)nb128;
     if (flags & PG_FLAG_DENSE_BM64) bm64 = true;
     if (flags & PG_FLAG_DENSE_BM128) bm64 = false;
     const int64_t BMv = bm64 ? 64 : 128;
     const int64_t nb = ((a->M + BMv - 1) / BMv) * ((a->F_out + BN - 1) / BN);
     hipStream_t s = (hipStream_t)stream;
-#define PG_LAUNCH(BMx, BNx)                                                                             \
-    do {                                                                                                 \
-        if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, true>), dim3((unsigned)nb), dim3(256), 0, s, p); \
-        else hipLaunchKernelGGL((dense_kernel<BMx, BNx, false>), dim3((unsigned)nb), dim3(256), 0, s, p);    \
+#define PG_LAUNCH(BMx, BNx, NWx)                                                                                \
+    do {                                                                                                           \
+        if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
+        else hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, false>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p);    \
     } while (0)
+    const bool w8 = (flags & PG_FLAG_DENSE_8WAVES) && !bm64;
     if (bm64) {
-        if (wide) PG_LAUNCH(64, 128);
-        else PG_LAUNCH(64, 64);
+        if (wide) PG_LAUNCH(64, 128, 4);
+        else PG_LAUNCH(64, 64, 4);
+    } else if (w8) {
+        if (wide) PG_LAUNCH(128, 128, 8);
+        else PG_LAUNCH(128, 64, 8);
     } else {
-        if (wide) PG_LAUNCH(128, 128);
-        else PG_LAUNCH(128, 64);
+        if (wide) PG_LAUNCH(128, 128, 4);
+        else PG_LAUNCH(128, 64, 4);
     }
 #undef PG_LAUNCH
     return pg::check_launch("pg_directgcn_dense_f32");

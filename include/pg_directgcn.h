@@ -70,13 +70,14 @@ typedef struct pg_edge1 {
 #define PG_FLAG_NO_XCD_REMAP (1u << 0) /* keep hardware blockIdx order instead of XCD-contiguous rows */
 #define PG_FLAG_EDGE_LDS (1u << 1)     /* stage edge records through LDS (variant B) */
 #define PG_FLAG_UNROLL4 (1u << 2)      /* alternate gathers-in-flight depth (variants A/B: 4 instead of 8; C: 8 instead of 4) */
+/* SpMM variants: C (default) = per-row-group LDS record window; A = every lane loads the record
+ * (PG_FLAG_BCAST_RECORDS); B = block-wide LDS staging of records (PG_FLAG_EDGE_LDS). */
 #define PG_FLAG_DENSE_BM64 (1u << 3)   /* dense kernel: force 64-row tiles */
 #define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
 #define PG_FLAG_TILED_FC64 (1u << 5)   /* tiled SpMM: 64-float feature chunks (default 32) */
 #define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
-#define PG_FLAG_DENSE_8WAVES (1u << 9)  /* dense kernel: 8 waves per 128x128 tile (32x64 per wave) */
-#define PG_FLAG_WINDOW (1u << 8)        /* SpMM variant C (per-row-group LDS record window) also for the transpose */
+#define PG_FLAG_DENSE_4WAVES (1u << 9)  /* dense kernel: 4 waves per 128-row tile (64x64 per wave) instead of 8 */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

@@ -20,7 +20,7 @@ PG_FLAG_DENSE_BM128 = 1 << 4
 PG_FLAG_TILED_FC64 = 1 << 5
 PG_FLAG_UNTILED = 1 << 6
 PG_FLAG_BCAST_RECORDS = 1 << 7
-PG_FLAG_WINDOW = 1 << 8
+PG_FLAG_DENSE_4WAVES = 1 << 9
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 

@@ -425,7 +425,7 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
         else hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, false>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p);    \
     } while (0)
-    const bool w8 = (flags & PG_FLAG_DENSE_8WAVES) && !bm64;
+    const bool w8 = !(flags & PG_FLAG_DENSE_4WAVES) && !bm64;
     if (bm64) {
         if (wide) PG_LAUNCH(64, 128, 4);
         else PG_LAUNCH(64, 64, 4);

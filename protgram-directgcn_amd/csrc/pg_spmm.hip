@@ -471,10 +471,9 @@ void launch_vec(const SpmmParams& p, hipStream_t s) {
 
 template <int MODE, int LPR, int NV>
 void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
-    // Default: variant C (record window) with 4 gathers in flight for the single-slice modes; the
-    // three-slice transpose (M3T) keeps variant A (its 3x wider gathers need the registers).
-    // PG_FLAG_WINDOW forces C for any mode; PG_FLAG_UNROLL4 toggles C to 8 gathers in flight.
-    const bool win = ((MODE != M3T) || (flags & PG_FLAG_WINDOW)) && !(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS));
+    // Default: variant C (record window) with 4 gathers in flight; PG_FLAG_UNROLL4 toggles it to 8.
+    // PG_FLAG_BCAST_RECORDS / PG_FLAG_EDGE_LDS select variants A / B (measurement only).
+    const bool win = !(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS));
     if (win && LPR >= 8) {
         constexpr int RPB = 256 / LPR;
         const int64_t nb = (p.n_rows + RPB - 1) / RPB;

@@ -345,3 +345,52 @@ def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
     ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
     w = torch.from_numpy(e[:, 1].copy().view(np.float32))
     assert torch.equal(ref[:, :F].cpu(), oc.propagate(ei, x.cpu(), w))
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
+                                                      (300, 32, 16, False, False, False), (513, 20, 12, True, True, False),
+                                                      (129, 16, 40, True, True, True), (64, 128, 96, False, True, True)])
+def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+    """pg_directgcn_dense_f32 (all tilings) against the same formula in float64."""
+    from protgram_directgcn_amd import ops
+    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_NO_XCD_REMAP
+    g = torch.Generator().manual_seed(M + Fin + Fout)
+    Ntot = M + 37
+    Z = torch.randn(M, 3 * Fin, generator=g)
+    xres = torch.randn(M, Fin, generator=g)
+    prm = {k: torch.randn(Fout, Fin, generator=g) * 0.1 for k in ("W_main_in", "W_main_out", "W_undirected", "W_shared")}
+    for k in ("b_main_in", "b_dir_shared_in", "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared"):
+        prm[k] = torch.randn(Fout, generator=g) * 0.1
+    gate = 0 if vec else 1
+    for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+        prm[k] = torch.rand((Ntot, 1) if vec else (1,), generator=g) + 0.5
+    const = torch.randn(Ntot, Fout, generator=g) if vec else None
+    r = torch.randperm(Ntot, generator=g)[:M] if rows else None
+    W_res = torch.randn(Fout, Fin, generator=g) * 0.1 if proj else None
+    b_res = torch.randn(Fout, generator=g) * 0.1 if proj else None
+    if not proj and Fin != Fout:
+        xres = None
+    # float64 reference
+    d = {k: v.double() for k, v in prm.items()}
+    idx = r if r is not None else torch.arange(M)
+    gv = (lambda k: d[k][idx]) if vec else (lambda k: d[k].expand(M, 1))
+    s = [gv("C_all") * gv("C_directed") * gv("C_in"), gv("C_all") * gv("C_directed") * gv("C_out"),
+         gv("C_all") * gv("C_undirected")]
+    Wk = [d["W_main_in"] + d["W_shared"], d["W_main_out"] + d["W_shared"], d["W_undirected"] + d["W_shared"]]
+    bk = [d["b_main_in"] + d["b_dir_shared_in"], d["b_main_out"] + d["b_dir_shared_out"],
+          d["b_undirected"] + d["b_undirected_shared"]]
+    Zd = Z.double()
+    y = sum(s[k] * (Zd[:, k * Fin:(k + 1) * Fin] @ Wk[k].t() + bk[k]) for k in range(3))
+    if const is not None:
+        y = y + const.double()[idx]
+    if xres is not None:
+        y = y + (xres.double() @ W_res.double().t() + b_res.double() if proj else xres.double())
+    y = torch.nn.functional.leaky_relu(y, 0.01)
+    dv = {k: v.to(cuda) for k, v in prm.items()}
+    for fl in (0, PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_NO_XCD_REMAP):
+        out = ops.layer_dense(Z.to(cuda), dv, gate, rows=None if r is None else r.to(cuda),
+                              constant=None if const is None else const.to(cuda),
+                              res_x=None if xres is None else xres.to(cuda),
+                              W_res=None if W_res is None else W_res.to(cuda),
+                              b_res=None if b_res is None else b_res.to(cuda), act=True, flags=fl)
+        assert_close(out, y.float(), f"dense flags={fl}", rtol=2e-5, atol=2e-5)

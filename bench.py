@@ -271,8 +271,12 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
         kin, kout = pkg.graph.class_keys(g.n_rows, *[torch.from_numpy(a).to(x.device) for a in
                                                       pkg.synth.de_bruijn_edges(round(math.log(g.n_rows, 20)))[1:3]])
         gt = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout))
-        for fl, name in ((0, "tiled_fc32_u8"), (4, "tiled_fc32_u4")):
+        for fl, name in ((0, "tiled_fc32_u8"),):
             res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(gt, x, flags=fl)), 4)
+        gr = dataclasses.replace(g, tiles=pkg.graph.build_row_tiles(g, kin, kout, x.size(1)))
+        res["row_tiles"] = [gr.tiles.n_tiles, gr.tiles.max_rows, gr.tiles.max_ucols, round(gr.tiles.reuse, 2)]
+        for fl, name in ((0, "tiled_rows"), (1, "tiled_rows_noremap")):
+            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(gr, x, flags=fl)), 4)
         # alternative tile shape: 4x4 tiles (<=176 staged rows: fits the 64-float chunk kernel)
         g44 = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout, K=4, L=4, max_ucols=192))
         for fl, name in ((32, "tiles44_fc64_u8"),):

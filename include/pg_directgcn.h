@@ -129,6 +129,12 @@ typedef struct pg_tiles {
 int pg_spmm3_tiled_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
                        float* Z, int64_t ldz, uint32_t flags, void* stream);
 
+/* Same output again, full-width-row tiles (v3): one workgroup per tile of <= 256/(F/4) rows staging
+ * <= 128 (F=128), 192 (F=64) or 64 (F=256) unique source rows whole in LDS; PG_ERR_UNSUPPORTED for other
+ * shapes. Tiles for it: graph.py build_tiles(K=4, L=2, max_ucols=128, max_rows=8) at F=128. */
+int pg_spmm3_tiled_rows_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
+                            float* Z, int64_t ldz, uint32_t flags, void* stream);
+
 /* Materialise the precomputed-weight records from raw records (same closed form as fused mode). */
 int pg_edges_normalize_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* raw,
                            const float* node_norm, float eps, pg_edge3_t* out, void* stream);

@@ -62,6 +62,8 @@ SIGNATURES = {
     "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
                                               c_u32, c_vp]),
     "pg_spmm3_tiled_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3_tiled_rows_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32,
+                                               c_vp]),
     "pg_edges_normalize_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
                                      c_vp]),

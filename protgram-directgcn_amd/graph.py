@@ -198,6 +198,7 @@ class RowTiles:
     max_ucols: int
     max_entries: int
     reuse: float               # entries / staged rows
+    kind: str = "chunk"        # "chunk": pg_spmm3_tiled_f32 (feature chunks); "rows": pg_spmm3_tiled_rows_f32
 
 
 def class_keys(n: int, src: torch.Tensor, dst: torch.Tensor):
@@ -251,8 +252,19 @@ def _rank_within(class_comp, class_of_row):
     return rank[class_of_row]
 
 
+ROW_TILE_SHAPES = {64: (4, 4, 192, 16), 128: (4, 2, 128, 8), 256: (2, 2, 64, 4)}  # F -> K, L, max_ucols, max_rows
+
+
+def build_row_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, F: int) -> RowTiles:
+    """Tiles for pg_spmm3_tiled_rows_f32 at feature width F (capacities in ROW_TILE_SHAPES)."""
+    K, L, mu, mr = ROW_TILE_SHAPES[F]
+    t = build_tiles(g, kin, kout, K=K, L=L, max_ucols=mu, max_rows=mr)
+    t.kind = "rows"
+    return t
+
+
 def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4, L: int = 8,
-                max_ucols: int = 320, max_entries: int = 1344) -> RowTiles:
+                max_ucols: int = 320, max_entries: int = 1344, max_rows: int = 1 << 30) -> RowTiles:
     """Tile the shared-pattern CSR for the LDS-staged kernel (tiles over max_ucols unique source rows are
     split by rows). Pure index work; the entries keep each row's CSR order (bit-identical sums)."""
     import numpy as np
@@ -274,7 +286,7 @@ def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4
     t_next = 0
     bounds = np.flatnonzero(np.diff(np.concatenate([[-1], tile_id, [-2]])) != 0)
     for t, (s0, s1) in enumerate(zip(bounds[:-1], bounds[1:])):
-        if ucount[t] <= max_ucols and ecount[t] <= max_entries:
+        if ucount[t] <= max_ucols and ecount[t] <= max_entries and s1 - s0 <= max_rows:
             new_tile[s0:s1] = t_next
             t_next += 1
             continue
@@ -282,7 +294,8 @@ def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4
         cur, start, ne = set(), s0, 0
         for j, r in enumerate(rows):
             cols = e[rp[r]:rp[r + 1], 0]
-            if cur and (len(cur.union(cols.tolist())) > max_ucols or ne + cols.size > max_entries):
+            if cur and (len(cur.union(cols.tolist())) > max_ucols or ne + cols.size > max_entries
+                        or s0 + j - start >= max_rows):
                 new_tile[start:s0 + j] = t_next
                 t_next += 1
                 cur, start, ne = set(), s0 + j, 0

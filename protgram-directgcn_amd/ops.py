@@ -81,7 +81,8 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     if g.shared and not fused and tl is not None and F % 32 == 0 and not (fl & PG_FLAG_UNTILED):
         a = TilesArgs(_p(tl.tile_rowptr), _p(tl.tile_rows), _p(tl.erow_ptr), _p(tl.entries), _p(tl.tile_uptr),
                       _p(tl.tile_ucols), tl.n_tiles, tl.max_rows, tl.max_ucols, tl.max_entries)
-        rc = lib.pg_spmm3_tiled_f32(ctypes.byref(a), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s)
+        fn = lib.pg_spmm3_tiled_rows_f32 if tl.kind == "rows" else lib.pg_spmm3_tiled_f32
+        rc = fn(ctypes.byref(a), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s)
         if rc == 0:
             _ev_end(x, ev)
             return Z

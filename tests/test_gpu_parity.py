@@ -345,6 +345,11 @@ def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
     ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
     w = torch.from_numpy(e[:, 1].copy().view(np.float32))
     assert torch.equal(ref[:, :F].cpu(), oc.propagate(ei, x.cpu(), w))
+    if F in pkg.graph.ROW_TILE_SHAPES:  # v3 full-row tiles
+        g.tiles = pkg.graph.build_row_tiles(g, *rc.class_keys, F)
+        assert g.tiles.max_rows <= pkg.graph.ROW_TILE_SHAPES[F][3]
+        for fl in (0, 1):
+            assert torch.equal(ops.spmm3(g, x, flags=fl), ref), ("rows", fl)
 
 
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),

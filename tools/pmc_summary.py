@@ -11,7 +11,7 @@ dur = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{d}/*/*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        short = ("spmm_untiled" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
+        short = ("spmm_window" if "spmm_win_kernel" in k else "spmm_bcast" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
                  else "dense" if "dense_kernel" in k else None)
         if short is None:
             continue
@@ -19,7 +19,7 @@ for f in sorted(glob.glob(f"{d}/*/*counter_collection.csv")):
 for f in sorted(glob.glob(f"{d}/*/*kernel_trace.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        short = ("spmm_untiled" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
+        short = ("spmm_window" if "spmm_win_kernel" in k else "spmm_bcast" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
                  else "dense" if "dense_kernel" in k else None)
         if short:
             dur[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Config 3 training step (4-gram, dims [128,128,128], C=20): reference loop of
+protgram_directgcn_trainer.py:91-100 (nll + 1e-7 * sum ||p||^2, Adam lr 1e-3). Prints ms/step."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from __graft_entry__ import load_package  # noqa: E402
+
+pkg = load_package()
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+dev = torch.device("cuda:0")
+n = 4
+N, s, d, c = pkg.synth.de_bruijn_edges(n)
+g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+torch.manual_seed(0)
+model = pkg.ProtGramDirectGCN([128, 128, 128], N, 20, n, 0, 512, 0.5, True).to(dev)
+x = torch.randn(N, 128, generator=torch.Generator().manual_seed(1234)).to(dev)
+y = torch.arange(N, device=dev) // (20 ** (n - 1))
+data = pkg.Data(x=x, graph=g)
+opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
+model.train()
+
+
+def step():
+    opt.zero_grad()
+    out, _ = model(data=data)
+    loss = F.nll_loss(out, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters() if p.requires_grad)
+    loss.backward()
+    opt.step()
+    return loss
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(steps):
+    loss = step()
+torch.cuda.synchronize()
+print(f"train step {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

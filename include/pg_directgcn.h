@@ -198,6 +198,35 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stre
  * read); W_res != NULL selects the projected residual. */
 int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
 
+/* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
+ * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output
+ * (read for leaky_relu' when act != 0); `packed` the forward's packed operand. Outputs:
+ *   dpre  [M, F_out]  = dY * leaky'(Y)         (also the identity residual's and the constant's gradient)
+ *   dZ    [M, 3F_in]  = s_q * (dpre B_q)        gradient of the propagated aggregates
+ *   dres  [M, F_in]   = dpre W_res              projected residual only (W_res != NULL)
+ *   dgate [5, M]      per-row dL/d{c_in, c_out, c_directed, c_undirected, c_all} (row m uses gate row r(m))
+ *   gates [M, 4]      the row gates s_in, s_out, s_und, 1 (scratch output)
+ *   dW    [F_out*K + 4*F_out]  dL/dB in the packed layout: segment q of [F_out, K] is the gradient of
+ *                     W_main_q + W_shared (W_res for q = 3); then [4, F_out] for the bias sums (b_res last)
+ * work: pg_directgcn_dense_bwd_workspace(args) floats. Deterministic (fixed-order reductions).
+ * Returns PG_ERR_UNSUPPORTED unless F_in, F_out and every leading dimension are multiples of 4 and the
+ * buffers 16-B aligned. Five launches on `stream`: transpose, dgrad (MFMA), gate grads, wgrad (MFMA,
+ * split over rows), split reduction. */
+typedef struct pg_layer_grad_args {
+    const float* dY; int64_t lddy;
+    float* dpre; int64_t ldp;
+    float* dZ; int64_t lddz;
+    float* dres; int64_t lddres;
+    float* dgate;
+    float* gates;
+    float* dW;
+    float* work; int64_t work_floats;
+} pg_layer_grad_args_t;
+
+int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* args);
+int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* args, const float* packed, const pg_layer_grad_args_t* grads,
+                               uint32_t flags, void* stream);
+
 /* Fused prediction head (protgram_directgcn.py:218-222, eval mode): per row m of h [M, F]
  *   logp[m] = log_softmax(W2 relu(W1 h[m] + b1) + b2)      W1 [H, F], W2 [C, H] (nn.Linear layout)
  *   emb[m]  = h[m] / (||h[m]||_2 + eps)                      (models_utils.py:139-147)

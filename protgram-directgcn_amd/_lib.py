@@ -25,6 +25,9 @@ PG_FLAG_DENSE_4WAVES = 1 << 9
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
 
+PG_OK, PG_ERR_ARG, PG_ERR_HIP, PG_ERR_UNSUPPORTED = 0, -1, -2, -3
+
+
 class NativeLibraryError(RuntimeError):
     pass
 
@@ -45,6 +48,13 @@ class LayerArgs(ctypes.Structure):
                 ("W_res", c_vp), ("b_res", c_vp),
                 ("act", c_i32), ("slope", c_f32),
                 ("Y", c_vp), ("ldy", c_i64)]
+
+
+class LayerGradArgs(ctypes.Structure):
+    """pg_layer_grad_args_t"""
+    _fields_ = [("dY", c_vp), ("lddy", c_i64), ("dpre", c_vp), ("ldp", c_i64), ("dZ", c_vp), ("lddz", c_i64),
+                ("dres", c_vp), ("lddres", c_i64), ("dgate", c_vp), ("gates", c_vp), ("dW", c_vp),
+                ("work", c_vp), ("work_floats", c_i64)]
 
 
 class TilesArgs(ctypes.Structure):
@@ -72,6 +82,9 @@ SIGNATURES = {
     "pg_directgcn_packed_floats": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "pg_directgcn_pack_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp]),
     "pg_directgcn_dense_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_u32, c_vp]),
+    "pg_directgcn_dense_bwd_workspace": (c_i64, [ctypes.POINTER(LayerArgs)]),
+    "pg_directgcn_dense_bwd_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
+                                                  c_u32, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                              c_vp, c_i64, c_vp, c_i64, c_vp]),
 }

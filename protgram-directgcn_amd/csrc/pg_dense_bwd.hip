@@ -1,0 +1,654 @@
+// Backward of the fused DirectGCN dense contraction (pg_dense.hip) on gfx950 fp32 MFMA.
+//
+// Forward (per row m, packed B = [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] as [F_out, K]):
+//   pre[m] = sum_q s_q[m] (Z_q[m] B_q^T + bsum_q) + bsum_3 + constant + residual,  y = leaky(pre)
+// This is the autograd of src/models/protgram_directgcn.py:100-133 (the six nn.Linear calls, the bias
+// adds and the c_* gate combine) plus ProtGramDirectGCN.forward :213-215 (residual, leaky_relu). Given
+// dY, with dpre = dY * leaky'(y):
+//   dZ_q[m]  = s_q[m] * (dpre[m] B_q)                     q = in, out, und       (dgrad_kernel)
+//   dres[m]  = dpre[m] B_3                                 projected residual     (dgrad_kernel)
+//   ds_q[m]  = <dpre[m] B_q, Z_q[m]> + <dpre[m], bsum_q>   -> dc_* per row        (dgrad + gate_grad_kernel)
+//   dB_q     = sum_m s_q[m] dpre[m]^T Z_q[m]  (dB_3 with res_x, s_3 = 1)         (wgrad_kernel, split-K)
+//   dbsum_q  = sum_m s_q[m] dpre[m]                                               (wgrad_kernel)
+// dB_q is the gradient of every weight summed into segment q (W_main_q and W_shared alike), so the
+// caller maps dW_main_q = dB_q, dW_shared = dB_0 + dB_1 + dB_2, dW_res = dB_3 and the bias pairs the same way.
+//
+// dgrad_kernel: the forward kernel's tiling (BM=128 x BN=128 x BK=32, 8 waves, double-buffered LDS,
+//   K-permuted ds_read_b128 operands) with K = F_out and B = the packed weights transposed once
+//   (transpose_kernel, [K, F_out]). The A loader computes dpre at stash time; the n-tile-0 blocks also
+//   write dpre, the row gates (for wgrad) and the bias dots. The epilogue parks the tile in LDS, then
+//   streams Z in and dZ out with float4 accesses and reduces <G_q, Z_q> per row in fixed order.
+// wgrad_kernel: C[P x N] = A^T diag(s) B over row chunks of 32 (the reduction runs over rows): both
+//   operands staged row-major in LDS; each MFMA k-step of lane half h reads row 4h+s with ds_read_b32
+//   (32 consecutive floats per half: conflict-free). Each split writes a partial; reduce_splits_kernel
+//   sums them in split order (deterministic, no atomics).
+#include <algorithm>
+
+#include "pg_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr int LDSW = 36;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+
+struct Gates {
+    int gate_mode;
+    const float *C_in, *C_out, *C_dir, *C_und, *C_all;
+    const int64_t* rows;
+};
+
+__device__ __forceinline__ void gate_values(const Gates& g, int64_t m, float& ci, float& co, float& cd, float& cu,
+                                            float& ca) {
+    const int64_t r = (g.gate_mode == PG_GATES_SCALAR) ? 0 : (g.rows ? g.rows[m] : m);
+    ci = g.C_in[r];
+    co = g.C_out[r];
+    cd = g.C_dir[r];
+    cu = g.C_und[r];
+    ca = g.C_all[r];
+}
+
+struct DgradP {
+    int64_t M;
+    int F_in, F_out, N;  // N = forward K (3 or 4 segments of F_in)
+    const float* dY;
+    int64_t lddy;
+    const float* Y;
+    int64_t ldy;
+    int act;
+    float slope;
+    const float* BT;    // [N, F_out]
+    const float* bsum;  // [4, F_out]
+    const float* Z;
+    int64_t ldz;
+    Gates g;
+    float* dpre;
+    int64_t ldp;
+    float* dZ;
+    int64_t lddz;
+    float* dres;
+    int64_t lddres;
+    float* gates;  // [M, 4]
+    float* dsp;    // [ntn * 3, M]
+    int remap;
+};
+
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(64 * NW) void dgrad_kernel(DgradP p) {
+    constexpr int NT = 64 * NW;
+    constexpr int WN = 2;
+    constexpr int WM = NW / WN;
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+    constexpr int A_F4 = BM * BK / 4 / NT;
+    constexpr int B_F4 = BN * BK / 4 / NT;
+    constexpr int TLD = BN + 4;
+    constexpr int MAIN_FLOATS = 2 * BM * LDSW + 2 * BN * LDSW;
+    constexpr int SMEM_FLOATS = MAIN_FLOATS > BM * TLD ? MAIN_FLOATS : BM * TLD;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM_FLOATS];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ float Bd[BM * 3];
+    static_assert(BM <= NT, "one thread per tile row");
+    float (*As)[BM * LDSW] = reinterpret_cast<float (*)[BM * LDSW]>(smem);
+    float (*Bs)[BN * LDSW] = reinterpret_cast<float (*)[BN * LDSW]>(smem + 2 * BM * LDSW);
+
+    const int ntn = (p.N + BN - 1) / BN;
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    // n-tiles fastest: the tiles of one row block run together (same XCD under the remap) and share
+    // their dY / Y rows through L2.
+    const int nt = (int)(lb % ntn);
+    const int64_t m0 = (lb / ntn) * BM;
+    const int n0 = nt * BN;
+    const bool lead = nt == 0;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+
+    if (tid < BM) {
+        const int64_t m = m0 + tid;
+        float4 s = make_float4(0.f, 0.f, 0.f, 1.f);
+        if (m < p.M) {
+            float ci, co, cd, cu, ca;
+            gate_values(p.g, m, ci, co, cd, cu, ca);
+            const float cad = ca * cd;
+            s.x = cad * ci;
+            s.y = cad * co;
+            s.z = ca * cu;
+            if (lead) st4(p.gates + m * 4, s);
+        }
+        st4(&Sg[tid * 4], s);
+    }
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    float4 ra[A_F4], ry[A_F4], rb[B_F4];
+    float bd[A_F4][3];
+#pragma unroll
+    for (int q = 0; q < A_F4; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
+    const int64_t mlast = p.M - 1;
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int64_t m = min(m0 + (idx >> 3), mlast);
+            const int k = k0 + 4 * (idx & 7);
+            const int kc = k < p.F_out ? k : 0;
+            ra[q] = ld4(p.dY + m * p.lddy + kc);
+            if (p.act) ry[q] = ld4(p.Y + m * p.ldy + kc);
+        }
+#pragma unroll
+        for (int q = 0; q < B_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int n = min(n0 + (idx >> 3), p.N - 1);
+            const int k = k0 + 4 * (idx & 7);
+            rb[q] = ld4(p.BT + (int64_t)n * p.F_out + (k < p.F_out ? k : 0));
+        }
+    };
+    auto stash = [&](int buf, int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 4 * (idx & 7);
+            const int64_t m = m0 + (idx >> 3);
+            float4 d = ra[q];
+            if (p.act) {
+                const float4 y = ry[q];
+                d.x = y.x > 0.f ? d.x : d.x * p.slope;
+                d.y = y.y > 0.f ? d.y : d.y * p.slope;
+                d.z = y.z > 0.f ? d.z : d.z * p.slope;
+                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+            }
+            if (k >= p.F_out) d = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lead && k < p.F_out && m < p.M) {
+                st4(p.dpre + m * p.ldp + k, d);
+#pragma unroll
+                for (int s = 0; s < 3; ++s) bd[q][s] += dot4(d, ld4(p.bsum + s * p.F_out + k));
+            }
+            st4(&As[buf][(idx >> 3) * LDSW + 4 * (idx & 7)], d);
+        }
+#pragma unroll
+        for (int q = 0; q < B_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 4 * (idx & 7);
+            st4(&Bs[buf][(idx >> 3) * LDSW + 4 * (idx & 7)], k < p.F_out ? rb[q] : make_float4(0.f, 0.f, 0.f, 0.f));
+        }
+    };
+
+    const int ntiles = (p.F_out + BK - 1) / BK;
+    fetch(0);
+    stash(0, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < ntiles) fetch((t + 1) * BK);
+        const float* Ab = As[cur];
+        const float* Bb = Bs[cur];
+#pragma unroll
+        for (int g = 0; g < BK / 8; ++g) {
+            float4 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) a[i] = ld4(&Ab[(wm * TM * 32 + i * 32 + li) * LDSW + g * 8 + 4 * lh]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[j] = ld4(&Bb[(wn * TN * 32 + j * 32 + li) * LDSW + g * 8 + 4 * lh]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+                }
+        }
+        if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BK);
+        __syncthreads();
+    }
+
+    // bias dots <dpre[m], bsum_q>: 8 consecutive lanes hold one row's K slices
+    if (lead) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                float v = bd[q][s];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                bd[q][s] = v;
+            }
+            const int idx = tid + NT * q;
+            if ((idx & 7) == 0) {
+                Bd[(idx >> 3) * 3 + 0] = bd[q][0];
+                Bd[(idx >> 3) * 3 + 1] = bd[q][1];
+                Bd[(idx >> 3) * 3 + 2] = bd[q][2];
+            }
+        }
+    }
+
+    float* T = smem;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                T[rl * TLD + wn * TN * 32 + j * 32 + li] = acc[i][j][r];
+            }
+    __syncthreads();
+
+    constexpr int C4 = BN / 4;
+    constexpr int ITER = BM * C4 / NT;
+    constexpr int BATCH = ITER < 4 ? ITER : 4;
+    const int c4 = tid % C4;
+    const int j = n0 + 4 * c4;
+    const int seg = j < p.N ? j / p.F_in : 4;  // F_in % 4 == 0: a float4 never straddles segments
+    for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+        float4 zv[BATCH];
+        int rl[BATCH];
+        int64_t mm[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            rl[u] = (tid + NT * (it0 + u)) / C4;
+            mm[u] = m0 + rl[u];
+            zv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mm[u] < p.M && seg < 3) zv[u] = ld4(p.Z + mm[u] * p.ldz + j);
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            float part = 0.f;
+            if (mm[u] < p.M && seg < 4) {
+                const float4 gv = ld4(&T[rl[u] * TLD + 4 * c4]);
+                if (seg < 3) {
+                    const float s = Sg[rl[u] * 4 + seg];
+                    st4(p.dZ + mm[u] * p.lddz + j, make_float4(s * gv.x, s * gv.y, s * gv.z, s * gv.w));
+                    part = dot4(gv, zv[u]);
+                } else {
+                    st4(p.dres + mm[u] * p.lddres + (j - 3 * p.F_in), gv);
+                }
+            }
+            T[rl[u] * TLD + 4 * c4] = part;  // own slot, already consumed
+        }
+    }
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+        const int64_t m = m0 + tid;
+        float ds[3] = {0.f, 0.f, 0.f};
+        if (lead) {
+            ds[0] = Bd[tid * 3 + 0];
+            ds[1] = Bd[tid * 3 + 1];
+            ds[2] = Bd[tid * 3 + 2];
+        }
+        for (int c = 0; c < C4; ++c) {
+            const int jj = n0 + 4 * c;
+            if (jj >= p.N) break;
+            const int q = jj / p.F_in;
+            if (q < 3) ds[q] += T[tid * TLD + 4 * c];
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
+    }
+}
+
+// ds_q[m] = sum over n-tiles (fixed order) -> dL/dc_* per row (chain rule of s_q(c), :116-133)
+__global__ __launch_bounds__(256) void gate_grad_kernel(int64_t M, int ntn, const float* dsp, Gates g, float* dgate) {
+    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+        float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+        for (int t = 0; t < ntn; ++t) {
+            d0 += dsp[((int64_t)t * 3 + 0) * M + m];
+            d1 += dsp[((int64_t)t * 3 + 1) * M + m];
+            d2 += dsp[((int64_t)t * 3 + 2) * M + m];
+        }
+        float ci, co, cd, cu, ca;
+        gate_values(g, m, ci, co, cd, cu, ca);
+        const float cad = ca * cd;
+        dgate[0 * M + m] = d0 * cad;                       // c_in
+        dgate[1 * M + m] = d1 * cad;                       // c_out
+        dgate[2 * M + m] = ca * (d0 * ci + d1 * co);        // c_directed
+        dgate[3 * M + m] = d2 * ca;                        // c_undirected
+        dgate[4 * M + m] = cd * (d0 * ci + d1 * co) + d2 * cu;  // c_all
+    }
+}
+
+__global__ __launch_bounds__(256) void transpose_kernel(int R, int C, const float* in, float* out) {
+    // out[c][r] = in[r][c]; tiny (the packed weights), run once per backward
+    const int64_t total = (int64_t)R * C;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i / R), r = (int)(i % R);
+        out[i] = in[(int64_t)r * C + c];
+    }
+}
+
+struct WgradP {
+    int64_t M;
+    int P, N, F_in;
+    const float* A;  // [M, P]
+    int64_t lda;
+    const float* Z;  // segments 0..2
+    int64_t ldz;
+    const float* R;  // segment 3 (projected residual input) or null
+    int64_t ldr;
+    const float* gates;  // [M, 4] or null (all scales 1)
+    int64_t rows_per_split;
+    int64_t part_stride;
+    float* part;  // [splits, P*N + 4*P]
+};
+
+constexpr int WROWS = 32;  // rows per K step
+constexpr int WLD = 132;   // LDS row (floats)
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
+    constexpr int NT = 64 * NW;
+    constexpr int BI = 128, BJ = 128;
+    constexpr int WJ = 2, WI = NW / WJ;
+    constexpr int TI = BI / WI / 32, TJ = BJ / WJ / 32;
+    constexpr int F4 = WROWS * 32 / NT;  // float4 per thread per operand (rows of 128 floats = 32 float4)
+    static_assert(TI >= 1 && TJ >= 1 && F4 >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) float smem[4 * WROWS * WLD];
+    float (*As)[WROWS * WLD] = reinterpret_cast<float (*)[WROWS * WLD]>(smem);
+    float (*Bs)[WROWS * WLD] = reinterpret_cast<float (*)[WROWS * WLD]>(smem + 2 * WROWS * WLD);
+
+    const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI;
+    const int64_t r0 = (int64_t)blockIdx.z * p.rows_per_split;
+    const int64_t rend = min(r0 + p.rows_per_split, p.M);
+    const bool do_db = blockIdx.x == 0;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wi = wave / WJ, wj = wave % WJ;
+    const int li = lane & 31, lh = lane >> 5;
+    const int c4 = tid & 31;
+    const int ia = i0 + 4 * c4, jb = j0 + 4 * c4;
+    const bool ia_ok = ia < p.P, jb_ok = jb < p.N;
+    const int seg = jb_ok ? jb / p.F_in : 0;
+    const float* bsrc = seg < 3 ? p.Z + jb : p.R + (jb - 3 * p.F_in);
+    const int64_t ldb = seg < 3 ? p.ldz : p.ldr;
+
+    f32x16 acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float db[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) db[q][0] = db[q][1] = db[q][2] = db[q][3] = 0.f;
+
+    float4 ra[F4], rb[F4], rs[F4];
+    const int64_t mlast = p.M - 1;
+    auto fetch = [&](int64_t base) {
+#pragma unroll
+        for (int q = 0; q < F4; ++q) {
+            const int row = (tid + NT * q) >> 5;
+            const int64_t m = min(base + row, mlast);
+            ra[q] = ld4(p.A + m * p.lda + (ia_ok ? ia : 0));
+            rb[q] = ld4((jb_ok ? bsrc : p.Z) + m * ldb);
+            rs[q] = p.gates ? ld4(p.gates + m * 4) : make_float4(1.f, 1.f, 1.f, 1.f);
+        }
+    };
+    auto stash = [&](int buf, int64_t base) {
+#pragma unroll
+        for (int q = 0; q < F4; ++q) {
+            const int row = (tid + NT * q) >> 5;
+            const bool ok = base + row < rend;
+            const float4 s = rs[q];
+            const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a = (ok && ia_ok) ? ra[q] : zero;
+            const float sc = seg == 0 ? s.x : seg == 1 ? s.y : seg == 2 ? s.z : 1.f;
+            const float4 b = (ok && jb_ok) ? make_float4(rb[q].x * sc, rb[q].y * sc, rb[q].z * sc, rb[q].w * sc) : zero;
+            if (do_db) {
+                const float sv[4] = {s.x, s.y, s.z, 1.f};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    db[t][0] += sv[t] * a.x;
+                    db[t][1] += sv[t] * a.y;
+                    db[t][2] += sv[t] * a.z;
+                    db[t][3] += sv[t] * a.w;
+                }
+            }
+            st4(&As[buf][row * WLD + 4 * c4], a);
+            st4(&Bs[buf][row * WLD + 4 * c4], b);
+        }
+    };
+
+    const int64_t nsteps = (rend - r0 + WROWS - 1) / WROWS;
+    if (nsteps > 0) {
+        fetch(r0);
+        stash(0, r0);
+    }
+    __syncthreads();
+    for (int64_t t = 0; t < nsteps; ++t) {
+        const int cur = (int)(t & 1);
+        const int64_t nb = r0 + (t + 1) * WROWS;
+        if (t + 1 < nsteps) fetch(nb);
+        const float* Ab = As[cur];
+        const float* Bb = Bs[cur];
+#pragma unroll
+        for (int g = 0; g < WROWS / 8; ++g) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int row = g * 8 + 4 * lh + s;
+                float a[TI], b[TJ];
+#pragma unroll
+                for (int i = 0; i < TI; ++i) a[i] = Ab[row * WLD + wi * TI * 32 + i * 32 + li];
+#pragma unroll
+                for (int j = 0; j < TJ; ++j) b[j] = Bb[row * WLD + wj * TJ * 32 + j * 32 + li];
+#pragma unroll
+                for (int i = 0; i < TI; ++i)
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        if (t + 1 < nsteps) stash(cur ^ 1, nb);
+        __syncthreads();
+    }
+
+    float* out = p.part + (int64_t)blockIdx.z * p.part_stride;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int oi = i0 + wi * TI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int oj = j0 + wj * TJ * 32 + j * 32 + li;
+                if (oi < p.P && oj < p.N) out[(int64_t)oi * p.N + oj] = acc[i][j][r];
+            }
+
+    if (do_db) {  // 16 row groups x 32 column groups x 16 sums -> fixed-order reduction over row groups
+        constexpr int RG = NT / 32;
+        float* D = smem;  // the K loop ended with a barrier
+        const int rg = tid >> 5;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) D[(rg * 32 + c4) * 16 + q * 4 + e] = db[q][e];
+        __syncthreads();
+        for (int w = tid; w < 32 * 16; w += NT) {
+            const int cc = w & 31, qe = w >> 5;
+            float v = 0.f;
+            for (int g2 = 0; g2 < RG; ++g2) v += D[(g2 * 32 + cc) * 16 + qe];
+            const int i = i0 + 4 * cc + (qe & 3);
+            if (i < p.P) out[(int64_t)p.P * p.N + (qe >> 2) * p.P + i] = v;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void reduce_splits_kernel(int64_t n4, int splits, int64_t stride, const float* part,
+                                                            float* out) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        float4 s = ld4(part + 4 * i);
+        for (int k = 1; k < splits; ++k) {
+            const float4 v = ld4(part + (int64_t)k * stride + 4 * i);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        st4(out + 4 * i, s);
+    }
+}
+
+constexpr int DG_BM = 128, DG_BN = 128, DG_NW = 8, WG_NW = 8;
+
+struct BwdPlan {
+    int K, ntn, splits;
+    int64_t rows_per_split, part_stride;
+    int64_t off_bt, off_dsp, off_part, total;
+};
+
+BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
+    BwdPlan b{};
+    b.K = (int)((proj ? 4 : 3) * F_in);
+    b.ntn = (b.K + DG_BN - 1) / DG_BN;
+    const int64_t tiles = ((F_out + 127) / 128) * ((b.K + 127) / 128);
+    int64_t splits = (512 + tiles - 1) / tiles;
+    const int64_t chunks = (M + WROWS - 1) / WROWS;
+    if (splits > chunks) splits = chunks;
+    if (splits < 1) splits = 1;
+    b.rows_per_split = ((chunks + splits - 1) / splits) * WROWS;
+    b.splits = (int)((M + b.rows_per_split - 1) / b.rows_per_split);
+    if (b.splits < 1) b.splits = 1;
+    b.part_stride = ((F_out * b.K + 4 * F_out + 3) / 4) * 4;
+    auto up4 = [](int64_t v) { return (v + 3) / 4 * 4; };
+    b.off_bt = 0;
+    b.off_dsp = up4((int64_t)b.K * F_out);
+    b.off_part = b.off_dsp + up4((int64_t)b.ntn * 3 * M);
+    b.total = b.off_part + (int64_t)b.splits * b.part_stride;
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* a) {
+    if (!a || a->M < 0 || a->F_in <= 0 || a->F_out <= 0) return -1;
+    return plan_of(a->M, a->F_in, a->F_out, a->W_res != nullptr).total;
+}
+
+int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, const pg_layer_grad_args_t* g,
+                               uint32_t flags, void* stream) {
+    PG_REQUIRE(a != nullptr && packed != nullptr && g != nullptr, "null args");
+    PG_REQUIRE(a->M >= 0 && a->F_in > 0 && a->F_out > 0 && a->F_in < (1 << 20) && a->F_out < (1 << 20),
+               "bad shape M=%lld F_in=%lld F_out=%lld", (long long)a->M, (long long)a->F_in, (long long)a->F_out);
+    PG_REQUIRE(a->C_in && a->C_out && a->C_directed && a->C_undirected && a->C_all, "null gate");
+    PG_REQUIRE(a->gate_mode == PG_GATES_VECTOR || a->gate_mode == PG_GATES_SCALAR, "bad gate_mode");
+    PG_REQUIRE(!a->W_res || a->res_x, "W_res needs res_x");
+    PG_REQUIRE(g->dY && g->dpre && g->dZ && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
+    PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
+    PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
+    const bool proj = a->W_res != nullptr;
+    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj);
+    PG_REQUIRE(g->work_floats >= pl.total, "workspace too small: %lld < %lld floats", (long long)g->work_floats,
+               (long long)pl.total);
+    // vector paths only: every row / column block is float4
+    const bool vec = a->F_in % 4 == 0 && a->F_out % 4 == 0 && a->ldz % 4 == 0 && g->lddy % 4 == 0 &&
+                     g->ldp % 4 == 0 && g->lddz % 4 == 0 && (!a->act || a->ldy % 4 == 0) &&
+                     (!proj || (a->ld_res % 4 == 0 && g->lddres % 4 == 0 && pg::aligned16(a->res_x) &&
+                                pg::aligned16(g->dres))) &&
+                     pg::aligned16(a->Z) && pg::aligned16(g->dY) && pg::aligned16(g->dpre) && pg::aligned16(g->dZ) &&
+                     pg::aligned16(g->gates) && pg::aligned16(g->dW) && pg::aligned16(g->work) &&
+                     pg::aligned16(packed) && (!a->act || pg::aligned16(a->Y));
+    if (!vec)
+        return pg::set_error(PG_ERR_UNSUPPORTED,
+                             "pg_directgcn_dense_bwd_f32: needs F_in, F_out and leading dims multiple of 4 and "
+                             "16-B aligned buffers");
+    PG_REQUIRE(a->ldz >= 3 * a->F_in && g->lddz >= 3 * a->F_in && g->lddy >= a->F_out && g->ldp >= a->F_out,
+               "leading dimensions too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int K = pl.K;
+    const int F_in = (int)a->F_in, F_out = (int)a->F_out;
+    float* work = g->work;
+    float* BT = work + pl.off_bt;
+    float* dsp = work + pl.off_dsp;
+    float* part = work + pl.off_part;
+    if (a->M == 0) {  // no rows: all parameter gradients are zero
+        if (hipMemsetAsync(g->dW, 0, sizeof(float) * ((int64_t)F_out * K + 4 * F_out), s) != hipSuccess)
+            return pg::set_error(PG_ERR_HIP, "pg_directgcn_dense_bwd_f32: memset failed");
+        return PG_OK;
+    }
+    {
+        const int64_t total = (int64_t)K * F_out;
+        const int nb = (int)std::min<int64_t>((total + 255) / 256, 1024);
+        hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed, BT);
+    }
+    Gates gt{a->gate_mode, a->C_in, a->C_out, a->C_directed, a->C_undirected, a->C_all, a->rows};
+    {
+        DgradP p{};
+        p.M = a->M;
+        p.F_in = F_in;
+        p.F_out = F_out;
+        p.N = K;
+        p.dY = g->dY;
+        p.lddy = g->lddy;
+        p.Y = a->Y;
+        p.ldy = a->ldy;
+        p.act = a->act;
+        p.slope = a->slope;
+        p.BT = BT;
+        p.bsum = packed + (int64_t)F_out * K;
+        p.Z = a->Z;
+        p.ldz = a->ldz;
+        p.g = gt;
+        p.dpre = g->dpre;
+        p.ldp = g->ldp;
+        p.dZ = g->dZ;
+        p.lddz = g->lddz;
+        p.dres = g->dres;
+        p.lddres = g->lddres;
+        p.gates = g->gates;
+        p.dsp = dsp;
+        p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+        const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
+        hipLaunchKernelGGL((dgrad_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
+    }
+    {
+        const int nb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);
+        hipLaunchKernelGGL(gate_grad_kernel, dim3(nb), dim3(256), 0, s, a->M, pl.ntn, (const float*)dsp, gt, g->dgate);
+    }
+    {
+        WgradP w{};
+        w.M = a->M;
+        w.P = F_out;
+        w.N = K;
+        w.F_in = F_in;
+        w.A = g->dpre;
+        w.lda = g->ldp;
+        w.Z = a->Z;
+        w.ldz = a->ldz;
+        w.R = a->res_x;
+        w.ldr = a->ld_res;
+        w.gates = g->gates;
+        w.rows_per_split = pl.rows_per_split;
+        w.part_stride = pl.part_stride;
+        w.part = part;
+        dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
+        hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
+    }
+    {
+        const int64_t n4 = pl.part_stride / 4;
+        const int nb = (int)std::min<int64_t>((n4 + 255) / 256, 1024);
+        // F_out % 4 == 0, so part_stride == F_out*K + 4*F_out == the dW buffer
+        hipLaunchKernelGGL(reduce_splits_kernel, dim3(nb), dim3(256), 0, s, n4, pl.splits, pl.part_stride,
+                           (const float*)part, g->dW);
+    }
+    return pg::check_launch("pg_directgcn_dense_bwd_f32");
+}
+
+}  // extern "C"

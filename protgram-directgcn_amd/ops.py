@@ -1,8 +1,9 @@
 """Torch-facing wrappers of the C-ABI kernels and their autograd rules.
 
 Forward passes run only in the HIP library (``libpgdgcn.so``) on the caller's current HIP stream.
-Backward passes use the same library for the sparse transposed propagation (``pg_spmm3t_f32`` /
-``pg_spmm1_f32``) and torch GPU ops for the small dense gradient products. CPU tensors are rejected:
+Backward passes use the same library: the sparse transposed propagation (``pg_spmm3t_f32`` /
+``pg_spmm1_f32``) and the dense layer backward (``pg_directgcn_dense_bwd_f32``; torch GPU ops only for
+shapes it does not take, F_in or F_out not a multiple of 4). CPU tensors are rejected:
 there is no CPU implementation of the product path.
 """
 from __future__ import annotations
@@ -86,7 +87,7 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
         if rc == 0:
             _ev_end(x, ev)
             return Z
-        if rc != -3:  # PG_ERR_UNSUPPORTED -> the untiled kernel below
+        if rc != _lib.PG_ERR_UNSUPPORTED:  # -> the untiled kernel below
             check(rc, "pg_spmm3_tiled_f32")
     if g.shared:
         if fused:
@@ -183,15 +184,11 @@ _PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in"
               "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared")
 
 
-def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
-                act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
-    """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header)."""
-    lib = load_library()
-    _require_gpu(Z)
-    packed = pack_weights(prm, W_res, b_res)
+def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None,
+                act: bool = False, slope: float = LEAKY_SLOPE, Y=None):
+    """pg_layer_args_t for the forward block; returns (args, keep-alive list)."""
     M, F_in = Z.size(0), Z.size(1) // 3
     F_out = prm["W_main_in"].size(0)
-    Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
     keep = []
 
     def c(t):
@@ -203,7 +200,7 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
     a = LayerArgs()
     a.M, a.F_in, a.F_out = M, F_in, F_out
-    Zc = _f32c(Z)
+    Zc = _f32c(Z.detach())
     a.Z, a.ldz = c(Zc), Zc.stride(0)
     a.gate_mode = gate_mode
     a.C_in, a.C_out, a.C_directed = c(prm["C_in"]), c(prm["C_out"]), c(prm["C_directed"])
@@ -217,10 +214,72 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
         a.res_x, a.ld_res = _p(rx), rx.stride(0)
     a.W_res = c(W_res)
     a.act, a.slope = int(bool(act)), float(slope)
+    if Y is not None:
+        a.Y, a.ldy = c(Y), Y.stride(0)
+    return a, keep
+
+
+def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
+                act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
+    """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header)."""
+    lib = load_library()
+    _require_gpu(Z)
+    packed = pack_weights(prm, W_res, b_res)
+    M = Z.size(0)
+    F_out = prm["W_main_in"].size(0)
+    Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
     check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
+    del keep
     return Y
+
+
+def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
+                         act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None):
+    """pg_directgcn_dense_bwd_f32. Returns None when the shape is not supported by the HIP kernels
+    (F_in / F_out not multiples of 4), else a dict with
+      dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
+      dgate [5, M] (per-row grads of c_in, c_out, c_directed, c_undirected, c_all),
+      dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out]."""
+    lib = load_library()
+    _require_gpu(dY, Z, Y)
+    M, F_in = Z.size(0), Z.size(1) // 3
+    F_out = prm["W_main_in"].size(0)
+    if F_in % 4 or F_out % 4:
+        return None
+    packed = pack_weights(prm, W_res, b_res)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, None, res_x, W_res, act, slope, Y=Y)
+    dev = Z.device
+    K = (4 if W_res is not None else 3) * F_in
+    dYc = _f32c(dY)
+    dpre = torch.empty(M, F_out, device=dev)
+    dZ = torch.empty(M, 3 * F_in, device=dev)
+    dres = torch.empty(M, F_in, device=dev) if W_res is not None else None
+    dgate = torch.empty(5, M, device=dev)
+    gates = torch.empty(M, 4, device=dev)
+    dW = torch.empty(F_out * K + 4 * F_out, device=dev)
+    nwork = lib.pg_directgcn_dense_bwd_workspace(ctypes.byref(a))
+    if nwork < 0:
+        raise RuntimeError("pg_directgcn_dense_bwd_workspace: bad arguments")
+    work = torch.empty(max(int(nwork), 4), device=dev)
+    g = _lib.LayerGradArgs()
+    g.dY, g.lddy = _p(dYc), dYc.stride(0)
+    g.dpre, g.ldp = _p(dpre), dpre.stride(0)
+    g.dZ, g.lddz = _p(dZ), dZ.stride(0)
+    if dres is not None:
+        g.dres, g.lddres = _p(dres), dres.stride(0)
+    g.dgate, g.gates, g.dW = _p(dgate), _p(gates), _p(dW)
+    g.work, g.work_floats = _p(work), work.numel()
+    fl = default_flags() if flags is None else flags
+    rc = lib.pg_directgcn_dense_bwd_f32(ctypes.byref(a), _p(packed), ctypes.byref(g), fl, _stream(Z))
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_directgcn_dense_bwd_f32")
+    del keep
+    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate,
+            "dB": dW[:F_out * K].view(F_out, K), "dbsum": dW[F_out * K:].view(4, F_out)}
 
 
 def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
@@ -273,10 +332,51 @@ _DENSE_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in
                "C_in", "C_out", "C_directed", "C_undirected", "C_all")
 
 
+def _dense_backward_torch(dY, Z, Y, prm, gate_mode, rows, res_x, W_res, act, slope):
+    """The dense backward as torch GPU ops (shapes the HIP kernels do not take: F_in or F_out % 4 != 0).
+    Same outputs as layer_dense_backward."""
+    M, F_in = Z.size(0), Z.size(1) // 3
+    dpre = dY * torch.where(Y > 0, 1.0, slope) if act else dY
+
+    def gate(name):
+        v = prm[name]
+        if gate_mode == 1:
+            return v.reshape(1, 1).expand(M, 1)
+        return (v[rows] if rows is not None else v[:M]).reshape(M, 1)
+
+    ci, co, cd, cu, ca = (gate(k) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"))
+    cad = ca * cd
+    s = [cad * ci, cad * co, ca * cu]
+    Wp = [prm["W_main_in"] + prm["W_shared"], prm["W_main_out"] + prm["W_shared"],
+          prm["W_undirected"] + prm["W_shared"]]
+    bp = [prm["b_main_in"] + prm["b_dir_shared_in"], prm["b_main_out"] + prm["b_dir_shared_out"],
+          prm["b_undirected"] + prm["b_undirected_shared"]]
+    dZ = torch.empty_like(Z)
+    ds, dB, db = [], [], []
+    for k in range(3):
+        Zk = Z[:, k * F_in:(k + 1) * F_in]
+        Gk = dpre @ Wp[k]
+        dZ[:, k * F_in:(k + 1) * F_in] = s[k] * Gk
+        ds.append((Gk * Zk).sum(1, keepdim=True) + dpre @ bp[k].reshape(-1, 1))
+        sd = s[k] * dpre
+        dB.append(sd.t() @ Zk)
+        db.append(sd.sum(0))
+    dres = None
+    if W_res is not None:
+        dres = dpre @ W_res
+        dB.append(dpre.t() @ res_x)
+    db.append(dpre.sum(0) if W_res is not None else torch.zeros_like(db[0]))
+    dgate = torch.stack([(ds[0] * cad).reshape(M), (ds[1] * cad).reshape(M),
+                         (ds[0] * ca * ci + ds[1] * ca * co).reshape(M), (ds[2] * ca).reshape(M),
+                         (ds[0] * cd * ci + ds[1] * cd * co + ds[2] * cu).reshape(M)])
+    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "dB": torch.cat(dB, 1),
+            "dbsum": torch.stack(db)}
+
+
 class LayerDense(torch.autograd.Function):
     """Y = act(sum_k s_k (Z_k W_k'^T + b_k') + constant[rows] + residual) (pg_directgcn_dense_f32).
 
-    Backward (GPU torch ops; dX of the propagation is handled by Propagate3):
+    Backward: pg_directgcn_dense_bwd_f32 (dX of the propagation is handled by Propagate3):
       G = dpre [W_in' | W_out' | W_und']  ->  dZ_k = s_k G_k,  ds_k = <G_k, Z_k> + <dpre, b_k'>
       dW_k' = (s_k dpre)^T Z_k,  db_k' = sum_m s_k dpre,  and the chain rule through s_k(c)."""
 
@@ -302,56 +402,33 @@ class LayerDense(torch.autograd.Function):
         constant = constant if ctx.has_const else None
         W_res = W_res if ctx.has_wres else None
         rows = rows if ctx.has_rows else None
-        M = Z.size(0)
-        F_in = Z.size(1) // 3
-        dpre = dY * torch.where(Y > 0, 1.0, ctx.slope) if ctx.act else dY
-
-        # gates
-        def gate(name):
-            v = prm[name]
-            if ctx.gate_mode == 1:
-                return v.reshape(1, 1).expand(M, 1)
-            idx = rows if rows is not None else None
-            return (v[idx] if idx is not None else v[:M]).reshape(M, 1)
-
-        ci, co, cd, cu, ca = (gate(k) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"))
-        cad = ca * cd
-        s = [cad * ci, cad * co, ca * cu]
-        Wp = [prm["W_main_in"] + prm["W_shared"], prm["W_main_out"] + prm["W_shared"],
-              prm["W_undirected"] + prm["W_shared"]]
-        bp = [prm["b_main_in"] + prm["b_dir_shared_in"], prm["b_main_out"] + prm["b_dir_shared_out"],
-              prm["b_undirected"] + prm["b_undirected_shared"]]
-        Zk = [Z[:, k * F_in:(k + 1) * F_in] for k in range(3)]
-        dZ = torch.empty_like(Z)
-        ds, dWp, dbp = [], [], []
-        for k in range(3):
-            Gk = dpre @ Wp[k]  # [M, F_in]
-            dZ[:, k * F_in:(k + 1) * F_in] = s[k] * Gk
-            ds.append((Gk * Zk[k]).sum(1, keepdim=True) + dpre @ bp[k].reshape(-1, 1))
-            sd = s[k] * dpre
-            dWp.append(sd.t() @ Zk[k])
-            dbp.append(sd.sum(0))
+        out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
+                                   act=ctx.act, slope=ctx.slope)
+        if out is None:  # F_in / F_out not multiples of 4: the same algebra as torch GPU ops
+            out = _dense_backward_torch(dY, Z, Y, prm, ctx.gate_mode, rows, res_x, W_res, ctx.act, ctx.slope)
+        dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]
+        M, F_in = Z.size(0), Z.size(1) // 3
         g = {}
-        g["W_main_in"], g["W_main_out"], g["W_undirected"] = dWp
-        g["W_shared"] = dWp[0] + dWp[1] + dWp[2]
-        g["b_main_in"] = g["b_dir_shared_in"] = dbp[0]
-        g["b_main_out"] = g["b_dir_shared_out"] = dbp[1]
-        g["b_undirected"] = g["b_undirected_shared"] = dbp[2]
-        dci = ds[0] * cad
-        dco = ds[1] * cad
-        dcd = ds[0] * ca * ci + ds[1] * ca * co
-        dcu = ds[2] * ca
-        dca = ds[0] * cd * ci + ds[1] * cd * co + ds[2] * cu
-        for name, dv in (("C_in", dci), ("C_out", dco), ("C_directed", dcd), ("C_undirected", dcu), ("C_all", dca)):
+        g["W_main_in"] = dB[:, :F_in]
+        g["W_main_out"] = dB[:, F_in:2 * F_in]
+        g["W_undirected"] = dB[:, 2 * F_in:3 * F_in]
+        g["W_shared"] = g["W_main_in"] + g["W_main_out"] + g["W_undirected"]
+        g["b_main_in"] = g["b_dir_shared_in"] = dbsum[0]
+        g["b_main_out"] = g["b_dir_shared_out"] = dbsum[1]
+        g["b_undirected"] = g["b_undirected_shared"] = dbsum[2]
+        for q, name in enumerate(("C_in", "C_out", "C_directed", "C_undirected", "C_all")):
             v = prm[name]
+            if not ctx.needs_input_grad[9 + _DENSE_KEYS.index(name)]:
+                continue
             if ctx.gate_mode == 1:
-                g[name] = dv.sum().reshape(v.shape)
+                g[name] = dgate[q].sum().reshape(v.shape)
+            elif rows is not None:
+                g[name] = torch.zeros_like(v).index_add_(0, rows, dgate[q].reshape(-1, *v.shape[1:]))
+            elif v.size(0) == M:
+                g[name] = dgate[q].reshape(v.shape)
             else:
                 full = torch.zeros_like(v)
-                if rows is not None:
-                    full.index_add_(0, rows, dv)
-                else:
-                    full[:M] += dv
+                full[:M] = dgate[q].reshape(M, *v.shape[1:])
                 g[name] = full
         d_const = None
         if constant is not None and ctx.needs_input_grad[2]:
@@ -365,8 +442,8 @@ class LayerDense(torch.autograd.Function):
             if W_res is None:
                 d_res = dpre
             else:
-                d_res = dpre @ W_res
-                d_wres = dpre.t() @ res_x
-                d_bres = dpre.sum(0)
+                d_res = out["dres"]
+                d_wres = dB[:, 3 * F_in:4 * F_in]
+                d_bres = dbsum[3]
         grads = [g[k] if ctx.needs_input_grad[9 + i] else None for i, k in enumerate(_DENSE_KEYS)]
         return (dZ, d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)

@@ -399,3 +399,93 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
                               W_res=None if W_res is None else W_res.to(cuda),
                               b_res=None if b_res is None else b_res.to(cuda), act=True, flags=fl)
         assert_close(out, y.float(), f"dense flags={fl}", rtol=2e-5, atol=2e-5)
+
+
+def _dense_case(M, Fin, Fout, proj, vec, rows, seed):
+    g = torch.Generator().manual_seed(seed)
+    Ntot = M + 37
+    Z = torch.randn(M, 3 * Fin, generator=g)
+    xres = torch.randn(M, Fin, generator=g)
+    prm = {k: torch.randn(Fout, Fin, generator=g) * 0.1 for k in ("W_main_in", "W_main_out", "W_undirected", "W_shared")}
+    for k in ("b_main_in", "b_dir_shared_in", "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared"):
+        prm[k] = torch.randn(Fout, generator=g) * 0.1
+    for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+        prm[k] = torch.rand((Ntot, 1) if vec else (1,), generator=g) + 0.5
+    const = torch.randn(Ntot, Fout, generator=g) if vec else None
+    r = torch.randperm(Ntot, generator=g)[:M] if rows else None
+    W_res = torch.randn(Fout, Fin, generator=g) * 0.1 if proj else None
+    b_res = torch.randn(Fout, generator=g) * 0.1 if proj else None
+    if not proj and Fin != Fout:
+        xres = None
+    dY = torch.randn(M, Fout, generator=g)
+    return Z, xres, prm, const, r, W_res, b_res, dY
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
+                                                      (300, 32, 16, False, False, False), (513, 20, 12, True, True, False),
+                                                      (129, 16, 40, True, True, True), (64, 128, 96, False, True, True),
+                                                      (5000, 32, 32, False, True, False), (300, 18, 10, True, True, False)])
+@pytest.mark.parametrize("hip", [True, False])
+def test_dense_backward_vs_float64(pkg, cuda, monkeypatch, M, Fin, Fout, proj, vec, rows, hip):
+    """Autograd of the fused dense layer (pg_directgcn_dense_bwd_f32, or the torch-GPU path for shapes it
+    does not take) against float64 autograd of protgram_directgcn.py:100-133 + residual + leaky_relu."""
+    from protgram_directgcn_amd import ops
+    if not hip:
+        monkeypatch.setattr(ops, "layer_dense_backward", lambda *a, **k: None)
+    Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, vec, rows, 7 * M + Fin)
+    gate = 0 if vec else 1
+    # float64 reference through autograd
+    d = {k: v.double().requires_grad_(True) for k, v in prm.items()}
+    Zd = Z.double().requires_grad_(True)
+    xd = xres.double().requires_grad_(True) if xres is not None else None
+    cd = const.double().requires_grad_(True) if const is not None else None
+    Wrd = W_res.double().requires_grad_(True) if proj else None
+    brd = b_res.double().requires_grad_(True) if proj else None
+    idx = r if r is not None else torch.arange(M)
+    gv = (lambda k: d[k][idx]) if vec else (lambda k: d[k].expand(M, 1))
+    s = [gv("C_all") * gv("C_directed") * gv("C_in"), gv("C_all") * gv("C_directed") * gv("C_out"),
+         gv("C_all") * gv("C_undirected")]
+    Wk = [d["W_main_in"] + d["W_shared"], d["W_main_out"] + d["W_shared"], d["W_undirected"] + d["W_shared"]]
+    bk = [d["b_main_in"] + d["b_dir_shared_in"], d["b_main_out"] + d["b_dir_shared_out"],
+          d["b_undirected"] + d["b_undirected_shared"]]
+    y = sum(s[k] * (Zd[:, k * Fin:(k + 1) * Fin] @ Wk[k].t() + bk[k]) for k in range(3))
+    if cd is not None:
+        y = y + cd[idx]
+    if xd is not None:
+        y = y + (xd @ Wrd.t() + brd if proj else xd)
+    y = torch.nn.functional.leaky_relu(y, 0.01)
+    (y * dY.double()).sum().backward()
+    # device path
+    dv = {k: v.to(cuda).requires_grad_(True) for k, v in prm.items()}
+    Zg = Z.to(cuda).requires_grad_(True)
+    xg = xres.to(cuda).requires_grad_(True) if xres is not None else None
+    cg = const.to(cuda).requires_grad_(True) if const is not None else None
+    Wrg = W_res.to(cuda).requires_grad_(True) if proj else None
+    brg = b_res.to(cuda).requires_grad_(True) if proj else None
+    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01,
+                               *[dv[k] for k in ops._DENSE_KEYS])
+    assert_close(out, y.detach().float(), "forward", rtol=2e-5, atol=2e-5)
+    out.backward(dY.to(cuda))
+    assert_grad_close(Zg.grad, Zd.grad, "dZ")
+    for k in ops._DENSE_KEYS:
+        assert_grad_close(dv[k].grad, d[k].grad, f"d{k}")
+    if xg is not None:
+        assert_grad_close(xg.grad, xd.grad, "dres_x")
+    if cg is not None:
+        assert_grad_close(cg.grad, cd.grad, "dconstant")
+    if proj:
+        assert_grad_close(Wrg.grad, Wrd.grad, "dW_res")
+        assert_grad_close(brg.grad, brd.grad, "db_res")
+
+
+def test_dense_backward_deterministic(pkg, cuda):
+    from protgram_directgcn_amd import ops
+    Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(20000, 128, 128, False, True, False, 3)
+    dv = {k: v.to(cuda) for k, v in prm.items()}
+    Zg, dYg = Z.to(cuda), dY.to(cuda)
+    Y = ops.layer_dense(Zg, dv, 0, res_x=xres.to(cuda), act=True)
+    a = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xres.to(cuda), act=True)
+    b = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xres.to(cuda), act=True)
+    assert a is not None
+    for k in ("dpre", "dZ", "dgate", "dB", "dbsum"):
+        assert torch.equal(a[k], b[k]), k

@@ -318,20 +318,29 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     b = torch.empty_like(a)
     ms = timeit(lambda: b.copy_(a))
     res["copy_GBs"] = round(2 * a.numel() * 4 / ms / 1e6, 1)
-    # training step (fwd + bwd + Adam)
+    # training step: the reference trainer's loop (protgram_directgcn_trainer.py:91-100: autocast +
+    # GradScaler + L2 term + Adam(wd=0)), and the same without autocast/GradScaler
     model.train()
     y = (torch.arange(x.size(0), device=x.device) // (20 ** 3)).clamp(max=19)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
+    scaler = torch.amp.GradScaler("cuda", enabled=True)
     import torch.nn.functional as F
 
-    def train_step():
+    def train_step(amp):
         opt.zero_grad()
-        lp, _ = model(data)
-        loss = F.nll_loss(lp, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters())
-        loss.backward()
-        opt.step()
+        with torch.amp.autocast("cuda", enabled=amp):
+            lp, _ = model(data)
+            loss = F.nll_loss(lp, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters() if p.requires_grad)
+        if amp:
+            scaler.scale(loss).backward()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            loss.backward()
+            opt.step()
 
-    res["train_step_ms"] = round(timeit(train_step, reps=5), 3)
+    res["train_step_ms"] = round(timeit(lambda: train_step(False), reps=5), 3)
+    res["train_step_trainer_amp_ms"] = round(timeit(lambda: train_step(True), reps=5), 3)
     model.eval()
     log(f"[bench] extra: {json.dumps(res)}")
     return res

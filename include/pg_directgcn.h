@@ -227,6 +227,16 @@ int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* args);
 int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* args, const float* packed, const pg_layer_grad_args_t* grads,
                                uint32_t flags, void* stream);
 
+/* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
+ * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
+ * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of
+ * protgram_directgcn.py:173-177 (M = graph nodes, P, N <= a few hundred) in training. Deterministic
+ * split-K MFMA (same kernel as the dense backward). Needs P, N, lda, ldb multiples of 4 and 16-B aligned
+ * buffers (else PG_ERR_UNSUPPORTED). work: pg_gemm_at_b_workspace(M, P, N) floats. */
+int64_t pg_gemm_at_b_workspace(int64_t M, int64_t P, int64_t N);
+int pg_gemm_at_b_f32(int64_t M, int64_t P, int64_t N, const float* A, int64_t lda, const float* B, int64_t ldb,
+                     float* out, float* work, int64_t work_floats, void* stream);
+
 /* Fused prediction head (protgram_directgcn.py:218-222, eval mode): per row m of h [M, F]
  *   logp[m] = log_softmax(W2 relu(W1 h[m] + b1) + b2)      W1 [H, F], W2 [C, H] (nn.Linear layout)
  *   emb[m]  = h[m] / (||h[m]||_2 + eps)                      (models_utils.py:139-147)

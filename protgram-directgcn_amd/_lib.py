@@ -85,6 +85,8 @@ SIGNATURES = {
     "pg_directgcn_dense_bwd_workspace": (c_i64, [ctypes.POINTER(LayerArgs)]),
     "pg_directgcn_dense_bwd_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
                                                   c_u32, c_vp]),
+    "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),
+    "pg_gemm_at_b_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                              c_vp, c_i64, c_vp, c_i64, c_vp]),
 }

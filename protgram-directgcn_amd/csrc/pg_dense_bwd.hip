@@ -489,19 +489,45 @@ __global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
     }
 }
 
+// out[c] = sum_s part[s][c]. A block owns 32 consecutive float4 columns (512 contiguous bytes per split);
+// its 8 thread groups take every 8th split and are combined in group order: deterministic, and enough
+// loads in flight to stream the partials at HBM rate.
+constexpr int RS_COLS = 32, RS_GROUPS = 8;
 __global__ __launch_bounds__(256) void reduce_splits_kernel(int64_t n4, int splits, int64_t stride, const float* part,
                                                             float* out) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-        float4 s = ld4(part + 4 * i);
-        for (int k = 1; k < splits; ++k) {
-            const float4 v = ld4(part + (int64_t)k * stride + 4 * i);
-            s.x += v.x;
-            s.y += v.y;
-            s.z += v.z;
-            s.w += v.w;
+    __shared__ float4 acc_s[RS_GROUPS][RS_COLS];
+    const int c = threadIdx.x % RS_COLS, grp = threadIdx.x / RS_COLS;
+    const int64_t i = (int64_t)blockIdx.x * RS_COLS + c;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    if (i < n4) {
+        int k = grp;
+        for (; k + RS_GROUPS < splits; k += 2 * RS_GROUPS) {  // two independent chains
+            const float4 u = ld4(part + (int64_t)k * stride + 4 * i);
+            const float4 v = ld4(part + (int64_t)(k + RS_GROUPS) * stride + 4 * i);
+            s0.x += u.x; s0.y += u.y; s0.z += u.z; s0.w += u.w;
+            s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
         }
-        st4(out + 4 * i, s);
+        if (k < splits) {
+            const float4 u = ld4(part + (int64_t)k * stride + 4 * i);
+            s0.x += u.x; s0.y += u.y; s0.z += u.z; s0.w += u.w;
+        }
     }
+    acc_s[grp][c] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
+    __syncthreads();
+    if (grp == 0 && i < n4) {
+        float4 t = acc_s[0][c];
+        for (int g = 1; g < RS_GROUPS; ++g) {
+            const float4 v = acc_s[g][c];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+        }
+        st4(out + 4 * i, t);
+    }
+}
+
+void launch_reduce(int64_t n4, int splits, int64_t stride, const float* part, float* out, hipStream_t s) {
+    const int64_t nb = (n4 + RS_COLS - 1) / RS_COLS;
+    hipLaunchKernelGGL(reduce_splits_kernel, dim3((unsigned)nb), dim3(RS_COLS * RS_GROUPS), 0, s, n4, splits, stride,
+                       part, out);
 }
 
 constexpr int DG_BM = 128, DG_BN = 128, DG_NW = 8, WG_NW = 8;
@@ -512,20 +538,35 @@ struct BwdPlan {
     int64_t off_bt, off_dsp, off_part, total;
 };
 
-BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
-    BwdPlan b{};
-    b.K = (int)((proj ? 4 : 3) * F_in);
-    b.ntn = (b.K + DG_BN - 1) / DG_BN;
-    const int64_t tiles = ((F_out + 127) / 128) * ((b.K + 127) / 128);
+struct SplitPlan {
+    int splits;
+    int64_t rows_per_split;
+};
+
+// Row splits for wgrad_kernel: about 512 blocks (2 per CU), whole 32-row chunks per split.
+SplitPlan split_rows(int64_t M, int64_t tiles) {
+    SplitPlan sp{};
     int64_t splits = (512 + tiles - 1) / tiles;
     const int64_t chunks = (M + WROWS - 1) / WROWS;
     if (splits > chunks) splits = chunks;
     if (splits < 1) splits = 1;
-    b.rows_per_split = ((chunks + splits - 1) / splits) * WROWS;
-    b.splits = (int)((M + b.rows_per_split - 1) / b.rows_per_split);
-    if (b.splits < 1) b.splits = 1;
-    b.part_stride = ((F_out * b.K + 4 * F_out + 3) / 4) * 4;
-    auto up4 = [](int64_t v) { return (v + 3) / 4 * 4; };
+    sp.rows_per_split = ((chunks + splits - 1) / splits) * WROWS;
+    if (sp.rows_per_split < WROWS) sp.rows_per_split = WROWS;
+    sp.splits = (int)((M + sp.rows_per_split - 1) / sp.rows_per_split);
+    if (sp.splits < 1) sp.splits = 1;
+    return sp;
+}
+
+int64_t up4(int64_t v) { return (v + 3) / 4 * 4; }
+
+BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
+    BwdPlan b{};
+    b.K = (int)((proj ? 4 : 3) * F_in);
+    b.ntn = (b.K + DG_BN - 1) / DG_BN;
+    const SplitPlan sp = split_rows(M, ((F_out + 127) / 128) * ((b.K + 127) / 128));
+    b.splits = sp.splits;
+    b.rows_per_split = sp.rows_per_split;
+    b.part_stride = up4(F_out * b.K + 4 * F_out);
     b.off_bt = 0;
     b.off_dsp = up4((int64_t)b.K * F_out);
     b.off_part = b.off_dsp + up4((int64_t)b.ntn * 3 * M);
@@ -641,14 +682,56 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
         hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
     }
-    {
-        const int64_t n4 = pl.part_stride / 4;
-        const int nb = (int)std::min<int64_t>((n4 + 255) / 256, 1024);
-        // F_out % 4 == 0, so part_stride == F_out*K + 4*F_out == the dW buffer
-        hipLaunchKernelGGL(reduce_splits_kernel, dim3(nb), dim3(256), 0, s, n4, pl.splits, pl.part_stride,
-                           (const float*)part, g->dW);
-    }
+    // F_out % 4 == 0, so part_stride == F_out*K + 4*F_out == the dW buffer
+    launch_reduce(pl.part_stride / 4, pl.splits, pl.part_stride, part, g->dW, s);
     return pg::check_launch("pg_directgcn_dense_bwd_f32");
+}
+
+int64_t pg_gemm_at_b_workspace(int64_t M, int64_t P, int64_t N) {
+    if (M < 0 || P <= 0 || N <= 0) return -1;
+    const SplitPlan sp = split_rows(M, ((P + 127) / 128) * ((N + 127) / 128));
+    return (int64_t)sp.splits * up4(P * N + 4 * P);
+}
+
+int pg_gemm_at_b_f32(int64_t M, int64_t P, int64_t N, const float* A, int64_t lda, const float* B, int64_t ldb,
+                     float* out, float* work, int64_t work_floats, void* stream) {
+    PG_REQUIRE(M >= 0 && P > 0 && N > 0 && P < (1 << 20) && N < (1 << 20), "bad shape M=%lld P=%lld N=%lld",
+               (long long)M, (long long)P, (long long)N);
+    PG_REQUIRE(out != nullptr && (M == 0 || (A && B && work)), "null buffer");
+    PG_REQUIRE(lda >= P && ldb >= N, "leading dimensions too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) {
+        if (hipMemsetAsync(out, 0, sizeof(float) * (P * N + P), s) != hipSuccess)
+            return pg::set_error(PG_ERR_HIP, "pg_gemm_at_b_f32: memset failed");
+        return PG_OK;
+    }
+    if (P % 4 || N % 4 || lda % 4 || ldb % 4 || !pg::aligned16(A) || !pg::aligned16(B) || !pg::aligned16(out) ||
+        !pg::aligned16(work))
+        return pg::set_error(PG_ERR_UNSUPPORTED,
+                             "pg_gemm_at_b_f32: needs P, N, lda, ldb multiples of 4 and 16-B aligned buffers");
+    const SplitPlan sp = split_rows(M, ((P + 127) / 128) * ((N + 127) / 128));
+    const int64_t stride = up4(P * N + 4 * P);
+    PG_REQUIRE(work_floats >= (int64_t)sp.splits * stride, "workspace too small: %lld < %lld floats",
+               (long long)work_floats, (long long)sp.splits * stride);
+    WgradP w{};
+    w.M = M;
+    w.P = (int)P;
+    w.N = (int)N;
+    w.F_in = (int)N;  // one segment, unit scales
+    w.A = A;
+    w.lda = lda;
+    w.Z = B;
+    w.ldz = ldb;
+    w.R = nullptr;
+    w.ldr = 0;
+    w.gates = nullptr;
+    w.rows_per_split = sp.rows_per_split;
+    w.part_stride = stride;
+    w.part = work;
+    dim3 grid((unsigned)((N + 127) / 128), (unsigned)((P + 127) / 128), (unsigned)sp.splits);
+    hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
+    launch_reduce((P * N + P) / 4, sp.splits, stride, work, out, s);  // C, then colsum(A) (db row 0)
+    return pg::check_launch("pg_gemm_at_b_f32");
 }
 
 }  // extern "C"

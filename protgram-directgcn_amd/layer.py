@@ -239,10 +239,15 @@ class ProtGramDirectGCN(nn.Module):
 
     def head(self, h):
         """decoder_fc -> log_softmax, and l2_normalize (protgram_directgcn.py:218-222). Inference (eval, no
-        autograd) runs the fused pg_directgcn_head_f32 kernel; training keeps torch's autograd."""
+        autograd) runs the fused pg_directgcn_head_f32 kernel; training runs the decoder Linears through
+        ops.row_linear (weight gradients in pg_gemm_at_b_f32)."""
         dec = self.decoder_fc
         if not self.training and not torch.is_grad_enabled() and h.is_cuda:
             return ops.head(h, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias, self.l2_eps)
-        logits = dec(h)
+        if h.is_cuda and len(dec) == 4 and isinstance(dec[0], nn.Linear) and isinstance(dec[3], nn.Linear):
+            a = dec[2](dec[1](ops.row_linear(h, dec[0].weight, dec[0].bias)))  # Linear, ReLU, Dropout
+            logits = ops.row_linear(a, dec[3].weight, dec[3].bias)
+        else:
+            logits = dec(h)
         emb = h / (torch.norm(h, p=2, dim=1, keepdim=True) + self.l2_eps)  # models_utils.py:139-147
         return F.log_softmax(logits, dim=-1), emb

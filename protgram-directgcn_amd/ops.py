@@ -298,18 +298,46 @@ def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
     return logp, emb
 
 
+def gemm_at_b(A: torch.Tensor, B: torch.Tensor):
+    """pg_gemm_at_b_f32: (A^T B [P, N], column sums of A [P]) over the M rows, or None when the shape is not
+    taken (P or N not a multiple of 4)."""
+    lib = load_library()
+    _require_gpu(A, B)
+    A, B = _f32c(A), _f32c(B)
+    M, P = A.shape
+    N = B.size(1)
+    if P % 4 or N % 4:
+        return None
+    out = torch.empty(P * N + P, device=A.device, dtype=torch.float32)
+    nwork = int(lib.pg_gemm_at_b_workspace(M, P, N))
+    work = torch.empty(max(nwork, 4), device=A.device, dtype=torch.float32)
+    rc = lib.pg_gemm_at_b_f32(M, P, N, _p(A), A.stride(0), _p(B), B.stride(0), _p(out), _p(work), work.numel(),
+                              _stream(A))
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_gemm_at_b_f32")
+    return out[:P * N].view(P, N), out[P * N:]
+
+
 # ------------------------------------------------------------------------------------------------
 # autograd
 # ------------------------------------------------------------------------------------------------
+# The reference trainer runs the model under torch.amp.autocast (protgram_directgcn_trainer.py:93):
+# the Functions below take fp32 inputs and compute in fp32 inside autocast regions (at least the
+# reference's precision; the kernels are fp32-only).
+_fwd32 = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+_bwd32 = torch.amp.custom_bwd(device_type="cuda")
 class Propagate3(torch.autograd.Function):
     """x [N, F] -> Z [N, 3F] = [A_in x | A_out x | A_und x]; backward = transposed propagation."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, x, g: CSRGraph, fused: bool = False):
         ctx.g = g
         return spmm3(g, x, fused=fused)
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dZ):
         if not ctx.needs_input_grad[0]:
             return None, None, None
@@ -318,11 +346,13 @@ class Propagate3(torch.autograd.Function):
 
 class Propagate1(torch.autograd.Function):
     @staticmethod
+    @_fwd32
     def forward(ctx, x, a: ShapedAdjacency):
         ctx.a = a
         return spmm1(a, x)
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dY):
         return spmm1(ctx.a, dY, transpose=True), None
 
@@ -381,6 +411,7 @@ class LayerDense(torch.autograd.Function):
       dW_k' = (s_k dpre)^T Z_k,  db_k' = sum_m s_k dpre,  and the chain rule through s_k(c)."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, Z, res_x, constant, W_res, b_res, rows, gate_mode, act, slope, *params):
         prm = dict(zip(_DENSE_KEYS, params))
         Y = layer_dense(Z, prm, gate_mode, rows=rows, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
@@ -395,6 +426,7 @@ class LayerDense(torch.autograd.Function):
         return Y
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dY):
         Z, res_x, constant, W_res, rows, Y, *params = ctx.saved_tensors
         prm = dict(zip(_DENSE_KEYS, params))
@@ -447,3 +479,35 @@ class LayerDense(torch.autograd.Function):
                 d_bres = dbsum[3]
         grads = [g[k] if ctx.needs_input_grad[9 + i] else None for i, k in enumerate(_DENSE_KEYS)]
         return (dZ, d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)
+
+
+class RowLinear(torch.autograd.Function):
+    """y = x W^T + b over many rows (the decoder nn.Linear layers, protgram_directgcn.py:173-177, in
+    training). Forward and dx = dy W are torch GEMMs; (dW, db) -- a reduction over all M rows, which the
+    library GEMMs tile badly -- run in pg_gemm_at_b_f32."""
+
+    @staticmethod
+    @_fwd32
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        ctx.has_b = b is not None
+        return torch.nn.functional.linear(x, W, b)
+
+    @staticmethod
+    @_bwd32
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dx = dy @ W if ctx.needs_input_grad[0] else None
+        dW = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            r = gemm_at_b(dy, x) if x.dim() == 2 else None
+            if r is None:
+                dW, db = dy.reshape(-1, dy.size(-1)).t() @ x.reshape(-1, x.size(-1)), dy.reshape(-1, dy.size(-1)).sum(0)
+            else:
+                dW, db = r
+        return dx, dW, (db if ctx.has_b else None)
+
+
+def row_linear(x, W, b=None):
+    return RowLinear.apply(x, W, b)
+

@@ -489,3 +489,49 @@ def test_dense_backward_deterministic(pkg, cuda):
     assert a is not None
     for k in ("dpre", "dZ", "dgate", "dB", "dbsum"):
         assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("M,P,N", [(160000, 20, 64), (160000, 64, 128), (1000, 128, 384), (33, 4, 8), (0, 8, 8),
+                                   (70001, 256, 132)])
+def test_gemm_at_b_vs_float64(pkg, cuda, M, P, N):
+    from protgram_directgcn_amd import ops
+    g = torch.Generator().manual_seed(M + P + N)
+    A, B = torch.randn(M, P, generator=g), torch.randn(M, N, generator=g)
+    C, cs = ops.gemm_at_b(A.to(cuda), B.to(cuda))
+    assert_grad_close(C, A.double().t() @ B.double(), "A^T B")
+    assert_grad_close(cs, A.double().sum(0), "colsum")
+    C2, cs2 = ops.gemm_at_b(A.to(cuda), B.to(cuda))
+    assert torch.equal(C, C2) and torch.equal(cs, cs2)
+
+
+def test_training_steps_under_autocast_and_gradscaler(pkg, cuda):
+    """The reference trainer's exact loop (protgram_directgcn_trainer.py:91-100: autocast + GradScaler +
+    L2 term + Adam): the model's Functions compute in fp32 inside autocast, so the steps match the fp32
+    fixture (the GradScaler factor is a power of two: exact)."""
+    import torch.nn.functional as F
+    fx = load("f1_fasta2")
+    ei, ew = graph(fx)
+    dei, dew = dev_graph(ei, ew, cuda)
+    m, dims, N, n, ogd = _model_from_fixture(pkg, fx, cuda)
+    m.eval()
+    data = pkg.Data(x=t(fx["M_x"]).to(cuda), edge_index_in=dei["in"], edge_weight_in=dew["in"],
+                    edge_index_out=dei["out"], edge_weight_out=dew["out"], edge_index_undirected_norm=dei["und"],
+                    edge_weight_undirected_norm=dew["und"])
+    y = t(fx["M_train_y"]).to(cuda)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=0.0)
+    scaler = torch.amp.GradScaler("cuda", enabled=True)
+    losses = []
+    for _ in range(len(fx["M_train_loss"])):
+        opt.zero_grad()
+        with torch.amp.autocast("cuda", enabled=True):
+            out, emb = m(data=data)
+            assert out.dtype == torch.float32 and emb.dtype == torch.float32
+            loss = F.nll_loss(out, y) + 1e-7 * sum(p.norm(2).pow(2) for p in m.parameters() if p.requires_grad)
+        scaler.scale(loss).backward()
+        scaler.step(opt)
+        scaler.update()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, fx["M_train_loss"], rtol=1e-5)
+    ref = params(fx, "M_train_p")
+    for k, v in m.state_dict().items():
+        assert_grad_close(v, ref[k], f"param after 2 autocast steps {k}")

@@ -14,6 +14,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+amp = "--amp" in sys.argv
 dev = torch.device("cuda:0")
 n = 4
 N, s, d, c = pkg.synth.de_bruijn_edges(n)
@@ -27,12 +28,17 @@ opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
 model.train()
 
 
+scaler = torch.amp.GradScaler("cuda", enabled=amp)
+
+
 def step():
     opt.zero_grad()
-    out, _ = model(data=data)
-    loss = F.nll_loss(out, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters() if p.requires_grad)
-    loss.backward()
-    opt.step()
+    with torch.amp.autocast("cuda", enabled=amp):
+        out, _ = model(data=data)
+        loss = F.nll_loss(out, y) + 1e-7 * sum(p.norm(2).pow(2) for p in model.parameters() if p.requires_grad)
+    scaler.scale(loss).backward()
+    scaler.step(opt)
+    scaler.update()
     return loss
 
 
@@ -43,4 +49,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step (amp={amp}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

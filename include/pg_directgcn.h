@@ -202,7 +202,7 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uin
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output
  * (read for leaky_relu' when act != 0); `packed` the forward's packed operand. Outputs:
  *   dpre  [M, F_out]  = dY * leaky'(Y)         (also the identity residual's and the constant's gradient)
- *   dZ    [M, 3F_in]  = s_q * (dpre B_q)        gradient of the propagated aggregates
+ *   dZ    [M, 3F_in]  = s_q * (dpre B_q)        gradient of the propagated aggregates (NULL: not needed)
  *   dres  [M, F_in]   = dpre W_res              projected residual only (W_res != NULL)
  *   dgate [5, M]      per-row dL/d{c_in, c_out, c_directed, c_undirected, c_all} (row m uses gate row r(m))
  *   gates [M, 4]      the row gates s_in, s_out, s_und, 1 (scratch output)

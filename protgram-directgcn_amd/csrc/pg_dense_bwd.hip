@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64 * NW) void dgrad_kernel(DgradP p) {
                 const float4 gv = ld4(&T[rl[u] * TLD + 4 * c4]);
                 if (seg < 3) {
                     const float s = Sg[rl[u] * 4 + seg];
-                    st4(p.dZ + mm[u] * p.lddz + j, make_float4(s * gv.x, s * gv.y, s * gv.z, s * gv.w));
+                    if (p.dZ) st4(p.dZ + mm[u] * p.lddz + j, make_float4(s * gv.x, s * gv.y, s * gv.z, s * gv.w));
                     part = dot4(gv, zv[u]);
                 } else {
                     st4(p.dres + mm[u] * p.lddres + (j - 3 * p.F_in), gv);
@@ -591,7 +591,7 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
     PG_REQUIRE(a->C_in && a->C_out && a->C_directed && a->C_undirected && a->C_all, "null gate");
     PG_REQUIRE(a->gate_mode == PG_GATES_VECTOR || a->gate_mode == PG_GATES_SCALAR, "bad gate_mode");
     PG_REQUIRE(!a->W_res || a->res_x, "W_res needs res_x");
-    PG_REQUIRE(g->dY && g->dpre && g->dZ && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
+    PG_REQUIRE(g->dY && g->dpre && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
     PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
     PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
     const bool proj = a->W_res != nullptr;
@@ -600,17 +600,17 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
                (long long)pl.total);
     // vector paths only: every row / column block is float4
     const bool vec = a->F_in % 4 == 0 && a->F_out % 4 == 0 && a->ldz % 4 == 0 && g->lddy % 4 == 0 &&
-                     g->ldp % 4 == 0 && g->lddz % 4 == 0 && (!a->act || a->ldy % 4 == 0) &&
+                     g->ldp % 4 == 0 && (!a->act || a->ldy % 4 == 0) &&
                      (!proj || (a->ld_res % 4 == 0 && g->lddres % 4 == 0 && pg::aligned16(a->res_x) &&
                                 pg::aligned16(g->dres))) &&
-                     pg::aligned16(a->Z) && pg::aligned16(g->dY) && pg::aligned16(g->dpre) && pg::aligned16(g->dZ) &&
+                     pg::aligned16(a->Z) && pg::aligned16(g->dY) && pg::aligned16(g->dpre) && (!g->dZ || (pg::aligned16(g->dZ) && g->lddz % 4 == 0)) &&
                      pg::aligned16(g->gates) && pg::aligned16(g->dW) && pg::aligned16(g->work) &&
                      pg::aligned16(packed) && (!a->act || pg::aligned16(a->Y));
     if (!vec)
         return pg::set_error(PG_ERR_UNSUPPORTED,
                              "pg_directgcn_dense_bwd_f32: needs F_in, F_out and leading dims multiple of 4 and "
                              "16-B aligned buffers");
-    PG_REQUIRE(a->ldz >= 3 * a->F_in && g->lddz >= 3 * a->F_in && g->lddy >= a->F_out && g->ldp >= a->F_out,
+    PG_REQUIRE(a->ldz >= 3 * a->F_in && (!g->dZ || g->lddz >= 3 * a->F_in) && g->lddy >= a->F_out && g->ldp >= a->F_out,
                "leading dimensions too small");
     hipStream_t s = (hipStream_t)stream;
     const int K = pl.K;

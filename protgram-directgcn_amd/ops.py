@@ -237,7 +237,8 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
-                         act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None):
+                         act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
+                         need_dZ: bool = True):
     """pg_directgcn_dense_bwd_f32. Returns None when the shape is not supported by the HIP kernels
     (F_in / F_out not multiples of 4), else a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
@@ -255,7 +256,7 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     K = (4 if W_res is not None else 3) * F_in
     dYc = _f32c(dY)
     dpre = torch.empty(M, F_out, device=dev)
-    dZ = torch.empty(M, 3 * F_in, device=dev)
+    dZ = torch.empty(M, 3 * F_in, device=dev) if need_dZ else None
     dres = torch.empty(M, F_in, device=dev) if W_res is not None else None
     dgate = torch.empty(5, M, device=dev)
     gates = torch.empty(M, 4, device=dev)
@@ -267,7 +268,8 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     g = _lib.LayerGradArgs()
     g.dY, g.lddy = _p(dYc), dYc.stride(0)
     g.dpre, g.ldp = _p(dpre), dpre.stride(0)
-    g.dZ, g.lddz = _p(dZ), dZ.stride(0)
+    if dZ is not None:
+        g.dZ, g.lddz = _p(dZ), dZ.stride(0)
     if dres is not None:
         g.dres, g.lddres = _p(dres), dres.stride(0)
     g.dgate, g.gates, g.dW = _p(dgate), _p(gates), _p(dW)
@@ -435,7 +437,7 @@ class LayerDense(torch.autograd.Function):
         W_res = W_res if ctx.has_wres else None
         rows = rows if ctx.has_rows else None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
-                                   act=ctx.act, slope=ctx.slope)
+                                   act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
         if out is None:  # F_in / F_out not multiples of 4: the same algebra as torch GPU ops
             out = _dense_backward_torch(dY, Z, Y, prm, ctx.gate_mode, rows, res_x, W_res, ctx.act, ctx.slope)
         dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]

@@ -486,9 +486,12 @@ def test_dense_backward_deterministic(pkg, cuda):
     Y = ops.layer_dense(Zg, dv, 0, res_x=xres.to(cuda), act=True)
     a = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xres.to(cuda), act=True)
     b = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xres.to(cuda), act=True)
-    assert a is not None
+    c = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xres.to(cuda), act=True, need_dZ=False)
+    assert a is not None and c["dZ"] is None
     for k in ("dpre", "dZ", "dgate", "dB", "dbsum"):
         assert torch.equal(a[k], b[k]), k
+        if k != "dZ":
+            assert torch.equal(a[k], c[k]), k
 
 
 @pytest.mark.parametrize("M,P,N", [(160000, 20, 64), (160000, 64, 128), (1000, 128, 384), (33, 4, 8), (0, 8, 8),

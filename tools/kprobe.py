@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Run selected hot-path kernels on the 4-gram workload a few times (target for rocprofv3 --pmc passes).
+"""Run the default hot-path kernels on the 4-gram workload a few times (target for rocprofv3 --pmc passes).
 usage: python tools/kprobe.py [reps]"""
 import dataclasses
 import os
@@ -19,14 +19,20 @@ dev = torch.device("cuda:0")
 N, s, d, c = pkg.synth.de_bruijn_edges(4)
 g = pkg.build_propagation_csr(N, s, d, c, device=dev)
 kin, kout = pkg.graph.class_keys(N, torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev))
-gt = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout))
+gt = dataclasses.replace(g, tiles=pkg.graph.build_row_tiles(g, kin, kout, 128))
 x = torch.randn(N, 128, device=dev)
 torch.manual_seed(0)
 layer = pkg.DirectGCNLayer(128, 128, N).to(dev)
 prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
+W1, b1 = torch.randn(64, 128, device=dev) * 0.1, torch.zeros(64, device=dev)
+W2, b2 = torch.randn(20, 64, device=dev) * 0.1, torch.zeros(20, device=dev)
+dY = torch.randn(N, 128, device=dev)
 for _ in range(reps):
-    Z = ops.spmm3(g, x)                 # spmm_vec_kernel (untiled)
-    ops.spmm3(gt, x)                    # spmm3_tiled_kernel
-    ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)
+    Z = ops.spmm3(g, x)                 # spmm_win_kernel<32,1,4,0>: the default propagation
+    ops.spmm3(gt, x)                    # spmm3_tiled_full_kernel (opt-in row tiles)
+    ops.spmm3_t(g, Z)                   # spmm_win_kernel<..,2>: transposed propagation (backward)
+    Y = ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)
+    ops.layer_dense_backward(dY, Z, Y, prm, 0, res_x=x, act=True)  # dgrad / wgrad / reduce
+    ops.head(Y, W1, b1, W2, b2, 1e-12)
 torch.cuda.synchronize()
 print("ok")

@@ -3,7 +3,22 @@
 import collections
 import csv
 import glob
+import re
 import sys
+
+
+
+def classify(k):
+    m = re.search(r"spmm_win_kernel<\d+, \d+, \d+, (\d)>", k)
+    if m:
+        return {"0": "spmm3_window", "1": "spmm3_fusednorm_window", "2": "spmm3t_window"}.get(m.group(1), "spmm_window")
+    for key, short in (("spmm_vec_kernel", "spmm_bcast"), ("spmm3_tiled_full", "spmm_tiled_rows"),
+                       ("spmm3_tiled", "spmm_tiled"), ("dgrad_kernel", "dense_dgrad"), ("wgrad_kernel", "dense_wgrad"),
+                       ("reduce_splits", "wgrad_reduce"), ("dense_kernel", "dense"), ("head_kernel", "head")):
+        if key in k:
+            return short
+    return None
+
 
 d = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -11,16 +26,14 @@ dur = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{d}/*/*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        short = ("spmm_window" if "spmm_win_kernel" in k else "spmm_bcast" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
-                 else "dense" if "dense_kernel" in k else None)
+        short = classify(k)
         if short is None:
             continue
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for f in sorted(glob.glob(f"{d}/*/*kernel_trace.csv")):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        short = ("spmm_window" if "spmm_win_kernel" in k else "spmm_bcast" if "spmm_vec_kernel" in k else "spmm_tiled" if "spmm3_tiled" in k
-                 else "dense" if "dense_kernel" in k else None)
+        short = classify(k)
         if short:
             dur[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, cs in vals.items():

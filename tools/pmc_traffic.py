@@ -10,6 +10,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 
@@ -33,7 +34,8 @@ def main():
         kernels[k] = {"read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
                       "FETCH_SIZE_KiB": fetch.get(k), "WRITE_SIZE_KiB": write.get(k),
                       "dispatches": [nf.get(k, 0), nw.get(k, 0)]}
-    spmm = [k for k in kernels if "spmm_vec_kernel" in k and ", 0, " in k]
+    # the default propagation kernel: variant C (window), MODE 0 (three precomputed weights)
+    spmm = [k for k in kernels if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0>", k)]
     res = {"workload": tag, "correction": "read = 2*FETCH_SIZE KiB (gfx950 half-count on 16B/lane reads); "
                                           "write = WRITE_SIZE KiB",
            "kernels": kernels}

@@ -59,6 +59,7 @@ class CSRGraph:
     nnz: int = 0
     row_order: Optional[torch.Tensor] = None  # int32 processing schedule of destination rows (None = 0..n-1)
     tiles: Optional["RowTiles"] = None       # LDS-staged tiling (pg_spmm3_tiled_f32), if built
+    n_cols: Optional[int] = None             # rows of X (= output rows of the transpose); None = n_rows
 
     @property
     def device(self):
@@ -394,7 +395,9 @@ def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu", schedule: bool = 
     with np.errstate(divide="ignore"):
         dout_inv = np.where(dout != 0, one / np.where(dout != 0, dout, one), np.float32(0)).astype(np.float32)
         din_inv = np.where(din != 0, one / np.where(din != 0, din, one), np.float32(0)).astype(np.float32)
-    deg = torch.bincount(r_row, weights=m.to(torch.float64), minlength=n).cpu().numpy().astype(np.float32)
+    # integer degree (multiplicity 1, or 2 on a raw self-loop): exact in float32 below 2^24
+    deg = (torch.bincount(r_row, minlength=n) + torch.bincount(r_row[m == 2.0], minlength=n)).cpu().numpy()
+    deg = deg.astype(np.float32)
     with np.errstate(divide="ignore"):
         r = (one / np.sqrt(deg)).astype(np.float32)
     r[np.isinf(r)] = 0

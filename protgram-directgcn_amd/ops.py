@@ -111,7 +111,7 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     lib = load_library()
     G = _f32c(G)
     _require_gpu(G)
-    N, F = g.n_rows, G.size(1) // 3
+    N, F = (g.n_cols if g.n_cols is not None else g.n_rows), G.size(1) // 3
     dX = torch.empty(N, F, device=G.device, dtype=torch.float32)
     fl = default_flags() if flags is None else flags
     s = _stream(G)

@@ -9,8 +9,16 @@ graph: in-neighbours c+s[:-1] and out-neighbours s[1:]+c of any id range span ev
 owned output rows are exchanged with one RCCL all-gather over xGMI per layer boundary
 (``dist.all_gather_into_tensor``, equal-sized shards padded to ceil(N/P) rows).
 
-Forward only (inference / embedding extraction path, ``models_utils.py:265-273``); the single-GPU
-training step runs through ``ProtGramDirectGCN`` with autograd.
+Training (``sharded_train_step``, the trainer's step protgram_directgcn_trainer.py:91-100 on P GPUs):
+  * the all-gather's autograd backward is a reduce-scatter of the partial input gradients: the
+    transposed propagation of this rank's rows scatters into ALL source rows, i.e. dX_partial =
+    A[:, owned]^T-block = (for the symmetric n-gram matrices) the owned COLUMN block of the global
+    CSR, an SpMM over all N rows reading only the owned rows of dZ (``partition(..., transpose=True)``);
+    RCCL ``reduce_scatter_tensor`` sums the P partials into their owners (1x the forward bytes);
+  * dense weights/biases (replicated): one flat all-reduce (sum) of their gradients per step;
+  * per-node parameters (C_*_vec gates, constant) are only ever read at owned rows, so their owned
+    rows get complete gradients locally and need no communication; rows owned elsewhere are stale on
+    this rank and never read (gather them with ``gather_node_params`` to checkpoint).
 """
 from __future__ import annotations
 
@@ -42,7 +50,9 @@ class NodeRangePartition:
         return self.r1 - self.r0
 
 
-def partition(g: CSRGraph, rank: int, world: int) -> NodeRangePartition:
+def partition(g: CSRGraph, rank: int, world: int, transpose: bool = False) -> NodeRangePartition:
+    """This rank's row block. ``transpose=True`` also builds the transposed column block needed by the
+    backward (training)."""
     if not g.shared:
         raise NotImplementedError("node-range partition needs the shared-pattern CSR")
     n = g.n_rows
@@ -56,9 +66,29 @@ def partition(g: CSRGraph, rank: int, world: int) -> NodeRangePartition:
         ro = g.row_order.to(torch.int64)
         order = (ro[(ro >= r0) & (ro < r1)] - r0).to(torch.int32)
     local = CSRGraph(n_rows=r1 - r0, shared=True, rowptr=(rp[r0:r1 + 1] - e0).contiguous(), edges3=g.edges3[e0:e1],
-                     rowptr_t=None, edges3_t=None, symmetric=False, nnz=e1 - e0, row_order=order)
+                     rowptr_t=None, edges3_t=None, symmetric=False, nnz=e1 - e0, row_order=order, n_cols=n)
+    if transpose:
+        local.rowptr_t, local.edges3_t = _column_block(g, r0, r1)
     rows = torch.arange(r0, r1, dtype=torch.int64, device=rp.device)
     return NodeRangePartition(rank, world, n, per, r0, r1, local, rows)
+
+
+def _column_block(g: CSRGraph, c0: int, c1: int):
+    """CSR over all N rows of the transposed structure restricted to source columns [c0, c1), columns
+    renumbered from 0: the transposed propagation of the row block [c0, c1). Uses the graph's own
+    transposed CSR (rowptr_t / edges3_t, which alias the forward CSR for symmetric matrices). Entries
+    stay in ascending column order within each row."""
+    rp, e = g.rowptr_t, g.edges3_t
+    n = rp.numel() - 1
+    col = e[:, 0].to(torch.int64)
+    keep = (col >= c0) & (col < c1)
+    row_of = torch.repeat_interleave(torch.arange(n, device=rp.device), rp[1:] - rp[:-1])
+    cnt = torch.bincount(row_of[keep], minlength=n)
+    rowptr_t = torch.zeros(n + 1, dtype=torch.int64, device=rp.device)
+    rowptr_t[1:] = torch.cumsum(cnt, 0)
+    et = e[keep].clone()
+    et[:, 0] -= c0
+    return rowptr_t, et
 
 
 def _layer_local(conv, part: NodeRangePartition, h_full, res: nn.Module, act=True):
@@ -105,3 +135,109 @@ def all_gather_rows(h_local: torch.Tensor, part: NodeRangePartition, group=None,
     else:
         dist.all_gather_into_tensor(out, h_local.contiguous(), group=group)
     return out[:part.n]
+
+
+def reduce_scatter_rows(d_full: torch.Tensor, part: NodeRangePartition, group=None) -> torch.Tensor:
+    """[N, F] partial sums on every rank -> this rank's rows [n_local, F] of their sum over ranks
+    (RCCL reduce-scatter; the backward of all_gather_rows)."""
+    Fd = d_full.size(1)
+    buf = d_full.new_zeros(part.per * part.world, Fd)
+    buf[:part.n] = d_full
+    if dist.get_backend(group) == "gloo":  # gloo has no reduce_scatter
+        dist.all_reduce(buf, group=group)
+        return buf[part.rank * part.per:part.rank * part.per + part.n_local].clone()
+    out = d_full.new_empty(part.per, Fd)
+    dist.reduce_scatter_tensor(out, buf, group=group)
+    return out[:part.n_local]
+
+
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h_local, part, group):
+        ctx.part, ctx.group = part, group
+        return all_gather_rows(h_local, part, group).clone()
+
+    @staticmethod
+    def backward(ctx, d_full):
+        return reduce_scatter_rows(d_full.contiguous(), ctx.part, ctx.group), None, None
+
+
+def _layer_local_train(conv, part: NodeRangePartition, h_full, res: nn.Module, act=True):
+    if part.local.rowptr_t is None:
+        raise ValueError("training needs partition(..., transpose=True)")
+    Z = ops.Propagate3.apply(h_full, part.local, False)
+    vec = conv.use_vector_coeffs
+    rows = part.rows if vec else None
+    constant = conv.constant if vec else None
+    res_x = h_full[part.r0:part.r1]
+    W_res, b_res = (res.weight, res.bias) if isinstance(res, nn.Linear) else (None, None)
+    return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, 0 if vec else 1, act, ops.LEAKY_SLOPE,
+                                *conv._dense_params())
+
+
+def sharded_forward_train(model, part: NodeRangePartition, x_full: torch.Tensor, group=None):
+    """ProtGramDirectGCN.forward on this rank's rows with autograd (dropout as in the model: training mode
+    only, per-rank RNG). Returns (log_probs, emb) for rows [r0, r1)."""
+    h_full = model._apply_pe(x_full)
+    L = len(model.convs)
+    h_local = None
+    for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
+        h_local = _layer_local_train(conv, part, h_full, res)
+        h_local = F.dropout(h_local, p=model.dropout, training=model.training)
+        if i + 1 < L:
+            h_full = _GatherRows.apply(h_local, part, group) if part.world > 1 else h_local
+    return model.head(h_local)
+
+
+def _is_node_param(name: str, p: torch.Tensor, n: int) -> bool:
+    leaf = name.split(".")[-1]
+    return (leaf == "constant" or (leaf.startswith("C_") and leaf.endswith("_vec"))) and p.dim() >= 1 and p.size(0) == n
+
+
+def sharded_train_step(model, part: NodeRangePartition, x_full: torch.Tensor, y_local: torch.Tensor, optimizer,
+                       l2_lambda: float = 1e-7, group=None) -> float:
+    """One step of the reference's full-batch loop (protgram_directgcn_trainer.py:91-100) on P ranks:
+    zero_grad -> forward -> nll_loss (mean over all N nodes) + l2_lambda * sum_p ||p||^2 -> backward ->
+    all-reduce of the replicated parameters' gradients -> optimizer.step(). Returns the global loss
+    (a host sync, as the reference's loss.item())."""
+    optimizer.zero_grad()
+    lp, _ = sharded_forward_train(model, part, x_full, group)
+    loss = F.nll_loss(lp, y_local, reduction="sum") / part.n
+    if l2_lambda:
+        l2 = 0.0
+        for name, p in model.named_parameters():
+            if not p.requires_grad:
+                continue
+            if _is_node_param(name, p, part.n):
+                l2 = l2 + p[part.r0:part.r1].norm(2).pow(2)   # owned rows: each row counted once overall
+            else:
+                l2 = l2 + p.norm(2).pow(2) / part.world     # replicated: summed over ranks below
+        loss = loss + l2_lambda * l2
+    loss.backward()
+    if part.world > 1:
+        dense = [p for name, p in model.named_parameters()
+                 if p.grad is not None and not _is_node_param(name, p, part.n)]
+        flat = torch.cat([p.grad.reshape(-1) for p in dense])
+        dist.all_reduce(flat, group=group)
+        off = 0
+        for p in dense:
+            k = p.numel()
+            p.grad.copy_(flat[off:off + k].view_as(p.grad))
+            off += k
+    optimizer.step()
+    tot = loss.detach().reshape(1).clone()
+    if part.world > 1:
+        dist.all_reduce(tot, group=group)
+    return float(tot)
+
+
+@torch.no_grad()
+def gather_node_params(model, part: NodeRangePartition, group=None):
+    """Make every rank's per-node parameters (C_*_vec, constant) whole again by all-gathering the owned
+    rows (for checkpointing / switching back to single-GPU inference)."""
+    for name, p in model.named_parameters():
+        if _is_node_param(name, p, part.n) and part.world > 1:
+            flat = p.data.reshape(part.n, -1)
+            full = all_gather_rows(flat[part.r0:part.r1].contiguous(), part, group)
+            flat.copy_(full)
+

@@ -1,5 +1,7 @@
-"""Multi-process (world_size 2, gloo, CPU) test of the node-range partition forward (shard.py):
-row slicing of the CSR, global-row gate/constant gathering, padded all-gather between layers.
+"""Multi-process (world_size 2 and 3, gloo, CPU) tests of the node-range partition (shard.py):
+row slicing of the CSR, global-row gate/constant gathering, padded all-gather between layers; and the
+sharded training step (reduce-scatter backward through the transposed column block, dense-gradient
+all-reduce, communication-free per-node parameters) against the single-process oracle + Adam.
 The two HIP kernels are replaced by CPU stand-ins inside this test (the product has no CPU path);
 the result on every rank must equal the single-process oracle model forward."""
 import os
@@ -32,6 +34,19 @@ def _cpu_spmm3(g, x, out=None, fused=False, flags=None):
         w = e[:, 1 + k].contiguous().view(torch.float32)
         Z[:, k * F:(k + 1) * F].index_add_(0, rows, w[:, None] * x[col])
     return Z
+
+
+def _cpu_spmm3_t(g, G, flags=None):
+    rp, e = g.rowptr_t, g.edges3_t
+    n = rp.numel() - 1
+    rows = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
+    col = e[:, 0].long()
+    F = G.size(1) // 3
+    dX = torch.zeros(n, F)
+    for k in range(3):
+        w = e[:, 1 + k].contiguous().view(torch.float32)
+        dX.index_add_(0, rows, w[:, None] * G[col, k * F:(k + 1) * F])
+    return dX
 
 
 def _cpu_layer_dense(Z, prm, gate_mode, rows=None, constant=None, res_x=None, W_res=None, b_res=None, act=False,
@@ -87,6 +102,94 @@ def _worker(rank, world, port, out_q):
         out_q.put((rank, part.r0, part.r1, bool(ok), float((lp - lp_r[part.r0:part.r1]).abs().max())))
     finally:
         dist.destroy_process_group()
+
+
+def _train_worker(rank, world, port, out_q):
+    """Two sharded training steps (eval-mode dropout, L2 term on) vs the single-process oracle + Adam."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard
+    from oracle import directgcn_cpu as oc
+    from oracle import graph_cpu as og
+    import torch.nn.functional as F
+    ops.spmm3 = _cpu_spmm3
+    ops.spmm3_t = _cpu_spmm3_t
+    ops.layer_dense = _cpu_layer_dense
+    ops.layer_dense_backward = lambda *a, **k: None  # -> the torch formulation of the same backward
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, s, d, c = pkg.synth.de_bruijn_edges(2)
+        m = og.build_matrices(N, s, d, c)
+        g = pkg.graph.csr_from_coo(N, *m["in"], *m["out"], *m["und"], cache=False)
+        dims = [16, 16, 12, 12]
+        torch.manual_seed(0)
+        model = pkg.ProtGramDirectGCN(dims, N, 5, 2, 0, 512, 0.5, True).eval()
+        with torch.no_grad():
+            gen = torch.Generator().manual_seed(5)
+            for name, p in model.named_parameters():
+                leaf = name.split(".")[-1]
+                if leaf.startswith("C_"):
+                    p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+                elif "bias" in leaf:
+                    p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+        ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+        x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
+        y = (torch.arange(N) // 20) % 5
+        lam, steps = 1e-3, 2
+        part = shard.partition(g, rank, world, transpose=True)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+        losses = [shard.sharded_train_step(model, part, x, y[part.r0:part.r1], opt, l2_lambda=lam)
+                  for _ in range(steps)]
+        ropt = torch.optim.Adam(list(ref.values()), lr=1e-2)
+        rlosses = []
+        for _ in range(steps):
+            ropt.zero_grad()
+            lp, _ = oc.model_forward(ref, dims, x, *m["in"], *m["out"], *m["und"], n_gram_len=2)
+            loss = F.nll_loss(lp, y) + lam * sum(v.norm(2).pow(2) for v in ref.values())
+            loss.backward()
+            ropt.step()
+            rlosses.append(float(loss))
+        bad = []
+        if not np.allclose(losses, rlosses, rtol=1e-5, atol=1e-6):
+            bad.append(("loss", losses, rlosses))
+        for name, p in model.named_parameters():
+            r = ref[name].detach()
+            if shard._is_node_param(name, p, N):
+                p, r = p[part.r0:part.r1], r[part.r0:part.r1]
+            err = float((p.detach() - r).abs().max())
+            if err > 2e-5:
+                bad.append((name, err))
+        shard.gather_node_params(model, part)
+        for name, p in model.named_parameters():
+            err = float((p.detach() - ref[name].detach()).abs().max())
+            if err > 2e-5:
+                bad.append(("gathered " + name, err))
+        out_q.put((rank, part.r0, part.r1, not bad, str(bad[:4])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_training_gloo(world):
+    res = _run(_train_worker, world)
+    for r in res:
+        assert r[3], f"rank {r[0]}: {r[4]}"
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -2,9 +2,10 @@
 //   logits = W2 relu(W1 h + b1) + b2            (decoder_fc: Linear -> ReLU -> Dropout(eval) -> Linear)
 //   logp   = log_softmax(logits)                (F.log_softmax(.., dim=-1))
 //   emb    = h / (||h||_2 + eps)                (EmbeddingProcessor.l2_normalize_torch, models_utils.py:139-147)
-// One pass over h: a block stages 64 rows of h in LDS, writes their embeddings, runs both decoder
-// products on fp32 MFMA (v_mfma_f32_32x32x2_f32, B operands straight from the L1/L2-resident
-// weights), and finishes the row softmax in LDS. Replaces 6+ framework launches and two re-reads of h.
+// One pass over h: a persistent block walks 64-row tiles, staging each in LDS (the next tile's rows are
+// already in flight into registers), writes their embeddings, runs both decoder products on fp32 MFMA
+// (v_mfma_f32_32x32x2_f32, B operands straight from the L1/L2-resident weights), and finishes the row
+// softmax in LDS. Replaces 6+ framework launches and two re-reads of h.
 // Fast path: F <= 256, H <= 128, C <= 64 (F, H multiples of 4); other shapes use a one-wave-per-row
 // fallback kernel.
 #include "pg_common.h"
@@ -33,141 +34,160 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 template <int FMAX, int HMAX, int CMAX>
 __global__ __launch_bounds__(256) void head_kernel(HeadP p) {
     constexpr int HLD = FMAX + 4, ZLD = HMAX + 4, LLD = CMAX + 1;
+    static_assert(HB * LLD <= HB * HLD, "logits alias the h tile");
+    constexpr int PF = HB * FMAX / 4 / 256;  // float4 of the h tile per thread
     __shared__ __attribute__((aligned(16))) float Hs[HB * HLD];
     __shared__ __attribute__((aligned(16))) float Zs[HB * ZLD];
-    __shared__ float Ls[HB * LLD];
+    float* Ls = Hs;  // logits reuse the h tile once both decoder products are done
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int li = lane & 31, lh = lane >> 5;
-    const int64_t m0 = (int64_t)blockIdx.x * HB;
     const int F4 = p.F >> 2;
+    const int64_t ntiles = (p.M + HB - 1) / HB;
 
-    // 1. stage h rows (float4, coalesced; rows past M are zero)
-    for (int idx = tid; idx < HB * F4; idx += 256) {
-        const int r = idx / F4, c4 = idx % F4;
-        const int64_t m = m0 + r;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (m < p.M) v = ld4(p.h + m * p.ldh + 4 * c4);
-        *reinterpret_cast<float4*>(&Hs[r * HLD + 4 * c4]) = v;
-    }
-    __syncthreads();
-
-    // 2. embeddings: 4 lanes... one 16-lane group per row, 16 rows per wave pass
-    {
-        const int g = lane >> 4, t = lane & 15;
-        for (int r = wave * 4 + g; r < HB; r += 16) {
-            float ss = 0.f;
-            for (int c4 = t; c4 < F4; c4 += 16) {
-                const float4 v = ld4(&Hs[r * HLD + 4 * c4]);
-                ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-            }
+    // Persistent: the block walks tiles blockIdx.x, +gridDim.x, ...; the next tile's h rows are loaded
+    // into registers while the current tile is computed (HBM latency hidden behind the MFMA / softmax).
+    float4 hv[PF];
+    auto load = [&](int64_t t) {
 #pragma unroll
-            for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
-            const int64_t m = m0 + r;
-            if (m < p.M) {
-                const float inv = 1.0f / (sqrtf(ss) + p.eps);
-                for (int c4 = t; c4 < F4; c4 += 16) {
-                    float4 v = ld4(&Hs[r * HLD + 4 * c4]);
-                    v = make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
-                    *reinterpret_cast<float4*>(p.emb + m * p.lde + 4 * c4) = v;
+        for (int q = 0; q < PF; ++q) {
+            const int idx = tid + 256 * q;
+            const int r = idx / (FMAX / 4), c4 = idx % (FMAX / 4);
+            const int64_t m = t * HB + r;
+            hv[q] = (m < p.M && c4 < F4) ? ld4(p.h + m * p.ldh + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    int64_t t = blockIdx.x;
+    if (t < ntiles) load(t);
+    for (; t < ntiles; t += gridDim.x) {
+        const int64_t m0 = t * HB;
+        // 1. stage h rows (rows past M and columns past F are zero)
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+            const int idx = tid + 256 * q;
+            const int r = idx / (FMAX / 4), c4 = idx % (FMAX / 4);
+            *reinterpret_cast<float4*>(&Hs[r * HLD + 4 * c4]) = hv[q];
+        }
+        __syncthreads();
+        if (t + gridDim.x < ntiles) load(t + gridDim.x);
+
+        // 2. embeddings: one 16-lane group per row, 16 rows per wave pass
+        {
+            const int g = lane >> 4, tt = lane & 15;
+            for (int r = wave * 4 + g; r < HB; r += 16) {
+                float ss = 0.f;
+                for (int c4 = tt; c4 < F4; c4 += 16) {
+                    const float4 v = ld4(&Hs[r * HLD + 4 * c4]);
+                    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                }
+#pragma unroll
+                for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+                const int64_t m = m0 + r;
+                if (m < p.M) {
+                    const float inv = 1.0f / (sqrtf(ss) + p.eps);
+                    for (int c4 = tt; c4 < F4; c4 += 16) {
+                        float4 v = ld4(&Hs[r * HLD + 4 * c4]);
+                        v = make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+                        *reinterpret_cast<float4*>(p.emb + m * p.lde + 4 * c4) = v;
+                    }
                 }
             }
         }
-    }
 
-    // 3. z = relu(h W1^T + b1): (HB/32) x (H/32) tiles of 32x32, K = F. Lane feeds A from LDS and
-    //    B (= W1 rows) from global, 4 k at a time with the K permutation of pg_dense.hip.
-    {
-        const int ntile_n = (p.H + 31) / 32;
-        for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
-            const int tm = tile / ntile_n, tn = tile % ntile_n;
-            const int j = tn * 32 + li;
-            const bool jok = j < p.H;
-            const float* w1row = p.W1 + (int64_t)(jok ? j : 0) * p.F;
-            // all B fragments of this tile issued up front (FMAX/8 float4 per lane), then the MFMA chain
-            constexpr int KG = FMAX / 8;
-            float4 bf[KG];
+        // 3. z = relu(h W1^T + b1): (HB/32) x (H/32) tiles of 32x32, K = F. A from LDS, B (= W1 rows)
+        //    from the L2-resident weights, 4 k at a time with the K permutation of pg_dense.hip.
+        {
+            const int ntile_n = (p.H + 31) / 32;
+            for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
+                const int tm = tile / ntile_n, tn = tile % ntile_n;
+                const int j = tn * 32 + li;
+                const bool jok = j < p.H;
+                const float* w1row = p.W1 + (int64_t)(jok ? j : 0) * p.F;
+                constexpr int KG = FMAX / 8;
+                float4 bf[KG];
 #pragma unroll
-            for (int g = 0; g < KG; ++g) {
-                const int k = g * 8 + 4 * lh;
-                bf[g] = (jok && k < p.F) ? ld4(w1row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            f32x16 acc;
+                for (int g = 0; g < KG; ++g) {
+                    const int k = g * 8 + 4 * lh;
+                    bf[g] = (jok && k < p.F) ? ld4(w1row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                f32x16 acc;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+                for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-            for (int g = 0; g < KG; ++g) {
-                const int k = g * 8 + 4 * lh;
-                const float4 a = k < p.F ? ld4(&Hs[(tm * 32 + li) * HLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 b = bf[g];
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
-            }
-            const float bj = jok ? p.b1[j] : 0.f;
+                for (int g = 0; g < KG; ++g) {
+                    const int k = g * 8 + 4 * lh;
+                    const float4 a = k < p.F ? ld4(&Hs[(tm * 32 + li) * HLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 b = bf[g];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+                }
+                const float bj = jok ? p.b1[j] : 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const float z = acc[r] + bj;
-                if (j < ZLD - 4) Zs[row * ZLD + j] = jok ? (z > 0.f ? z : 0.f) : 0.f;
+                for (int r = 0; r < 16; ++r) {
+                    const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float z = acc[r] + bj;
+                    if (j < ZLD - 4) Zs[row * ZLD + j] = jok ? (z > 0.f ? z : 0.f) : 0.f;
+                }
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();  // Zs complete; Hs free (-> Ls)
 
-    // 4. logits = z W2^T + b2: (HB/32) x (C/32) tiles, K = H
-    {
-        const int ntile_n = (p.C + 31) / 32;
-        for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
-            const int tm = tile / ntile_n, tn = tile % ntile_n;
-            const int c = tn * 32 + li;
-            const bool cok = c < p.C;
-            const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * p.H;
-            constexpr int KG = HMAX / 8;
-            float4 bf[KG];
+        // 4. logits = z W2^T + b2: (HB/32) x (C/32) tiles, K = H
+        {
+            const int ntile_n = (p.C + 31) / 32;
+            for (int tile = wave; tile < 2 * ntile_n; tile += 4) {
+                const int tm = tile / ntile_n, tn = tile % ntile_n;
+                const int c = tn * 32 + li;
+                const bool cok = c < p.C;
+                const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * p.H;
+                constexpr int KG = HMAX / 8;
+                float4 bf[KG];
 #pragma unroll
-            for (int g = 0; g < KG; ++g) {
-                const int k = g * 8 + 4 * lh;
-                bf[g] = (cok && k < p.H) ? ld4(w2row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            f32x16 acc;
+                for (int g = 0; g < KG; ++g) {
+                    const int k = g * 8 + 4 * lh;
+                    bf[g] = (cok && k < p.H) ? ld4(w2row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                f32x16 acc;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+                for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-            for (int g = 0; g < KG; ++g) {
-                const int k = g * 8 + 4 * lh;
-                const float4 a = k < p.H ? ld4(&Zs[(tm * 32 + li) * ZLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 b = bf[g];
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
-            }
-            const float bc = cok ? p.b2[c] : 0.f;
+                for (int g = 0; g < KG; ++g) {
+                    const int k = g * 8 + 4 * lh;
+                    const float4 a = k < p.H ? ld4(&Zs[(tm * 32 + li) * ZLD + k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float4 b = bf[g];
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+                }
+                const float bc = cok ? p.b2[c] : 0.f;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (cok) Ls[row * LLD + c] = acc[r] + bc;
+                for (int r = 0; r < 16; ++r) {
+                    const int row = tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    if (cok) Ls[row * LLD + c] = acc[r] + bc;
+                }
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // 5. log_softmax per row (max-shifted, as torch): 4 lanes per row
-    {
-        const int r = tid >> 2, t = tid & 3;
-        const int64_t m = m0 + r;
-        float mx = -INFINITY;
-        for (int c = t; c < p.C; c += 4) mx = fmaxf(mx, Ls[r * LLD + c]);
-        mx = fmaxf(mx, __shfl_xor(mx, 1, 4));
-        mx = fmaxf(mx, __shfl_xor(mx, 2, 4));
-        float se = 0.f;
-        for (int c = t; c < p.C; c += 4) se += expf(Ls[r * LLD + c] - mx);
-        se += __shfl_xor(se, 1, 4);
-        se += __shfl_xor(se, 2, 4);
-        const float lse = mx + logf(se);
-        if (m < p.M)
-            for (int c = t; c < p.C; c += 4) p.logp[m * p.ldp + c] = Ls[r * LLD + c] - lse;
+        // 5. log_softmax per row (max-shifted, as torch): 4 lanes per row
+        {
+            const int r = tid >> 2, tt = tid & 3;
+            const int64_t m = m0 + r;
+            float mx = -INFINITY;
+            for (int c = tt; c < p.C; c += 4) mx = fmaxf(mx, Ls[r * LLD + c]);
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 4));
+            mx = fmaxf(mx, __shfl_xor(mx, 2, 4));
+            float se = 0.f;
+            for (int c = tt; c < p.C; c += 4) se += expf(Ls[r * LLD + c] - mx);
+            se += __shfl_xor(se, 1, 4);
+            se += __shfl_xor(se, 2, 4);
+            const float lse = mx + logf(se);
+            if (m < p.M)
+                for (int c = tt; c < p.C; c += 4) p.logp[m * p.ldp + c] = Ls[r * LLD + c] - lse;
+        }
+        __syncthreads();  // Ls (= Hs) is read before the next tile is staged
     }
 }
 
@@ -225,11 +245,17 @@ extern "C" int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C,
     hipStream_t s = (hipStream_t)stream;
     const bool vec = F % 4 == 0 && H % 4 == 0 && ldh % 4 == 0 && lde % 4 == 0 && pg::aligned16(h) &&
                      pg::aligned16(emb) && pg::aligned16(W1) && pg::aligned16(W2);
-    const unsigned nb = (unsigned)((M + HB - 1) / HB);
+    const int64_t ntiles = (M + HB - 1) / HB;
+    // persistent grid: blocks per CU as VGPRs allow (179 / 256 VGPRs), tiles split evenly over one wave
+    auto grid_of = [&](int64_t per_cu) {
+        const int64_t slots = 256 * per_cu;
+        const int64_t per_block = (ntiles + slots - 1) / slots;
+        return (unsigned)((ntiles + per_block - 1) / per_block);
+    };
     if (vec && F <= 128 && H <= 64 && C <= 32) {
-        hipLaunchKernelGGL((head_kernel<128, 64, 32>), dim3(nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((head_kernel<128, 64, 32>), dim3(grid_of(2)), dim3(256), 0, s, p);
     } else if (vec && F <= 256 && H <= 128 && C <= 64) {
-        hipLaunchKernelGGL((head_kernel<256, 128, 64>), dim3(nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((head_kernel<256, 128, 64>), dim3(grid_of(1)), dim3(256), 0, s, p);
     } else {
         const size_t shm = 4 * (size_t)(F + H + C) * sizeof(float);
         PG_REQUIRE(shm <= 160 * 1024, "head too wide for the generic kernel");

@@ -303,7 +303,7 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
     conv = model.convs[0]
     prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
     flops = 2 * x.size(0) * 3 * Fd * conv.out_channels
-    for fl, name in ((0, "dense"), (512, "dense_4waves"), (8, "dense_bm64")):
+    for fl, name in ((0, "dense"), (512, "dense_4waves"), (8, "dense_bm64_w8"), (8 | 512, "dense_bm64_w4")):
         ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True, flags=fl))
         res[f"{name}_ms"] = round(ms, 4)
         res[f"{name}_TFLOPs"] = round(flops / ms / 1e9, 2)

@@ -64,7 +64,7 @@ __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_
 template <int BM, int BN, int NW, bool VEC>
 __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
     constexpr int NT = 64 * NW;  // threads
-    constexpr int WN = (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
+    constexpr int WN = (BM == 64 && NW == 8) ? 4 : (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
     constexpr int WM = NW / WN;
     static_assert(BM / WM >= 32 && BN / WN >= 32, "wave tile too small");
     constexpr int TM = BM / WM / 32;
@@ -425,8 +425,10 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
         else hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, false>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p);    \
     } while (0)
-    const bool w8 = !(flags & PG_FLAG_DENSE_4WAVES) && !bm64;
-    if (bm64) {
+    const bool w8 = !(flags & PG_FLAG_DENSE_4WAVES);
+    if (bm64 && w8 && wide) {
+        PG_LAUNCH(64, 128, 8);  // 8 waves of 32x32 (measured 0.186 ms vs 0.177 for the default at B(20,4))
+    } else if (bm64) {
         if (wide) PG_LAUNCH(64, 128, 4);
         else PG_LAUNCH(64, 64, 4);
     } else if (w8) {

@@ -392,7 +392,7 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
         y = y + (xres.double() @ W_res.double().t() + b_res.double() if proj else xres.double())
     y = torch.nn.functional.leaky_relu(y, 0.01)
     dv = {k: v.to(cuda) for k, v in prm.items()}
-    for fl in (0, PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_NO_XCD_REMAP):
+    for fl in (0, PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_DENSE_BM64 | PG_FLAG_DENSE_4WAVES, PG_FLAG_NO_XCD_REMAP):
         out = ops.layer_dense(Z.to(cuda), dv, gate, rows=None if r is None else r.to(cuda),
                               constant=None if const is None else const.to(cuda),
                               res_x=None if xres is None else xres.to(cuda),

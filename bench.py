@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--fused-norm", action="store_true", help="compute edge weights inside the SpMM")
+    ap.add_argument("--bf16", action="store_true", help="bf16 mode (config 5): bf16 features/activations, fp32 sums")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-layers", type=int, default=1)
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
@@ -100,6 +101,11 @@ def main():
     model = model.to(dev).eval()
     model.fused_norm = args.fused_norm
     x = torch.randn(N, Fd, generator=torch.Generator().manual_seed(1234)).to(dev)
+    if args.bf16:
+        if args.fused_norm:
+            raise SystemExit("--bf16 uses precomputed weights (no fused-norm bf16 kernel)")
+        model.compute_dtype = torch.bfloat16
+        x = x.to(torch.bfloat16)  # inputs resident in HBM in the compute dtype
     data = pkg.Data(x=x, graph=g)
 
     part = shard.partition(g, rank, world) if world > 1 else None
@@ -139,22 +145,24 @@ def main():
 
     # roofline of the dominant kernel (SURVEY §8d B_agg, per launch = this rank's rows)
     if part is None:
-        launch_bytes = g.algorithmic_bytes(Fd)
+        launch_bytes = g.algorithmic_bytes(Fd, elem=2 if args.bf16 else 4)
         launch_nnz, launch_rows = g.nnz, N
     else:
         launch_nnz, launch_rows = part.local.nnz, part.n_local
-        launch_bytes = 8 * (launch_rows + 1) + launch_nnz * (16 + 4 * Fd) + 3 * launch_rows * Fd * 4
+        el = 2 if args.bf16 else 4
+        launch_bytes = 8 * (launch_rows + 1) + launch_nnz * (16 + el * Fd) + 3 * launch_rows * Fd * el
     achieved = launch_bytes / (spmm_avg_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "traffic_r01.json")
     if os.path.exists(tfile) and world == 1:
         try:
             tj = json.load(open(tfile))
-            if tj.get("workload") == f"B(20,{n})/F{Fd}" and tj.get("kernel_bytes_per_launch"):
+            if tj.get("workload") == f"B(20,{n})/F{Fd}" and tj.get("kernel_bytes_per_launch") and not args.bf16:
                 traffic = tj["kernel_bytes_per_launch"]
         except (OSError, ValueError):
             traffic = None
-    roofline = {"bound": "hbm", "kernel": "pg_spmm3_f32" if not args.fused_norm else "pg_spmm3_fusednorm_f32",
+    kname = "pg_spmm3_bf16" if args.bf16 else ("pg_spmm3_fusednorm_f32" if args.fused_norm else "pg_spmm3_f32")
+    roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": launch_bytes, "avg_launch_ms": round(spmm_avg_ms, 4),
@@ -173,7 +181,7 @@ def main():
             "metric": "edges/sec propagated, DirectGCN fwd on 4-gram graph, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.bf16 else "f32", "data": "synthetic",
             "config": {"workload": f"directgcn_fwd_B(20,{n})", "graph": f"complete n-gram de Bruijn B(20,{n})",
                        "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
                        "layers": L, "layer_dims": dims, "classes": C,
@@ -281,17 +289,6 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
         g44 = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout, K=4, L=4, max_ucols=192))
         for fl, name in ((32, "tiles44_fc64_u8"),):
             res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(g44, x, flags=fl)), 4)
-        # untiled kernel driven by 2-D tile orders (L1 reuse inside a block of 8 rows)
-        import numpy as np
-        for K, L, bmajor in ((4, 8, False), (4, 8, True), (2, 4, True), (4, 2, False), (8, 4, True), (20, 20, True)):
-            order, tid = pkg.graph.tile_schedule(kin, kout, K, L)
-            if bmajor:  # inside each tile sort by (out-class, in-class) instead of (in-class, out-class)
-                kin_np, kout_np = kin.cpu().numpy(), kout.cpu().numpy()
-                o2 = np.lexsort((kin_np[order], kout_np[order], tid))
-                order = order[o2]
-            ro = torch.from_numpy(order.astype(np.int32)).to(x.device)
-            gk = dataclasses.replace(g, tiles=None, row_order=ro)
-            res[f"spmm3_order_{K}x{L}{'_b' if bmajor else '_a'}_ms"] = round(timeit(lambda: ops.spmm3(gk, x)), 4)
     for fl, name in ((0, "window_u4"), (4, "window_u8"), (128, "bcast_u8"), (1, "window_u4_noremap")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
@@ -339,8 +336,9 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
             loss.backward()
             opt.step()
 
-    res["train_step_ms"] = round(timeit(lambda: train_step(False), reps=5), 3)
-    res["train_step_trainer_amp_ms"] = round(timeit(lambda: train_step(True), reps=5), 3)
+    if x.dtype == torch.float32 or getattr(ops, "BF16_BACKWARD", False):
+        res["train_step_ms"] = round(timeit(lambda: train_step(False), reps=5), 3)
+        res["train_step_trainer_amp_ms"] = round(timeit(lambda: train_step(True), reps=5), 3)
     model.eval()
     log(f"[bench] extra: {json.dumps(res)}")
     return res

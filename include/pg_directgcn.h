@@ -227,6 +227,39 @@ int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* args);
 int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* args, const float* packed, const pg_layer_grad_args_t* grads,
                                uint32_t flags, void* stream);
 
+/* ---- bf16 mode (config 5: bf16 storage, fp32 accumulation) --------------------------------------
+ * Features, aggregates, layer outputs and their gradients are bf16 (uint16_t bit patterns); every sum is
+ * fp32, rounded once to bf16 (round-to-nearest-even, as torch) when stored. Parameters stay fp32. */
+
+/* out[i] = bf16(in[i]) (e.g. the packed contraction operand of pg_directgcn_pack_f32). */
+int pg_f32_to_bf16(int64_t n, const float* in, uint16_t* out, void* stream);
+
+/* pg_spmm3_f32 over bf16 rows: Z = bf16([A_in X | A_out X | A_und X]), fp32 FMA sums in the same entry
+ * order as pg_spmm3_f32 (so within one bf16 rounding of bf16(pg_spmm3_f32(X))). F in {16,32,64,128,256,512}; F, ldx, ldz multiples of 8; 16-B aligned (else
+ * PG_ERR_UNSUPPORTED). */
+int pg_spmm3_bf16(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                  const uint16_t* X, int64_t ldx, int64_t F, uint16_t* Z, int64_t ldz, uint32_t flags, void* stream);
+
+/* Transpose of pg_spmm3_bf16 (backward): dX[i] = bf16(sum_e w_in G[col,0:F] + w_out G[col,F:2F] + w_und G[col,2F:3F])
+ * over the transposed CSR (= the forward CSR for symmetric matrices). */
+int pg_spmm3t_bf16(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                   const uint16_t* G, int64_t ldg, int64_t F, uint16_t* dX, int64_t lddx, uint32_t flags,
+                   void* stream);
+
+/* pg_directgcn_dense_f32 on bf16 MFMA (v_mfma_f32_32x32x16_bf16). In `args`, Z, res_x and Y point to bf16
+ * data (their float* types are reinterpreted); gates, constant and the bias sums (read from the fp32
+ * `packed`) stay fp32. `packed_bf16` = pg_f32_to_bf16 of the first F_out*K floats of `packed`. Needs
+ * F_in % 8 == 0, F_out % 4 == 0, ldz and ld_res multiples of 8, 16-B aligned Z / res_x / packed_bf16 /
+ * constant, 8-B aligned Y (else PG_ERR_UNSUPPORTED). */
+int pg_directgcn_dense_bf16(const pg_layer_args_t* args, const float* packed, const uint16_t* packed_bf16,
+                            uint32_t flags, void* stream);
+
+/* pg_directgcn_head_f32 with a bf16 input h (bf16 mode); outputs stay fp32. Needs the fast-path shape
+ * (F <= 256, H <= 128, C <= 64; F, H, ldh, lde multiples of 4), else PG_ERR_UNSUPPORTED. */
+int pg_directgcn_head_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uint16_t* h, int64_t ldh,
+                           const float* W1, const float* b1, const float* W2, const float* b2, float eps,
+                           float* logp, int64_t ldp, float* emb, int64_t lde, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

@@ -85,6 +85,12 @@ SIGNATURES = {
     "pg_directgcn_dense_bwd_workspace": (c_i64, [ctypes.POINTER(LayerArgs)]),
     "pg_directgcn_dense_bwd_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
                                                   c_u32, c_vp]),
+    "pg_f32_to_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
+    "pg_spmm3_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3t_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_directgcn_dense_bf16": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp, c_u32, c_vp]),
+    "pg_directgcn_head_bf16": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                              c_vp, c_i64, c_vp, c_i64, c_vp]),
     "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "pg_gemm_at_b_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,

@@ -20,6 +20,7 @@ struct HeadP {
     int64_t M;
     int F, H, C;
     const float* h;
+    const uint16_t* hb;  // bf16 input instead of h (bf16 mode), or null
     int64_t ldh;
     const float *W1, *b1, *W2, *b2;
     float eps;
@@ -53,7 +54,17 @@ __global__ __launch_bounds__(256) void head_kernel(HeadP p) {
             const int idx = tid + 256 * q;
             const int r = idx / (FMAX / 4), c4 = idx % (FMAX / 4);
             const int64_t m = t * HB + r;
-            hv[q] = (m < p.M && c4 < F4) ? ld4(p.h + m * p.ldh + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < p.M && c4 < F4) {
+                if (p.hb) {
+                    const uint2 w = *reinterpret_cast<const uint2*>(p.hb + m * p.ldh + 4 * c4);
+                    hv[q] = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                        __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+                } else {
+                    hv[q] = ld4(p.h + m * p.ldh + 4 * c4);
+                }
+            } else {
+                hv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
     };
     int64_t t = blockIdx.x;
@@ -234,17 +245,22 @@ __global__ __launch_bounds__(256) void head_generic_kernel(HeadP p) {
 
 }  // namespace
 
-extern "C" int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, int64_t ldh,
-                                     const float* W1, const float* b1, const float* W2, const float* b2, float eps,
-                                     float* logp, int64_t ldp, float* emb, int64_t lde, void* stream) {
+namespace {
+int head_launch(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, const uint16_t* hb, int64_t ldh,
+                const float* W1, const float* b1, const float* W2, const float* b2, float eps, float* logp, int64_t ldp,
+                float* emb, int64_t lde, void* stream) {
     PG_REQUIRE(M >= 0 && F > 0 && H > 0 && C > 0 && F < (1 << 16) && H < (1 << 16) && C < (1 << 16), "bad shape");
     if (M == 0) return PG_OK;
-    PG_REQUIRE(h && W1 && b1 && W2 && b2 && logp && emb, "null pointer");
+    PG_REQUIRE((h || hb) && W1 && b1 && W2 && b2 && logp && emb, "null pointer");
     PG_REQUIRE(ldh >= F && lde >= F && ldp >= C, "bad leading dimension");
-    HeadP p{M, (int)F, (int)H, (int)C, h, ldh, W1, b1, W2, b2, eps, logp, ldp, emb, lde};
+    HeadP p{M, (int)F, (int)H, (int)C, h, hb, ldh, W1, b1, W2, b2, eps, logp, ldp, emb, lde};
     hipStream_t s = (hipStream_t)stream;
-    const bool vec = F % 4 == 0 && H % 4 == 0 && ldh % 4 == 0 && lde % 4 == 0 && pg::aligned16(h) &&
+    const bool in_ok = hb ? ((reinterpret_cast<uintptr_t>(hb) & 7) == 0) : pg::aligned16(h);
+    const bool vec = F % 4 == 0 && H % 4 == 0 && ldh % 4 == 0 && lde % 4 == 0 && in_ok &&
                      pg::aligned16(emb) && pg::aligned16(W1) && pg::aligned16(W2);
+    if (hb && !(vec && F <= 256 && H <= 128 && C <= 64))
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_head_bf16: needs F <= 256, H <= 128, C <= 64, "
+                                                 "F, H, ldh multiples of 4");
     const int64_t ntiles = (M + HB - 1) / HB;
     // persistent grid: blocks per CU as VGPRs allow (179 / 256 VGPRs), tiles split evenly over one wave
     auto grid_of = [&](int64_t per_cu) {
@@ -262,4 +278,17 @@ extern "C" int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C,
         hipLaunchKernelGGL(head_generic_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), shm, s, p);
     }
     return pg::check_launch("pg_directgcn_head_f32");
+}
+}  // namespace
+
+extern "C" int pg_directgcn_head_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, int64_t ldh,
+                                     const float* W1, const float* b1, const float* W2, const float* b2, float eps,
+                                     float* logp, int64_t ldp, float* emb, int64_t lde, void* stream) {
+    return head_launch(M, F, H, C, h, nullptr, ldh, W1, b1, W2, b2, eps, logp, ldp, emb, lde, stream);
+}
+
+extern "C" int pg_directgcn_head_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uint16_t* h, int64_t ldh,
+                                      const float* W1, const float* b1, const float* W2, const float* b2, float eps,
+                                      float* logp, int64_t ldp, float* emb, int64_t lde, void* stream) {
+    return head_launch(M, F, H, C, nullptr, h, ldh, W1, b1, W2, b2, eps, logp, ldp, emb, lde, stream);
 }

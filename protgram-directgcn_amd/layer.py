@@ -190,6 +190,9 @@ class ProtGramDirectGCN(nn.Module):
         self.decoder_fc = nn.Sequential(nn.Linear(final_dim, hidden), nn.ReLU(), nn.Dropout(p=0.5),
                                         nn.Linear(hidden, task_num_output_classes))
         self.fused_norm = False  # use pg_spmm3_fusednorm_f32 when the graph carries raw counts
+        # torch.float32 (default, the reference's CPU precision) or torch.bfloat16 (bf16 storage of features,
+        # aggregates and activations with fp32 accumulation; BASELINE config 5). Not part of the state_dict.
+        self.compute_dtype = torch.float32
 
     def _apply_pe(self, x: torch.Tensor) -> torch.Tensor:
         """:182-193, out of place (the reference's in-place add fails under autograd when x has no grad)."""
@@ -228,6 +231,10 @@ class ProtGramDirectGCN(nn.Module):
         ops._require_gpu(x)
         g = self.graph_of(data)
         h = self._apply_pe(x)
+        if self.compute_dtype == torch.bfloat16:
+            h = h.to(torch.bfloat16)
+        elif self.compute_dtype != torch.float32:
+            raise ValueError("compute_dtype must be torch.float32 or torch.bfloat16")
         for conv, res in zip(self.convs, self.res_projs):
             if isinstance(res, nn.Linear):
                 h = conv.fused_forward(h, g, original_indices, res_x=h, W_res=res.weight, b_res=res.bias, act=True,
@@ -244,6 +251,7 @@ class ProtGramDirectGCN(nn.Module):
         dec = self.decoder_fc
         if not self.training and not torch.is_grad_enabled() and h.is_cuda:
             return ops.head(h, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias, self.l2_eps)
+        h = h.float()  # bf16 mode: the decoder and the embeddings are computed in fp32
         if h.is_cuda and len(dec) == 4 and isinstance(dec[0], nn.Linear) and isinstance(dec[3], nn.Linear):
             a = dec[2](dec[1](ops.row_linear(h, dec[0].weight, dec[0].bias)))  # Linear, ReLU, Dropout
             logits = ops.row_linear(a, dec[3].weight, dec[3].bias)

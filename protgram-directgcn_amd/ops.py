@@ -9,6 +9,7 @@ there is no CPU implementation of the product path.
 from __future__ import annotations
 
 import ctypes
+import functools
 from typing import Optional
 
 import torch
@@ -46,7 +47,7 @@ def _require_gpu(*ts):
         if not t.is_cuda:
             raise RuntimeError("protgram_directgcn_amd runs on the MI355X only: got a CPU tensor "
                                "(move the model and data to 'cuda'; there is no CPU fallback)")
-        if t.dtype not in (torch.float32, torch.int32, torch.int64):
+        if t.dtype not in (torch.float32, torch.bfloat16, torch.int32, torch.int64):
             raise TypeError(f"unsupported dtype {t.dtype}")
 
 
@@ -62,13 +63,24 @@ def _f32c(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
 
 
+def _bf16c(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous() if t.dtype == torch.bfloat16 else t.to(torch.bfloat16).contiguous()
+
+
+def _is_bf16(t) -> bool:
+    return t is not None and t.dtype == torch.bfloat16
+
+
 # ------------------------------------------------------------------------------------------------
 # raw kernel calls
 # ------------------------------------------------------------------------------------------------
 def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
           flags: Optional[int] = None) -> torch.Tensor:
-    """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels."""
+    """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels. bf16 x -> bf16 Z
+    (pg_spmm3_bf16: fp32 sums, one rounding)."""
     lib = load_library()
+    if _is_bf16(x):
+        return _spmm3_bf16(lib, g, x, out, fused, flags)
     x = _f32c(x)
     _require_gpu(x)
     N, F = g.n_rows, x.size(1)
@@ -106,9 +118,47 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     return Z
 
 
+def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
+    x = _bf16c(x)
+    _require_gpu(x)
+    N, F = g.n_rows, x.size(1)
+    if x.size(0) < N:
+        raise ValueError("x has fewer rows than the graph")
+    if g.shared and not fused:
+        Z = out if out is not None else torch.empty(N, 3 * F, device=x.device, dtype=torch.bfloat16)
+        fl = default_flags() if flags is None else flags
+        ev = _ev_start(x)
+        rc = lib.pg_spmm3_bf16(N, _p(g.rowptr), _p(g.row_order), _p(g.edges3), _p(x), x.stride(0), F, _p(Z),
+                               Z.stride(0), fl, _stream(x))
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_spmm3_bf16")
+            _ev_end(x, ev)
+            return Z
+    # shapes / graph kinds without a bf16 kernel: the fp32 kernels on the widened input, one rounding
+    Z = spmm3(g, x.float(), fused=fused, flags=flags).to(torch.bfloat16)
+    if out is not None:
+        out.copy_(Z)
+        return out
+    return Z
+
+
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
-    """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3)."""
+    """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX."""
     lib = load_library()
+    if _is_bf16(G):
+        G = _bf16c(G)
+        _require_gpu(G)
+        N, F = (g.n_cols if g.n_cols is not None else g.n_rows), G.size(1) // 3
+        if g.shared:
+            dX = torch.empty(N, F, device=G.device, dtype=torch.bfloat16)
+            ro = g.row_order if g.symmetric else None
+            fl = default_flags() if flags is None else flags
+            rc = lib.pg_spmm3t_bf16(N, _p(g.rowptr_t), _p(ro), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX),
+                                    dX.stride(0), fl, _stream(G))
+            if rc != _lib.PG_ERR_UNSUPPORTED:
+                check(rc, "pg_spmm3t_bf16")
+                return dX
+        return spmm3_t(g, G.float(), flags).to(torch.bfloat16)
     G = _f32c(G)
     _require_gpu(G)
     N, F = (g.n_cols if g.n_cols is not None else g.n_rows), G.size(1) // 3
@@ -180,6 +230,27 @@ def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
     return out
 
 
+_PACK16_CACHE: dict = {}
+
+
+def pack_weights_bf16(prm: dict, W_res=None, b_res=None):
+    """(fp32 packed operand, its bf16 copy [F_out*K]) for pg_directgcn_dense_bf16; cached like pack_weights."""
+    packed = pack_weights(prm, W_res, b_res)
+    key = (packed.data_ptr(), _version_key([prm[k] for k in _PACK_KEYS] + [W_res, b_res]))
+    hit = _PACK16_CACHE.get(key)
+    if hit is not None:
+        return packed, hit
+    lib = load_library()
+    F_out, F_in = prm["W_main_in"].shape
+    n = F_out * (4 if W_res is not None else 3) * F_in
+    out = torch.empty(n, device=packed.device, dtype=torch.bfloat16)
+    check(lib.pg_f32_to_bf16(n, _p(packed), _p(out), _stream(packed)), "pg_f32_to_bf16")
+    if len(_PACK16_CACHE) >= 32:
+        _PACK16_CACHE.pop(next(iter(_PACK16_CACHE)))
+    _PACK16_CACHE[key] = out
+    return packed, out
+
+
 _PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in", "b_dir_shared_in",
               "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared")
 
@@ -200,8 +271,9 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
     a = LayerArgs()
     a.M, a.F_in, a.F_out = M, F_in, F_out
-    Zc = _f32c(Z.detach())
-    a.Z, a.ldz = c(Zc), Zc.stride(0)
+    Zc = _bf16c(Z.detach()) if _is_bf16(Z) else _f32c(Z.detach())
+    keep.append(Zc)
+    a.Z, a.ldz = _p(Zc), Zc.stride(0)
     a.gate_mode = gate_mode
     a.C_in, a.C_out, a.C_directed = c(prm["C_in"]), c(prm["C_out"]), c(prm["C_directed"])
     a.C_undirected, a.C_all = c(prm["C_undirected"]), c(prm["C_all"])
@@ -209,7 +281,7 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     if constant is not None:
         a.constant, a.ld_const = c(constant), constant.size(1)
     if res_x is not None:
-        rx = _f32c(res_x.detach())
+        rx = _bf16c(res_x.detach()) if _is_bf16(Z) else _f32c(res_x.detach())
         keep.append(rx)
         a.res_x, a.ld_res = _p(rx), rx.stride(0)
     a.W_res = c(W_res)
@@ -221,9 +293,16 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
                 act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
-    """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header)."""
+    """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header). bf16 Z ->
+    pg_directgcn_dense_bf16 (bf16 output)."""
     lib = load_library()
     _require_gpu(Z)
+    if _is_bf16(Z):
+        Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags)
+        if Y is not None:
+            return Y
+        return layer_dense(Z.float(), prm, gate_mode, rows, constant, None if res_x is None else res_x.float(),
+                           W_res, b_res, act, slope, flags).to(torch.bfloat16)
     packed = pack_weights(prm, W_res, b_res)
     M = Z.size(0)
     F_out = prm["W_main_in"].size(0)
@@ -233,6 +312,23 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     fl = default_flags() if flags is None else flags
     check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
     del keep
+    return Y
+
+
+def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags):
+    lib = load_library()
+    packed, p16 = pack_weights_bf16(prm, W_res, b_res)
+    M = Z.size(0)
+    F_out = prm["W_main_in"].size(0)
+    Y = torch.empty(M, F_out, device=Z.device, dtype=torch.bfloat16)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
+    a.Y, a.ldy = _p(Y), Y.stride(0)
+    fl = default_flags() if flags is None else flags
+    rc = lib.pg_directgcn_dense_bf16(ctypes.byref(a), _p(packed), _p(p16), fl, _stream(Z))
+    del keep
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_directgcn_dense_bf16")
     return Y
 
 
@@ -285,15 +381,23 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
 
 
 def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
-    """Fused decoder + log_softmax + L2-normalised embedding (eval-mode forward, no autograd)."""
+    """Fused decoder + log_softmax + L2-normalised embedding (eval-mode forward, no autograd). A bf16 h
+    (bf16 mode) is read as bf16 (pg_directgcn_head_bf16); outputs are fp32."""
     lib = load_library()
-    h = _f32c(h.detach())
     _require_gpu(h)
     M, F = h.shape
     H, C = W1.size(0), W2.size(0)
     W1, b1, W2, b2 = (_f32c(t.detach()) for t in (W1, b1, W2, b2))
     logp = torch.empty(M, C, device=h.device, dtype=torch.float32)
     emb = torch.empty(M, F, device=h.device, dtype=torch.float32)
+    if _is_bf16(h):
+        hb = _bf16c(h.detach())
+        rc = lib.pg_directgcn_head_bf16(M, F, H, C, _p(hb), hb.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), float(eps),
+                                        _p(logp), logp.stride(0), _p(emb), emb.stride(0), _stream(hb))
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_directgcn_head_bf16")
+            return logp, emb
+    h = _f32c(h.detach())
     check(lib.pg_directgcn_head_f32(M, F, H, C, _p(h), h.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), float(eps),
                                     _p(logp), logp.stride(0), _p(emb), emb.stride(0), _stream(h)),
           "pg_directgcn_head_f32")
@@ -325,10 +429,28 @@ def gemm_at_b(A: torch.Tensor, B: torch.Tensor):
 # autograd
 # ------------------------------------------------------------------------------------------------
 # The reference trainer runs the model under torch.amp.autocast (protgram_directgcn_trainer.py:93):
-# the Functions below take fp32 inputs and compute in fp32 inside autocast regions (at least the
-# reference's precision; the kernels are fp32-only).
-_fwd32 = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-_bwd32 = torch.amp.custom_bwd(device_type="cuda")
+# the Functions below compute in the model's own dtype inside autocast regions (fp32, or bf16 in the
+# explicit bf16 mode) -- at least the reference's fp16-GEMM precision.
+# bf16 inputs (the model's bf16 mode) are kept as they are; fp16 (autocast's default dtype) is widened.
+
+
+def _fwd32(fn):
+    @functools.wraps(fn)
+    def forward(ctx, *args):
+        if torch.is_autocast_enabled("cuda"):
+            args = tuple(a.float() if torch.is_tensor(a) and a.dtype == torch.float16 else a for a in args)
+            with torch.autocast("cuda", enabled=False):
+                return fn(ctx, *args)
+        return fn(ctx, *args)
+    return forward
+
+
+def _bwd32(fn):
+    @functools.wraps(fn)
+    def backward(ctx, *grads):
+        with torch.autocast("cuda", enabled=False):
+            return fn(ctx, *grads)
+    return backward
 class Propagate3(torch.autograd.Function):
     """x [N, F] -> Z [N, 3F] = [A_in x | A_out x | A_und x]; backward = transposed propagation."""
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Config 3 training step (4-gram, dims [128,128,128], C=20): reference loop of
+"""Config 3 / 5 training step (4-gram, dims [128,128,128] or --dims=128,256,256,256, C=20): reference loop of
 protgram_directgcn_trainer.py:91-100 (nll + 1e-7 * sum ||p||^2, Adam lr 1e-3). Prints ms/step."""
 import os
 import sys
@@ -15,13 +15,17 @@ from __graft_entry__ import load_package  # noqa: E402
 pkg = load_package()
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 amp = "--amp" in sys.argv
+dims = [128, 128, 128]
+for a in sys.argv:
+    if a.startswith("--dims="):
+        dims = [int(v) for v in a.split("=", 1)[1].split(",")]
 dev = torch.device("cuda:0")
 n = 4
 N, s, d, c = pkg.synth.de_bruijn_edges(n)
 g = pkg.build_propagation_csr(N, s, d, c, device=dev)
 torch.manual_seed(0)
-model = pkg.ProtGramDirectGCN([128, 128, 128], N, 20, n, 0, 512, 0.5, True).to(dev)
-x = torch.randn(N, 128, generator=torch.Generator().manual_seed(1234)).to(dev)
+model = pkg.ProtGramDirectGCN(dims, N, 20, n, 0, 512, 0.5, True).to(dev)
+x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(dev)
 y = torch.arange(N, device=dev) // (20 ** (n - 1))
 data = pkg.Data(x=x, graph=g)
 opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
@@ -49,4 +53,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step (amp={amp}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

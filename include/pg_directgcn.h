@@ -254,6 +254,13 @@ int pg_spmm3t_bf16(int64_t n_rows, const int64_t* rowptr, const int32_t* row_ord
 int pg_directgcn_dense_bf16(const pg_layer_args_t* args, const float* packed, const uint16_t* packed_bf16,
                             uint32_t flags, void* stream);
 
+/* pg_directgcn_dense_bwd_f32 in bf16 mode (bf16 MFMA products, fp32 sums): in `args` Z, res_x and Y are
+ * bf16, in `grads` dY, dpre, dZ and dres are bf16; dgate, gates, dW and work stay fp32. Same workspace
+ * (pg_directgcn_dense_bwd_workspace) and output layout as the fp32 entry point. Needs F_in, F_out and
+ * every leading dimension a multiple of 8 and 16-B aligned buffers (else PG_ERR_UNSUPPORTED). */
+int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* args, const float* packed, const uint16_t* packed_bf16,
+                                const pg_layer_grad_args_t* grads, uint32_t flags, void* stream);
+
 /* pg_directgcn_head_f32 with a bf16 input h (bf16 mode); outputs stay fp32. Needs the fast-path shape
  * (F <= 256, H <= 128, C <= 64; F, H, ldh, lde multiples of 4), else PG_ERR_UNSUPPORTED. */
 int pg_directgcn_head_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uint16_t* h, int64_t ldh,

@@ -89,6 +89,8 @@ SIGNATURES = {
     "pg_spmm3_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_directgcn_dense_bf16": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp, c_u32, c_vp]),
+    "pg_directgcn_dense_bwd_bf16": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp, ctypes.POINTER(LayerGradArgs),
+                                                   c_u32, c_vp]),
     "pg_directgcn_head_bf16": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                               c_vp, c_i64, c_vp, c_i64, c_vp]),
     "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),

@@ -16,28 +16,19 @@
 // i.e. one ds_read_b128 of a k-contiguous LDS row each; C/D: col = lane&31, row = (r&3)+8(r>>2)+4h.
 #include <algorithm>
 
+#include "pg_bf16_util.h"
 #include "pg_common.h"
 
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
-__device__ __forceinline__ uint32_t f2bf(float f) {  // c10::BFloat16 round_to_nearest_even
-    const uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
-    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-}
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
-__device__ __forceinline__ void unpack8(uint4 v, float (&f)[8]) {
-    f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
-    f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
-}
-__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
-    return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
-}
+using pgbf::bf16x8;
+using pgbf::f2bf;
+using pgbf::pack2;
+using pgbf::pack8;
+using pgbf::unpack8;
+__device__ __forceinline__ float bf_lo(uint32_t w) { return pgbf::lo(w); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return pgbf::hi(w); }
 __device__ __forceinline__ float fb(int v) { return __int_as_float(v); }
 
 // ------------------------------------------------------------------------------------------------

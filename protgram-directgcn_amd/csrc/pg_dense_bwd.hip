@@ -24,6 +24,7 @@
 //   sums them in split order (deterministic, no atomics).
 #include <algorithm>
 
+#include "pg_bf16_util.h"
 #include "pg_common.h"
 
 namespace {
@@ -530,6 +531,438 @@ void launch_reduce(int64_t n4, int splits, int64_t stride, const float* part, fl
                        part, out);
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16 mode: the same two products on v_mfma_f32_32x32x16_bf16 (bf16 operands, fp32 sums)
+// ------------------------------------------------------------------------------------------------
+constexpr int BKB = 64;  // K per dgrad tile (4 MFMA k-steps)
+constexpr int LDKB = 72; // dgrad LDS row in bf16 (144 B: conflict-free ds_read_b128)
+
+struct DgradB {
+    int64_t M;
+    int F_in, F_out, N;
+    const uint16_t* dY;
+    int64_t lddy;
+    const uint16_t* Y;
+    int64_t ldy;
+    int act;
+    float slope;
+    const uint16_t* BT;  // [N, F_out] bf16
+    const float* bsum;   // [4, F_out]
+    const uint16_t* Z;
+    int64_t ldz;
+    Gates g;
+    uint16_t* dpre;
+    int64_t ldp;
+    uint16_t* dZ;
+    int64_t lddz;
+    uint16_t* dres;
+    int64_t lddres;
+    float* gates;
+    float* dsp;
+    int remap;
+};
+
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(64 * NW) void dgrad_bf16_kernel(DgradB p) {
+    using namespace pgbf;
+    constexpr int NT = 64 * NW;
+    constexpr int WN = 2, WM = NW / WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static_assert(TM >= 1 && TN >= 1, "wave tile");
+    constexpr int A_C = BM * BKB / 8 / NT;
+    constexpr int B_C = BN * BKB / 8 / NT;
+    static_assert(A_C >= 1 && B_C >= 1, "chunks");
+    constexpr int TLD = BN + 4;
+    constexpr int MAIN_BYTES = 2 * (BM + BN) * LDKB * 2;
+    constexpr int EPI_BYTES = BM * TLD * 4;
+    constexpr int SMEM_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ float Bd[BM * 3];
+    uint16_t* As = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* Bs = As + 2 * BM * LDKB;
+
+    const int ntn = (p.N + BN - 1) / BN;
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int nt = (int)(lb % ntn);
+    const int64_t m0 = (lb / ntn) * BM;
+    const int n0 = nt * BN;
+    const bool lead = nt == 0;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+
+    if (tid < BM) {
+        const int64_t m = m0 + tid;
+        float4 sv = make_float4(0.f, 0.f, 0.f, 1.f);
+        if (m < p.M) {
+            float ci, co, cd, cu, ca;
+            gate_values(p.g, m, ci, co, cd, cu, ca);
+            const float cad = ca * cd;
+            sv.x = cad * ci;
+            sv.y = cad * co;
+            sv.z = ca * cu;
+            if (lead) st4(p.gates + m * 4, sv);
+        }
+        st4(&Sg[tid * 4], sv);
+    }
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    uint4 ra[A_C], ry[A_C], rb[B_C];
+    float bd[A_C][3];
+#pragma unroll
+    for (int q = 0; q < A_C; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
+    const int64_t mlast = p.M - 1;
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < A_C; ++q) {
+            const int idx = tid + NT * q;
+            const int64_t m = min(m0 + (idx >> 3), mlast);
+            const int k = k0 + 8 * (idx & 7);
+            const int kc = k < p.F_out ? k : 0;
+            ra[q] = *reinterpret_cast<const uint4*>(p.dY + m * p.lddy + kc);
+            if (p.act) ry[q] = *reinterpret_cast<const uint4*>(p.Y + m * p.ldy + kc);
+        }
+#pragma unroll
+        for (int q = 0; q < B_C; ++q) {
+            const int idx = tid + NT * q;
+            const int n = min(n0 + (idx >> 3), p.N - 1);
+            const int k = k0 + 8 * (idx & 7);
+            rb[q] = *reinterpret_cast<const uint4*>(p.BT + (int64_t)n * p.F_out + (k < p.F_out ? k : 0));
+        }
+    };
+    auto stash = [&](int buf, int k0) {
+        uint16_t* Ab = As + buf * BM * LDKB;
+        uint16_t* Bb = Bs + buf * BN * LDKB;
+#pragma unroll
+        for (int q = 0; q < A_C; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 8 * (idx & 7);
+            const int64_t m = m0 + (idx >> 3);
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (k < p.F_out) {
+                float d[8];
+                unpack8(ra[q], d);
+                if (p.act) {
+                    float y[8];
+                    unpack8(ry[q], y);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d[e] = y[e] > 0.f ? d[e] : d[e] * p.slope;
+                }
+                v = pack8(d);
+                if (lead && m < p.M) {
+                    *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
+                    float dr[8];
+                    unpack8(v, dr);  // the rounded gradient, as the products below see it
+#pragma unroll
+                    for (int sg = 0; sg < 3; ++sg) {
+                        const float4 b0 = ld4(p.bsum + sg * p.F_out + k), b1 = ld4(p.bsum + sg * p.F_out + k + 4);
+                        bd[q][sg] += dr[0] * b0.x + dr[1] * b0.y + dr[2] * b0.z + dr[3] * b0.w + dr[4] * b1.x +
+                                     dr[5] * b1.y + dr[6] * b1.z + dr[7] * b1.w;
+                    }
+                }
+            }
+            *reinterpret_cast<uint4*>(&Ab[(idx >> 3) * LDKB + 8 * (idx & 7)]) = v;
+        }
+#pragma unroll
+        for (int q = 0; q < B_C; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 8 * (idx & 7);
+            *reinterpret_cast<uint4*>(&Bb[(idx >> 3) * LDKB + 8 * (idx & 7)]) =
+                k < p.F_out ? rb[q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+
+    const int ntiles = (p.F_out + BKB - 1) / BKB;
+    fetch(0);
+    stash(0, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < ntiles) fetch((t + 1) * BKB);
+        const uint16_t* Ab = As + cur * BM * LDKB;
+        const uint16_t* Bb = Bs + cur * BN * LDKB;
+#pragma unroll
+        for (int kk = 0; kk < BKB / 16; ++kk) {
+            bf16x8 a[TM], b[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                      &Ab[(wm * TM * 32 + i * 32 + li) * LDKB + kk * 16 + 8 * lh]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                      &Bb[(wn * TN * 32 + j * 32 + li) * LDKB + kk * 16 + 8 * lh]));
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BKB);
+        __syncthreads();
+    }
+
+    if (lead) {
+#pragma unroll
+        for (int q = 0; q < A_C; ++q) {
+#pragma unroll
+            for (int sg = 0; sg < 3; ++sg) {
+                float v = bd[q][sg];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                bd[q][sg] = v;
+            }
+            const int idx = tid + NT * q;
+            if ((idx & 7) == 0) {
+                Bd[(idx >> 3) * 3 + 0] = bd[q][0];
+                Bd[(idx >> 3) * 3 + 1] = bd[q][1];
+                Bd[(idx >> 3) * 3 + 2] = bd[q][2];
+            }
+        }
+    }
+
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                T[rl * TLD + wn * TN * 32 + j * 32 + li] = acc[i][j][r];
+            }
+    __syncthreads();
+
+    constexpr int C4 = BN / 4;
+    constexpr int ITER = BM * C4 / NT;
+    constexpr int BATCH = ITER < 4 ? ITER : 4;
+    const int c4 = tid % C4;
+    const int j = n0 + 4 * c4;
+    const int seg = j < p.N ? j / p.F_in : 4;
+    for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+        uint2 zv[BATCH];
+        int rl[BATCH];
+        int64_t mm[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            rl[u] = (tid + NT * (it0 + u)) / C4;
+            mm[u] = m0 + rl[u];
+            zv[u] = make_uint2(0u, 0u);
+            if (mm[u] < p.M && seg < 3) zv[u] = *reinterpret_cast<const uint2*>(p.Z + mm[u] * p.ldz + j);
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            float part = 0.f;
+            if (mm[u] < p.M && seg < 4) {
+                const float4 gv = ld4(&T[rl[u] * TLD + 4 * c4]);
+                if (seg < 3) {
+                    const float sc = Sg[rl[u] * 4 + seg];
+                    if (p.dZ)
+                        *reinterpret_cast<uint2*>(p.dZ + mm[u] * p.lddz + j) =
+                            pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
+                    part = dot4(gv, unpack4(zv[u]));
+                } else {
+                    *reinterpret_cast<uint2*>(p.dres + mm[u] * p.lddres + (j - 3 * p.F_in)) = pack4(gv);
+                }
+            }
+            T[rl[u] * TLD + 4 * c4] = part;
+        }
+    }
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+        const int64_t m = m0 + tid;
+        float ds[3] = {0.f, 0.f, 0.f};
+        if (lead) {
+            ds[0] = Bd[tid * 3 + 0];
+            ds[1] = Bd[tid * 3 + 1];
+            ds[2] = Bd[tid * 3 + 2];
+        }
+        for (int c = 0; c < C4; ++c) {
+            const int jj = n0 + 4 * c;
+            if (jj >= p.N) break;
+            const int q = jj / p.F_in;
+            if (q < 3) ds[q] += T[tid * TLD + 4 * c];
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
+    }
+}
+
+struct WgradB {
+    int64_t M;
+    int P, N, F_in;
+    const uint16_t* A;  // dpre [M, P] bf16
+    int64_t lda;
+    const uint16_t* Z;  // [M, >= 3 F_in] bf16
+    int64_t ldz;
+    const uint16_t* R;  // segment 3 (projected residual input) bf16, or null
+    int64_t ldr;
+    const float* gates; // [M, 4]
+    int64_t rows_per_split;
+    int64_t part_stride;
+    float* part;
+};
+
+constexpr int WRB = 32;  // rows per K step (2 MFMA k-steps)
+constexpr int LDM = 40;  // transposed LDS row in bf16: 32 rows + 8 pad (80 B: conflict-free ds_read_b128)
+
+// C[P x N] = A^T diag(s) B with both operands staged TRANSPOSED in LDS (rows of the K step along the LDS
+// row), so each MFMA operand (8 consecutive K = rows) is one ds_read_b128. Waves 0-3 stage A (and sum
+// the bias gradients), waves 4-7 stage s*B; a thread owns a row pair x 8 columns and writes each column's
+// two rows as one 32-bit LDS word.
+__global__ __launch_bounds__(512) void wgrad_bf16_kernel(WgradB p) {
+    using namespace pgbf;
+    constexpr int BI = 128, BJ = 128;
+    __shared__ __attribute__((aligned(16))) uint16_t At[2][BI * LDM];
+    __shared__ __attribute__((aligned(16))) uint16_t Bt[2][BJ * LDM];
+    const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI;
+    const int64_t r0 = (int64_t)blockIdx.z * p.rows_per_split;
+    const int64_t rend = min(r0 + p.rows_per_split, p.M);
+    const bool do_db = blockIdx.x == 0;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wi = wave >> 1, wj = wave & 1;  // wave tile 32 (i) x 64 (j)
+    const int li = lane & 31, lh = lane >> 5;
+    const int half = tid >> 8, lt = tid & 255;
+    const int rp = lt & 15, cg = lt >> 4;
+    const int col = (half ? j0 : i0) + 8 * cg;
+    const bool col_ok = col < (half ? p.N : p.P);
+    const int seg = (half && col_ok) ? col / p.F_in : 0;
+    const uint16_t* src = half ? (seg < 3 ? p.Z + col : p.R + (col - 3 * p.F_in)) : p.A + col;
+    const int64_t ld = half ? (seg < 3 ? p.ldz : p.ldr) : p.lda;
+    const bool need_s = half || do_db;
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    float db[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) db[q][e] = 0.f;
+
+    uint4 v0, v1;
+    float4 s0 = make_float4(1.f, 1.f, 1.f, 1.f), s1 = s0;
+    const int64_t mlast = p.M - 1;
+    auto fetch = [&](int64_t base) {
+        const int64_t ma = min(base + 2 * rp, mlast), mb = min(base + 2 * rp + 1, mlast);
+        v0 = col_ok ? *reinterpret_cast<const uint4*>(src + ma * ld) : make_uint4(0u, 0u, 0u, 0u);
+        v1 = col_ok ? *reinterpret_cast<const uint4*>(src + mb * ld) : make_uint4(0u, 0u, 0u, 0u);
+        if (need_s && p.gates) {
+            s0 = ld4(p.gates + ma * 4);
+            s1 = ld4(p.gates + mb * 4);
+        }
+    };
+    auto stash = [&](int buf, int64_t base) {
+        const bool oka = col_ok && base + 2 * rp < rend, okb = col_ok && base + 2 * rp + 1 < rend;
+        float fa[8], fb2[8];
+        unpack8(v0, fa);
+        unpack8(v1, fb2);
+        uint32_t ba[8], bb[8];
+        if (half) {
+            const float sa = seg == 0 ? s0.x : seg == 1 ? s0.y : seg == 2 ? s0.z : 1.f;
+            const float sb = seg == 0 ? s1.x : seg == 1 ? s1.y : seg == 2 ? s1.z : 1.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                ba[e] = oka ? f2bf(fa[e] * sa) : 0u;
+                bb[e] = okb ? f2bf(fb2[e] * sb) : 0u;
+            }
+        } else {
+            const uint32_t wa[4] = {v0.x, v0.y, v0.z, v0.w}, wb[4] = {v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                ba[e] = oka ? ((e & 1) ? wa[e >> 1] >> 16 : wa[e >> 1] & 0xffffu) : 0u;
+                bb[e] = okb ? ((e & 1) ? wb[e >> 1] >> 16 : wb[e >> 1] & 0xffffu) : 0u;
+            }
+            if (do_db) {
+                const float sa[4] = {s0.x, s0.y, s0.z, 1.f}, sb[4] = {s1.x, s1.y, s1.z, 1.f};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        db[q][e] += (oka ? sa[q] * fa[e] : 0.f) + (okb ? sb[q] * fb2[e] : 0.f);
+            }
+        }
+        uint16_t* T = half ? Bt[buf] : At[buf];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            *reinterpret_cast<uint32_t*>(&T[(8 * cg + e) * LDM + 2 * rp]) = ba[e] | (bb[e] << 16);
+    };
+
+    const int64_t nsteps = (rend - r0 + WRB - 1) / WRB;
+    if (nsteps > 0) {
+        fetch(r0);
+        stash(0, r0);
+    }
+    __syncthreads();
+    for (int64_t t = 0; t < nsteps; ++t) {
+        const int cur = (int)(t & 1);
+        const int64_t nb = r0 + (t + 1) * WRB;
+        if (t + 1 < nsteps) fetch(nb);
+#pragma unroll
+        for (int ks = 0; ks < WRB / 16; ++ks) {
+            const bf16x8 a = __builtin_bit_cast(
+                bf16x8, *reinterpret_cast<const uint4*>(&At[cur][(wi * 32 + li) * LDM + ks * 16 + 8 * lh]));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8 b = __builtin_bit_cast(
+                    bf16x8, *reinterpret_cast<const uint4*>(&Bt[cur][(wj * 64 + j * 32 + li) * LDM + ks * 16 + 8 * lh]));
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+            }
+        }
+        if (t + 1 < nsteps) stash(cur ^ 1, nb);
+        __syncthreads();
+    }
+
+    float* out = p.part + (int64_t)blockIdx.z * p.part_stride;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int oi = i0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const int oj = j0 + wj * 64 + j * 32 + li;
+            if (oi < p.P && oj < p.N) out[(int64_t)oi * p.N + oj] = acc[j][r];
+        }
+    if (do_db && !half) {  // sum the 16 row pairs of each column group (16 consecutive lanes)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float v = db[q][e];
+                v += __shfl_xor(v, 1, 16);
+                v += __shfl_xor(v, 2, 16);
+                v += __shfl_xor(v, 4, 16);
+                v += __shfl_xor(v, 8, 16);
+                db[q][e] = v;
+            }
+        if (rp == 0 && col_ok) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (col + e < p.P) out[(int64_t)p.P * p.N + q * p.P + col + e] = db[q][e];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void transpose_u16_kernel(int R, int C, const uint16_t* in, uint16_t* out) {
+    const int64_t total = (int64_t)R * C;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i / R), r = (int)(i % R);
+        out[i] = in[(int64_t)r * C + c];
+    }
+}
+
 constexpr int DG_BM = 128, DG_BN = 128, DG_NW = 8, WG_NW = 8;
 
 struct BwdPlan {
@@ -732,6 +1165,112 @@ int pg_gemm_at_b_f32(int64_t M, int64_t P, int64_t N, const float* A, int64_t ld
     hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
     launch_reduce((P * N + P) / 4, sp.splits, stride, work, out, s);  // C, then colsum(A) (db row 0)
     return pg::check_launch("pg_gemm_at_b_f32");
+}
+
+int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, const uint16_t* packed_bf16,
+                                const pg_layer_grad_args_t* g, uint32_t flags, void* stream) {
+    PG_REQUIRE(a != nullptr && packed != nullptr && packed_bf16 != nullptr && g != nullptr, "null args");
+    PG_REQUIRE(a->M >= 0 && a->F_in > 0 && a->F_out > 0 && a->F_in < (1 << 20) && a->F_out < (1 << 20), "bad shape");
+    PG_REQUIRE(a->C_in && a->C_out && a->C_directed && a->C_undirected && a->C_all, "null gate");
+    PG_REQUIRE(a->gate_mode == PG_GATES_VECTOR || a->gate_mode == PG_GATES_SCALAR, "bad gate_mode");
+    PG_REQUIRE(!a->W_res || a->res_x, "W_res needs res_x");
+    PG_REQUIRE(g->dY && g->dpre && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
+    PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
+    PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
+    const bool proj = a->W_res != nullptr;
+    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj);
+    PG_REQUIRE(g->work_floats >= pl.total, "workspace too small");
+    const uint16_t* Zb = reinterpret_cast<const uint16_t*>(a->Z);
+    const uint16_t* Yb = reinterpret_cast<const uint16_t*>(a->Y);
+    const uint16_t* Rb = reinterpret_cast<const uint16_t*>(a->res_x);
+    const uint16_t* dYb = reinterpret_cast<const uint16_t*>(g->dY);
+    uint16_t* dpb = reinterpret_cast<uint16_t*>(g->dpre);
+    uint16_t* dZb = reinterpret_cast<uint16_t*>(g->dZ);
+    uint16_t* drb = reinterpret_cast<uint16_t*>(g->dres);
+    const bool ok = a->F_in % 8 == 0 && a->F_out % 8 == 0 && a->ldz % 8 == 0 && g->lddy % 8 == 0 && g->ldp % 8 == 0 &&
+                    (!a->act || a->ldy % 8 == 0) && (!dZb || (g->lddz % 4 == 0 && (reinterpret_cast<uintptr_t>(dZb) & 7) == 0)) &&
+                    (!proj || (a->ld_res % 8 == 0 && g->lddres % 4 == 0 && pg::aligned16(Rb) &&
+                               (reinterpret_cast<uintptr_t>(drb) & 7) == 0)) &&
+                    pg::aligned16(Zb) && pg::aligned16(dYb) && pg::aligned16(dpb) && pg::aligned16(g->gates) &&
+                    pg::aligned16(g->dW) && pg::aligned16(g->work) && pg::aligned16(packed) &&
+                    pg::aligned16(packed_bf16) && (!a->act || pg::aligned16(Yb));
+    if (!ok)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_bwd_bf16: needs F_in, F_out and leading dims "
+                                                 "multiples of 8 and aligned buffers");
+    PG_REQUIRE(a->ldz >= 3 * a->F_in && (!dZb || g->lddz >= 3 * a->F_in) && g->lddy >= a->F_out &&
+                   g->ldp >= a->F_out,
+               "leading dimensions too small");
+    hipStream_t s = (hipStream_t)stream;
+    const int K = pl.K;
+    const int F_in = (int)a->F_in, F_out = (int)a->F_out;
+    if (a->M == 0) {
+        if (hipMemsetAsync(g->dW, 0, sizeof(float) * ((int64_t)F_out * K + 4 * F_out), s) != hipSuccess)
+            return pg::set_error(PG_ERR_HIP, "pg_directgcn_dense_bwd_bf16: memset failed");
+        return PG_OK;
+    }
+    uint16_t* BT = reinterpret_cast<uint16_t*>(g->work + pl.off_bt);
+    float* dsp = g->work + pl.off_dsp;
+    float* part = g->work + pl.off_part;
+    {
+        const int64_t total = (int64_t)K * F_out;
+        const int nb = (int)std::min<int64_t>((total + 255) / 256, 1024);
+        hipLaunchKernelGGL(transpose_u16_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed_bf16, BT);
+    }
+    Gates gt{a->gate_mode, a->C_in, a->C_out, a->C_directed, a->C_undirected, a->C_all, a->rows};
+    {
+        DgradB p{};
+        p.M = a->M;
+        p.F_in = F_in;
+        p.F_out = F_out;
+        p.N = K;
+        p.dY = dYb;
+        p.lddy = g->lddy;
+        p.Y = Yb;
+        p.ldy = a->ldy;
+        p.act = a->act;
+        p.slope = a->slope;
+        p.BT = BT;
+        p.bsum = packed + (int64_t)F_out * K;
+        p.Z = Zb;
+        p.ldz = a->ldz;
+        p.g = gt;
+        p.dpre = dpb;
+        p.ldp = g->ldp;
+        p.dZ = dZb;
+        p.lddz = g->lddz;
+        p.dres = drb;
+        p.lddres = g->lddres;
+        p.gates = g->gates;
+        p.dsp = dsp;
+        p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+        const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
+        hipLaunchKernelGGL((dgrad_bf16_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
+    }
+    {
+        const int nb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);
+        hipLaunchKernelGGL(gate_grad_kernel, dim3(nb), dim3(256), 0, s, a->M, pl.ntn, (const float*)dsp, gt, g->dgate);
+    }
+    {
+        WgradB w{};
+        w.M = a->M;
+        w.P = F_out;
+        w.N = K;
+        w.F_in = F_in;
+        w.A = dpb;
+        w.lda = g->ldp;
+        w.Z = Zb;
+        w.ldz = a->ldz;
+        w.R = Rb;
+        w.ldr = a->ld_res;
+        w.gates = g->gates;
+        w.rows_per_split = pl.rows_per_split;
+        w.part_stride = pl.part_stride;
+        w.part = part;
+        dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
+        hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(512), 0, s, w);
+    }
+    launch_reduce(pl.part_stride / 4, pl.splits, pl.part_stride, part, g->dW, s);
+    return pg::check_launch("pg_directgcn_dense_bwd_bf16");
 }
 
 }  // extern "C"

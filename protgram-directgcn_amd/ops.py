@@ -20,6 +20,8 @@ from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
 
+BF16_BACKWARD = True  # bf16 mode trains through pg_directgcn_dense_bwd_bf16 / pg_spmm3t_bf16
+
 # Optional live timing of the propagation kernel: when set to a list, spmm3 appends one
 # (start, end) pair of HIP events recorded on the launch stream around each propagation launch.
 SPMM_EVENTS: Optional[list] = None
@@ -287,7 +289,9 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     a.W_res = c(W_res)
     a.act, a.slope = int(bool(act)), float(slope)
     if Y is not None:
-        a.Y, a.ldy = c(Y), Y.stride(0)
+        Yc = Y.detach().contiguous()
+        keep.append(Yc)
+        a.Y, a.ldy = _p(Yc), Yc.stride(0)
     return a, keep
 
 
@@ -344,16 +348,22 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     _require_gpu(dY, Z, Y)
     M, F_in = Z.size(0), Z.size(1) // 3
     F_out = prm["W_main_in"].size(0)
-    if F_in % 4 or F_out % 4:
+    bf = _is_bf16(Z)
+    if (F_in % 8 or F_out % 8) if bf else (F_in % 4 or F_out % 4):
         return None
-    packed = pack_weights(prm, W_res, b_res)
+    if bf:
+        packed, p16 = pack_weights_bf16(prm, W_res, b_res)
+        Y = _bf16c(Y)
+    else:
+        packed = pack_weights(prm, W_res, b_res)
     a, keep = _layer_args(Z, prm, gate_mode, rows, None, res_x, W_res, act, slope, Y=Y)
     dev = Z.device
     K = (4 if W_res is not None else 3) * F_in
-    dYc = _f32c(dY)
-    dpre = torch.empty(M, F_out, device=dev)
-    dZ = torch.empty(M, 3 * F_in, device=dev) if need_dZ else None
-    dres = torch.empty(M, F_in, device=dev) if W_res is not None else None
+    act_dt = torch.bfloat16 if bf else torch.float32
+    dYc = _bf16c(dY) if bf else _f32c(dY)
+    dpre = torch.empty(M, F_out, device=dev, dtype=act_dt)
+    dZ = torch.empty(M, 3 * F_in, device=dev, dtype=act_dt) if need_dZ else None
+    dres = torch.empty(M, F_in, device=dev, dtype=act_dt) if W_res is not None else None
     dgate = torch.empty(5, M, device=dev)
     gates = torch.empty(M, 4, device=dev)
     dW = torch.empty(F_out * K + 4 * F_out, device=dev)
@@ -371,10 +381,13 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     g.dgate, g.gates, g.dW = _p(dgate), _p(gates), _p(dW)
     g.work, g.work_floats = _p(work), work.numel()
     fl = default_flags() if flags is None else flags
-    rc = lib.pg_directgcn_dense_bwd_f32(ctypes.byref(a), _p(packed), ctypes.byref(g), fl, _stream(Z))
+    if bf:
+        rc = lib.pg_directgcn_dense_bwd_bf16(ctypes.byref(a), _p(packed), _p(p16), ctypes.byref(g), fl, _stream(Z))
+    else:
+        rc = lib.pg_directgcn_dense_bwd_f32(ctypes.byref(a), _p(packed), ctypes.byref(g), fl, _stream(Z))
     if rc == _lib.PG_ERR_UNSUPPORTED:
         return None
-    check(rc, "pg_directgcn_dense_bwd_f32")
+    check(rc, "pg_directgcn_dense_bwd_bf16" if bf else "pg_directgcn_dense_bwd_f32")
     del keep
     return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate,
             "dB": dW[:F_out * K].view(F_out, K), "dbsum": dW[F_out * K:].view(4, F_out)}
@@ -560,8 +573,15 @@ class LayerDense(torch.autograd.Function):
         rows = rows if ctx.has_rows else None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
                                    act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
-        if out is None:  # F_in / F_out not multiples of 4: the same algebra as torch GPU ops
-            out = _dense_backward_torch(dY, Z, Y, prm, ctx.gate_mode, rows, res_x, W_res, ctx.act, ctx.slope)
+        if out is None:  # shapes the HIP kernels do not take: the same algebra as torch GPU ops
+            if _is_bf16(Z):
+                out = _dense_backward_torch(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows,
+                                            None if res_x is None else res_x.float(), W_res, ctx.act, ctx.slope)
+                for k in ("dpre", "dZ", "dres"):
+                    if out[k] is not None:
+                        out[k] = out[k].to(torch.bfloat16)
+            else:
+                out = _dense_backward_torch(dY, Z, Y, prm, ctx.gate_mode, rows, res_x, W_res, ctx.act, ctx.slope)
         dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]
         M, F_in = Z.size(0), Z.size(1) // 3
         g = {}
@@ -589,10 +609,11 @@ class LayerDense(torch.autograd.Function):
         d_const = None
         if constant is not None and ctx.needs_input_grad[2]:
             d_const = torch.zeros_like(constant)
+            dp = dpre.to(constant.dtype)
             if rows is not None:
-                d_const.index_add_(0, rows, dpre)
+                d_const.index_add_(0, rows, dp)
             else:
-                d_const[:M] += dpre
+                d_const[:M] += dp
         d_res = d_wres = d_bres = None
         if res_x is not None:
             if W_res is None:

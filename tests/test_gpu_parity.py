@@ -655,3 +655,93 @@ def test_head_bf16_input_equals_widened(pkg, cuda, F, H, C):
     lp, emb = ops.head(h, W1, b1, W2, b2, 1e-12)
     lp32, emb32 = ops.head(h.float(), W1, b1, W2, b2, 1e-12)
     assert torch.equal(lp, lp32) and torch.equal(emb, emb32)
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
+                                                      (300, 32, 16, False, False, False), (5000, 256, 256, False, True, False),
+                                                      (129, 16, 40, True, True, True), (300, 20, 12, True, True, False)])
+def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+    """bf16-mode autograd of the dense layer (pg_directgcn_dense_bwd_bf16; the last case falls back to the
+    torch formulation) against float64 autograd on the same bf16-valued activations, with the leaky_relu
+    mask taken from the device's own (bf16) forward output -- near y = 0 a float64 forward can pick the
+    other slope. Tolerance: bf16 rounding of dpre, s*Z and the stored gradients, 2% of each gradient's max."""
+    from protgram_directgcn_amd import ops
+    Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, vec, rows, 13 * M + Fin)
+    Zb, dYb = Z.to(torch.bfloat16), dY.to(torch.bfloat16)
+    xb = xres.to(torch.bfloat16) if xres is not None else None
+    gate = 0 if vec else 1
+    d = {k: v.double().requires_grad_(True) for k, v in prm.items()}
+    Zd = Zb.double().requires_grad_(True)
+    xd = xb.double().requires_grad_(True) if xb is not None else None
+    cd = const.double().requires_grad_(True) if const is not None else None
+    Wrd = W_res.double().requires_grad_(True) if proj else None
+    brd = b_res.double().requires_grad_(True) if proj else None
+    idx = r if r is not None else torch.arange(M)
+    gv = (lambda k: d[k][idx]) if vec else (lambda k: d[k].expand(M, 1))
+    s = [gv("C_all") * gv("C_directed") * gv("C_in"), gv("C_all") * gv("C_directed") * gv("C_out"),
+         gv("C_all") * gv("C_undirected")]
+    Wk = [d["W_main_in"] + d["W_shared"], d["W_main_out"] + d["W_shared"], d["W_undirected"] + d["W_shared"]]
+    bk = [d["b_main_in"] + d["b_dir_shared_in"], d["b_main_out"] + d["b_dir_shared_out"],
+          d["b_undirected"] + d["b_undirected_shared"]]
+    y = sum(s[k] * (Zd[:, k * Fin:(k + 1) * Fin] @ Wk[k].t() + bk[k]) for k in range(3))
+    if cd is not None:
+        y = y + cd[idx]
+    if xd is not None:
+        y = y + (xd @ Wrd.t() + brd if proj else xd)
+    dv = {k: v.to(cuda).requires_grad_(True) for k, v in prm.items()}
+    Zg = Zb.to(cuda).requires_grad_(True)
+    xg = xb.to(cuda).requires_grad_(True) if xb is not None else None
+    cg = const.to(cuda).requires_grad_(True) if const is not None else None
+    Wrg = W_res.to(cuda).requires_grad_(True) if proj else None
+    brg = b_res.to(cuda).requires_grad_(True) if proj else None
+    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01,
+                               *[dv[k] for k in ops._DENSE_KEYS])
+    assert out.dtype == torch.bfloat16
+    mask = torch.where(out.detach().cpu().double() > 0, 1.0, 0.01)
+    (y * mask * dYb.double()).sum().backward()  # leaky_relu' from the device's forward output
+    out.backward(dYb.to(cuda))
+    assert Zg.grad.dtype == torch.bfloat16
+
+    def close(got, ref, what):
+        got, ref = got.detach().double().cpu(), ref.detach().double()
+        err = (got - ref).abs()
+        tol = 2e-2 * float(ref.abs().max()) + 2e-2 * ref.abs() + 1e-6
+        assert not bool((err > tol).any()), f"{what}: max |d| {float(err.max()):.3e} vs max|ref| {float(ref.abs().max()):.3e}"
+
+    close(Zg.grad, Zd.grad, "dZ")
+    for k in ops._DENSE_KEYS:
+        close(dv[k].grad, d[k].grad, f"d{k}")
+    if xg is not None:
+        close(xg.grad, xd.grad, "dres_x")
+    if cg is not None:
+        close(cg.grad, cd.grad, "dconstant")
+    if proj:
+        close(Wrg.grad, Wrd.grad, "dW_res")
+        close(brg.grad, brd.grad, "db_res")
+
+
+def test_model_bf16_training_step_close_to_fp32(pkg, cuda):
+    """One bf16-mode training step (autocast + GradScaler loop of the trainer) vs the fp32 model: the loss
+    agrees to bf16 precision and every parameter gradient points the same way (cosine > 0.99)."""
+    import torch.nn.functional as F
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    grads, losses = [], []
+    for dt in (torch.float32, torch.bfloat16):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 128, 128, 128], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        m.compute_dtype = dt
+        with torch.amp.autocast("cuda", enabled=True):
+            lp, _ = m(data)
+            loss = F.nll_loss(lp, y) + 1e-7 * sum(p.norm(2).pow(2) for p in m.parameters())
+        loss.backward()
+        losses.append(float(loss))
+        grads.append({k: p.grad.detach().float().clone() for k, p in m.named_parameters()})
+    assert abs(losses[0] - losses[1]) < 2e-2 * abs(losses[0])
+    for k, g32 in grads[0].items():
+        g16 = grads[1][k]
+        cos = float((g32 * g16).sum() / (g32.norm() * g16.norm() + 1e-30))
+        assert cos > 0.99, (k, cos)

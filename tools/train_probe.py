@@ -15,6 +15,7 @@ from __graft_entry__ import load_package  # noqa: E402
 pkg = load_package()
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 amp = "--amp" in sys.argv
+bf16 = "--bf16" in sys.argv
 dims = [128, 128, 128]
 for a in sys.argv:
     if a.startswith("--dims="):
@@ -27,6 +28,8 @@ torch.manual_seed(0)
 model = pkg.ProtGramDirectGCN(dims, N, 20, n, 0, 512, 0.5, True).to(dev)
 x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(dev)
 y = torch.arange(N, device=dev) // (20 ** (n - 1))
+if bf16:
+    model.compute_dtype = torch.bfloat16
 data = pkg.Data(x=x, graph=g)
 opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
 model.train()
@@ -53,4 +56,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step dims={dims} (amp={amp}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}, bf16={bf16}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

@@ -563,7 +563,7 @@ struct DgradB {
 };
 
 template <int BM, int BN, int NW>
-__global__ __launch_bounds__(64 * NW) void dgrad_bf16_kernel(DgradB p) {
+__global__ __launch_bounds__(64 * NW, 4) void dgrad_bf16_kernel(DgradB p) {
     using namespace pgbf;
     constexpr int NT = 64 * NW;
     constexpr int WN = 2, WM = NW / WN;
@@ -819,7 +819,7 @@ constexpr int LDM = 40;  // transposed LDS row in bf16: 32 rows + 8 pad (80 B: c
 // row), so each MFMA operand (8 consecutive K = rows) is one ds_read_b128. Waves 0-3 stage A (and sum
 // the bias gradients), waves 4-7 stage s*B; a thread owns a row pair x 8 columns and writes each column's
 // two rows as one 32-bit LDS word.
-__global__ __launch_bounds__(512) void wgrad_bf16_kernel(WgradB p) {
+__global__ __launch_bounds__(512, 4) void wgrad_bf16_kernel(WgradB p) {
     using namespace pgbf;
     constexpr int BI = 128, BJ = 128;
     __shared__ __attribute__((aligned(16))) uint16_t At[2][BI * LDM];

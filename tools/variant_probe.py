@@ -51,3 +51,26 @@ for _ in range(4):
         res[k].append(timeit(fn))
 for k, v in res.items():
     print(f"{k:10s} " + " ".join(f"{t:.4f}" for t in v) + f"   min {min(v):.4f}")
+
+# dense backward (fp32 and bf16) at this F, identity residual, vector gates
+torch.manual_seed(0)
+layer = pkg.DirectGCNLayer(F, F, N).to(dev)
+prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
+Z32 = ops.spmm3(g, x32)
+Z16 = ops.spmm3(g, x16)
+Y32 = ops.layer_dense(Z32, prm, 0, constant=layer.constant.detach(), res_x=x32, act=True)
+Y16 = ops.layer_dense(Z16, prm, 0, constant=layer.constant.detach(), res_x=x16, act=True)
+dY32 = torch.randn(N, F, device=dev)
+dY16 = dY32.to(torch.bfloat16)
+bw = {
+    "dense_f32": lambda: ops.layer_dense(Z32, prm, 0, constant=layer.constant.detach(), res_x=x32, act=True),
+    "dense_bf16": lambda: ops.layer_dense(Z16, prm, 0, constant=layer.constant.detach(), res_x=x16, act=True),
+    "dbwd_f32": lambda: ops.layer_dense_backward(dY32, Z32, Y32, prm, 0, res_x=x32, act=True),
+    "dbwd_bf16": lambda: ops.layer_dense_backward(dY16, Z16, Y16, prm, 0, res_x=x16, act=True),
+}
+res = {k: [] for k in bw}
+for _ in range(3):
+    for k, fn in bw.items():
+        res[k].append(timeit(fn, reps=10))
+for k, v in res.items():
+    print(f"{k:10s} " + " ".join(f"{t:.4f}" for t in v) + f"   min {min(v):.4f}")

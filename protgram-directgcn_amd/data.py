@@ -19,6 +19,8 @@ class Data:
         for k, v in list(vars(self).items()):
             if torch.is_tensor(v):
                 setattr(self, k, v.to(device, non_blocking=non_blocking))
+            elif hasattr(v, "to") and hasattr(v, "tensors"):  # a prebuilt CSRGraph (data.graph)
+                setattr(self, k, v.to(device))
         return self
 
     @property

@@ -29,8 +29,11 @@ from typing import Optional
 import numpy as np
 import torch
 
-_CACHE: "dict[tuple, CSRGraph]" = {}
-_CACHE_MAX = 8
+# (key -> (source tensors, CSRGraph)). Holding the source tensors keeps their storage alive, so a key
+# (data_ptr, version, shape, ...) can never match a different tensor that reused freed memory. Sized for
+# Cluster-GCN training (one entry per subgraph: the reference's default is up to 500 clusters).
+_CACHE: "dict[tuple, tuple]" = {}
+_CACHE_MAX = 1024
 
 
 @dataclass
@@ -65,6 +68,28 @@ class CSRGraph:
     def device(self):
         t = self.rowptr if self.shared else self.adj[0].rowptr
         return t.device
+
+    def to(self, device) -> "CSRGraph":
+        """A copy with every tensor on `device` (self if already there)."""
+        device = torch.device(device)
+        if self.device == device:
+            return self
+        mv = lambda t: None if t is None else t.to(device)  # noqa: E731
+        g = CSRGraph(n_rows=self.n_rows, shared=self.shared, rowptr=mv(self.rowptr), edges3=mv(self.edges3),
+                     symmetric=self.symmetric, raw=mv(self.raw), node_norm=mv(self.node_norm), eps=self.eps,
+                     nnz=self.nnz, row_order=mv(self.row_order), tiles=None, n_cols=self.n_cols)
+        if self.symmetric and self.rowptr_t is self.rowptr:
+            g.rowptr_t, g.edges3_t = g.rowptr, g.edges3
+        else:
+            g.rowptr_t, g.edges3_t = mv(self.rowptr_t), mv(self.edges3_t)
+        g.adj = [ShapedAdjacency(mv(a.rowptr), mv(a.edges), mv(a.rowptr_t), mv(a.edges_t), a.nnz) for a in self.adj]
+        return g
+
+    def tensors(self):
+        ts = [self.rowptr, self.edges3, self.rowptr_t, self.edges3_t, self.row_order]
+        for a in self.adj:
+            ts += [a.rowptr, a.edges, a.rowptr_t, a.edges_t]
+        return [t for t in ts if t is not None]
 
     def nnz_total(self) -> int:
         return 3 * self.nnz if self.shared else sum(a.nnz for a in self.adj)
@@ -131,8 +156,11 @@ def _key(*ts, n):
 def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, cache: bool = True) -> CSRGraph:
     """Convert the reference's three COO adjacencies to the device CSR (cached by tensor identity)."""
     key = _key(ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, n=num_rows)
-    if cache and key in _CACHE:
-        return _CACHE[key]
+    if cache:
+        hit = _CACHE.get(key)
+        if hit is not None:
+            _CACHE[key] = _CACHE.pop(key)  # LRU
+            return hit[1]
     n = int(num_rows)
     for name, ei in (("edge_index_in", ei_in), ("edge_index_out", ei_out), ("edge_index_undirected", ei_und)):
         _validate(ei, n, name)
@@ -172,7 +200,7 @@ def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, ca
     if cache:
         if len(_CACHE) >= _CACHE_MAX:
             _CACHE.pop(next(iter(_CACHE)))
-        _CACHE[key] = g
+        _CACHE[key] = ((ei_in, ew_in, ei_out, ew_out, ei_und, ew_und), g)
     return g
 
 

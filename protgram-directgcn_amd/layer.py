@@ -212,6 +212,10 @@ class ProtGramDirectGCN(nn.Module):
         """CSRGraph for a Data object: a prebuilt ``data.graph`` (build_propagation_csr) or the COO inputs."""
         g = getattr(data, "graph", None)
         if g is not None:
+            x = getattr(data, "x", None)
+            if x is not None and g.device != x.device:
+                g = g.to(x.device)  # e.g. a PyG Data moved with .to(), which leaves non-tensor attributes
+                data.graph = g
             return g
         x = data.x
         return csr_from_coo(x.size(0), data.edge_index_in, getattr(data, "edge_weight_in", None),

@@ -42,6 +42,13 @@ def _ev_end(x, e0):
         SPMM_EVENTS.append((e0, e1))
 
 
+def _require_graph_on(g, x):
+    for t in g.tensors():
+        if t.device != x.device:
+            raise RuntimeError(f"graph tensors on {t.device} but features on {x.device}: move the graph "
+                               "(CSRGraph.to) -- the kernels read both")
+
+
 def _require_gpu(*ts):
     for t in ts:
         if t is None:
@@ -85,6 +92,7 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
         return _spmm3_bf16(lib, g, x, out, fused, flags)
     x = _f32c(x)
     _require_gpu(x)
+    _require_graph_on(g, x)
     N, F = g.n_rows, x.size(1)
     if x.size(0) < N:
         raise ValueError("x has fewer rows than the graph")
@@ -123,6 +131,7 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
 def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
     x = _bf16c(x)
     _require_gpu(x)
+    _require_graph_on(g, x)
     N, F = g.n_rows, x.size(1)
     if x.size(0) < N:
         raise ValueError("x has fewer rows than the graph")
@@ -150,6 +159,7 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     if _is_bf16(G):
         G = _bf16c(G)
         _require_gpu(G)
+        _require_graph_on(g, G)
         N, F = (g.n_cols if g.n_cols is not None else g.n_rows), G.size(1) // 3
         if g.shared:
             dX = torch.empty(N, F, device=G.device, dtype=torch.bfloat16)
@@ -163,6 +173,7 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
         return spmm3_t(g, G.float(), flags).to(torch.bfloat16)
     G = _f32c(G)
     _require_gpu(G)
+    _require_graph_on(g, G)
     N, F = (g.n_cols if g.n_cols is not None else g.n_rows), G.size(1) // 3
     dX = torch.empty(N, F, device=G.device, dtype=torch.float32)
     fl = default_flags() if flags is None else flags
@@ -182,6 +193,8 @@ def spmm1(a: ShapedAdjacency, x: torch.Tensor, transpose: bool = False, flags: O
     lib = load_library()
     x = _f32c(x)
     _require_gpu(x)
+    if a.rowptr.device != x.device:
+        raise RuntimeError(f"adjacency on {a.rowptr.device} but features on {x.device}")
     N = a.rowptr.numel() - 1
     Y = torch.empty(N, x.size(1), device=x.device, dtype=torch.float32)
     rp, e = (a.rowptr_t, a.edges_t) if transpose else (a.rowptr, a.edges)

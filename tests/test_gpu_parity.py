@@ -547,7 +547,7 @@ def _bf16_graphs(pkg, cuda):
     fx = load("f5_fasta3")
     ei, ew = graph(fx)
     dei, dew = dev_graph(ei, ew, cuda)
-    g1 = pkg.graph.csr_from_coo(int(fx["N"]), dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"],
+    g1 = pkg.graph.csr_from_coo(int(fx["N"].item()), dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"],
                                 cache=False)
     N, s, d, c = pkg.synth.de_bruijn_edges(3)
     g2 = pkg.build_propagation_csr(N, s, d, c, device=cuda)
@@ -745,3 +745,47 @@ def test_model_bf16_training_step_close_to_fp32(pkg, cuda):
         g16 = grads[1][k]
         cos = float((g32 * g16).sum() / (g32.norm() * g16.norm() + 1e-30))
         assert cos > 0.99, (k, cos)
+
+
+def test_clustered_subgraphs_on_gpu(pkg, cuda):
+    """Cluster-GCN path: the model on each built subgraph (prebuilt CSR in data.graph) equals the model on the
+    same subgraph's COO fields, and the oracle with original_indices; one clustered_forward over the
+    block-diagonal union equals the per-cluster forwards bit for bit."""
+    from protgram_directgcn_amd import cluster
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    mats = og.build_matrices(N, s, d, c)
+    ei = {k: v[0].to(cuda) for k, v in mats.items()}
+    ew = {k: v[1].to(cuda) for k, v in mats.items()}
+    order = pkg.graph.locality_schedule(N, torch.from_numpy(s).to(cuda), torch.from_numpy(d).to(cuda)).long()
+    parts = cluster.range_clusters(N, cluster.cluster_count(N), order=order)
+    x = torch.randn(N, 32, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    subs = cluster.build_subgraphs(N, parts, ei["in"], ew["in"], ei["out"], ew["out"], ei["und"], ew["und"], x)
+    assert len(subs) == 16
+    torch.manual_seed(0)
+    m = pkg.ProtGramDirectGCN([32, 32, 16], N, 7, 3, 0, 512, 0.5, True).to(cuda).eval()
+    with torch.no_grad():
+        for p_ in m.parameters():
+            if p_.dim() == 2 and p_.size(1) == 1:
+                p_.uniform_(0.5, 1.5)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    outs = []
+    with torch.no_grad():
+        for dd in subs[:5] + subs[-2:]:
+            lp, emb = m(dd)
+            coo = pkg.Data(x=dd.x, edge_index_in=dd.edge_index_in, edge_weight_in=dd.edge_weight_in,
+                           edge_index_out=dd.edge_index_out, edge_weight_out=dd.edge_weight_out,
+                           edge_index_undirected_norm=dd.edge_index_undirected_norm,
+                           edge_weight_undirected_norm=dd.edge_weight_undirected_norm,
+                           original_indices=dd.original_indices)
+            lp2, emb2 = m(coo)
+            assert torch.equal(lp, lp2) and torch.equal(emb, emb2)
+            lpr, embr = oc.model_forward(sd, [32, 32, 16], dd.x.cpu(), dd.edge_index_in.cpu(), dd.edge_weight_in.cpu(),
+                                         dd.edge_index_out.cpu(), dd.edge_weight_out.cpu(),
+                                         dd.edge_index_undirected_norm.cpu(), dd.edge_weight_undirected_norm.cpu(),
+                                         original_indices=dd.original_indices.cpu(), n_gram_len=3)
+            assert_close(lp, lpr, "cluster log_probs")
+            assert_close(emb, embr, "cluster emb")
+        lp_all, emb_all = cluster.clustered_forward(m, subs)
+        for dd in subs:
+            lp, emb = m(dd)
+            assert torch.equal(lp_all[dd.original_indices], lp) and torch.equal(emb_all[dd.original_indices], emb)

@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-layers", type=int, default=1)
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
+    ap.add_argument("--chunks", type=int, default=4, help="N>1: layer-boundary all-gather in this many pieces, "
+                    "overlapped with the compute (1 = one exchange after the layer)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     return ap.parse_args()
@@ -109,13 +111,12 @@ def main():
     data = pkg.Data(x=x, graph=g)
 
     part = shard.partition(g, rank, world) if world > 1 else None
-    gbufs = [torch.empty(part.per * world, Fd, device=dev) for _ in range(L - 1)] if part else None
 
     def step():
         with torch.no_grad():
             if part is None:
                 return model(data)
-            return shard.sharded_forward(model, part, x, gather_buf=gbufs)
+            return shard.sharded_forward(model, part, x, chunks=args.chunks)
 
     for _ in range(args.warmup):
         step()
@@ -186,7 +187,8 @@ def main():
                        "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
                        "layers": L, "layer_dims": dims, "classes": C,
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
-                       "parallelism": f"node_range_x{world}" if world > 1 else "single"},
+                       "parallelism": f"node_range_x{world}" if world > 1 else "single",
+                       "exchange_chunks": args.chunks if world > 1 else None},
             "nodes_per_sec": round(N * L * args.steps / elapsed, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,

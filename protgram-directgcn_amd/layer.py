@@ -106,12 +106,14 @@ class DirectGCNLayer(nn.Module):
         """out[ei[1]] += w * x[ei[0]] with out rows = x.size(0) (PyG aggr='add')."""
         ops._require_gpu(x, edge_index)
         k = ("p1",) + _key(edge_index, edge_weight, n=x.size(0))
-        a = _P1_CACHE.get(k)
-        if a is None:
+        hit = _P1_CACHE.get(k)
+        if hit is None:
             a = _single(edge_index, edge_weight, x.size(0))
             if len(_P1_CACHE) > 16:
                 _P1_CACHE.clear()
-            _P1_CACHE[k] = a
+            _P1_CACHE[k] = ((edge_index, edge_weight), a)  # holds its keys (no stale address reuse)
+        else:
+            a = hit[1]
         return ops.Propagate1.apply(x, a)
 
     # --- forward ----------------------------------------------------------------------------------

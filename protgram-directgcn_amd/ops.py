@@ -223,12 +223,15 @@ def _version_key(ts):
 
 def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
     """pg_directgcn_pack_f32: [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] + bias sums, cached while the
-    parameters are unchanged (keyed on storage pointer + in-place version counter)."""
+    parameters are unchanged: keyed on storage pointer + in-place version counter (optimizer steps,
+    load_state_dict and in-place ops under no_grad all bump it; writes through ``p.data`` do not -- call
+    clear_caches() after those). Entries hold their source tensors, so a key can never match a new tensor
+    that reused a freed address."""
     srcs = [prm[k] for k in _PACK_KEYS] + [W_res, b_res]
     key = _version_key(srcs)
     hit = _PACK_CACHE.get(key)
     if hit is not None:
-        return hit
+        return hit[1]
     lib = load_library()
     F_out, F_in = prm["W_main_in"].shape
     n = lib.pg_directgcn_packed_floats(F_in, F_out, 1 if W_res is not None else 0)
@@ -241,7 +244,7 @@ def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
     check(lib.pg_directgcn_pack_f32(ctypes.byref(a), _p(out), _stream(out)), "pg_directgcn_pack_f32")
     if len(_PACK_CACHE) >= 32:
         _PACK_CACHE.pop(next(iter(_PACK_CACHE)))
-    _PACK_CACHE[key] = out
+    _PACK_CACHE[key] = (srcs, out)
     return out
 
 
@@ -251,10 +254,11 @@ _PACK16_CACHE: dict = {}
 def pack_weights_bf16(prm: dict, W_res=None, b_res=None):
     """(fp32 packed operand, its bf16 copy [F_out*K]) for pg_directgcn_dense_bf16; cached like pack_weights."""
     packed = pack_weights(prm, W_res, b_res)
-    key = (packed.data_ptr(), _version_key([prm[k] for k in _PACK_KEYS] + [W_res, b_res]))
+    srcs = [prm[k] for k in _PACK_KEYS] + [W_res, b_res]
+    key = (packed.data_ptr(), _version_key(srcs))
     hit = _PACK16_CACHE.get(key)
     if hit is not None:
-        return packed, hit
+        return packed, hit[1]
     lib = load_library()
     F_out, F_in = prm["W_main_in"].shape
     n = F_out * (4 if W_res is not None else 3) * F_in
@@ -262,8 +266,16 @@ def pack_weights_bf16(prm: dict, W_res=None, b_res=None):
     check(lib.pg_f32_to_bf16(n, _p(packed), _p(out), _stream(packed)), "pg_f32_to_bf16")
     if len(_PACK16_CACHE) >= 32:
         _PACK16_CACHE.pop(next(iter(_PACK16_CACHE)))
-    _PACK16_CACHE[key] = out
+    _PACK16_CACHE[key] = (srcs + [packed], out)
     return packed, out
+
+
+def clear_caches():
+    """Drop the packed-weight and COO->CSR caches (e.g. after writing parameters through ``p.data``)."""
+    from .graph import clear_cache
+    _PACK_CACHE.clear()
+    _PACK16_CACHE.clear()
+    clear_cache()
 
 
 _PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in", "b_dir_shared_in",
@@ -309,21 +321,30 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
-                act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None) -> torch.Tensor:
+                act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header). bf16 Z ->
     pg_directgcn_dense_bf16 (bf16 output)."""
     lib = load_library()
     _require_gpu(Z)
     if _is_bf16(Z):
         Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags)
-        if Y is not None:
-            return Y
-        return layer_dense(Z.float(), prm, gate_mode, rows, constant, None if res_x is None else res_x.float(),
-                           W_res, b_res, act, slope, flags).to(torch.bfloat16)
+        if Y is None:
+            Y = layer_dense(Z.float(), prm, gate_mode, rows, constant, None if res_x is None else res_x.float(),
+                            W_res, b_res, act, slope, flags).to(torch.bfloat16)
+        if out is not None:
+            out.copy_(Y)
+            return out
+        return Y
     packed = pack_weights(prm, W_res, b_res)
     M = Z.size(0)
     F_out = prm["W_main_in"].size(0)
-    Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
+    if out is not None:
+        if out.shape != (M, F_out) or out.dtype != torch.float32 or out.stride(1) != 1 or out.device != Z.device:
+            raise ValueError("out must be a row-major fp32 [M, F_out] tensor on Z's device")
+        Y = out
+    else:
+        Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
     a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags

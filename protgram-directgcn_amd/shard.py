@@ -23,7 +23,8 @@ Training (``sharded_train_step``, the trainer's step protgram_directgcn_trainer.
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -44,6 +45,7 @@ class NodeRangePartition:
     r1: int
     local: CSRGraph
     rows: torch.Tensor  # int64 [r1-r0] global row ids (gate / constant gather)
+    cache: dict = field(default_factory=dict)
 
     @property
     def n_local(self) -> int:
@@ -91,33 +93,121 @@ def _column_block(g: CSRGraph, c0: int, c1: int):
     return rowptr_t, et
 
 
-def _layer_local(conv, part: NodeRangePartition, h_full, res: nn.Module, act=True):
-    Z = ops.spmm3(part.local, h_full)
+def _rows_slice(g: CSRGraph, a: int, b: int, order: Optional[torch.Tensor]) -> CSRGraph:
+    """Rows [a, b) of a row-block CSR (zero-copy), keeping the schedule's order among them."""
+    rp = g.rowptr
+    e0, e1 = int(rp[a]), int(rp[b])
+    o = None
+    if order is not None:
+        ol = order.to(torch.int64)
+        o = (ol[(ol >= a) & (ol < b)] - a).to(torch.int32)
+    return CSRGraph(n_rows=b - a, shared=True, rowptr=(rp[a:b + 1] - e0).contiguous(), edges3=g.edges3[e0:e1],
+                    symmetric=False, nnz=e1 - e0, row_order=o, n_cols=g.n_cols)
+
+
+@dataclass
+class GatherPlan:
+    """Layer-boundary exchange in `chunks` pieces (overlap the all-gather with compute).
+
+    The boundary layer is computed in `chunks` row chunks of `cs` rows; as soon as chunk k is done its
+    rows are all-gathered (asynchronously: RCCL's own stream) while chunk k+1 computes. The gathered
+    buffer is chunk-major -- [chunk k][rank p][cs rows] -- so the next layers read it through `remap`, a
+    once-built copy of the local CSR whose column ids point into that buffer. Entry order inside rows is
+    unchanged: results are bit-identical to the unchunked exchange."""
+    chunks: int
+    cs: int
+    first: List[CSRGraph]    # layer-1 row chunks (global column ids, reads the replicated input)
+    remap: CSRGraph          # local CSR with buffer column ids (layers >= 2)
+    remap_chunks: List[CSRGraph]
+
+
+def gather_plan(part: NodeRangePartition, chunks: int) -> GatherPlan:
+    key = ("plan", chunks)
+    cached = part.cache.get(key)
+    if cached is not None:
+        return cached
+    chunks = max(1, min(int(chunks), part.per))
+    cs = -(-part.per // chunks)
+    W = part.world
+    col = part.local.edges3[:, 0].to(torch.int64)
+    p = col // part.per
+    off = col - p * part.per
+    k = off // cs
+    pos = (k * W + p) * cs + (off - k * cs)
+    e = part.local.edges3.clone()
+    e[:, 0] = pos.to(torch.int32)
+    remap = CSRGraph(n_rows=part.n_local, shared=True, rowptr=part.local.rowptr, edges3=e, symmetric=False,
+                     nnz=part.local.nnz, row_order=part.local.row_order, n_cols=chunks * W * cs)
+    bounds = [(min(c * cs, part.n_local), min((c + 1) * cs, part.n_local)) for c in range(chunks)]
+    first = [_rows_slice(part.local, a, b, part.local.row_order) for a, b in bounds]
+    remap_chunks = [_rows_slice(remap, a, b, part.local.row_order) for a, b in bounds]
+    plan = GatherPlan(chunks, cs, first, remap, remap_chunks)
+    part.cache[key] = plan
+    return plan
+
+
+def _dense_local(conv, part: NodeRangePartition, Z, res: nn.Module, res_x, a: int, b: int, out=None, act=True):
     prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
-    rows = part.rows if conv.use_vector_coeffs else None
-    constant = conv.constant.detach() if conv.use_vector_coeffs else None
-    res_x = h_full[part.r0:part.r1]
-    if isinstance(res, nn.Linear):
-        return ops.layer_dense(Z, prm, 0 if conv.use_vector_coeffs else 1, rows=rows, constant=constant, res_x=res_x,
-                               W_res=res.weight.detach(), b_res=res.bias.detach(), act=act)
-    return ops.layer_dense(Z, prm, 0 if conv.use_vector_coeffs else 1, rows=rows, constant=constant, res_x=res_x,
-                           act=act)
+    vec = conv.use_vector_coeffs
+    rows = part.rows[a:b] if vec else None
+    constant = conv.constant.detach() if vec else None
+    W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
+    return ops.layer_dense(Z, prm, 0 if vec else 1, rows=rows, constant=constant, res_x=res_x, W_res=W_res,
+                           b_res=b_res, act=act, out=out)
+
+
+def _all_gather_chunk(send: torch.Tensor, dst: torch.Tensor, part: NodeRangePartition, group=None):
+    """send [cs, F] from every rank -> dst [world * cs, F] (rank-major). Async on RCCL (returns the work)."""
+    if dist.get_backend(group) == "gloo":  # rehearsal backend: synchronous list form
+        dist.all_gather(list(dst.view(part.world, send.size(0), -1).unbind(0)), send, group=group)
+        return None
+    return dist.all_gather_into_tensor(dst, send, group=group, async_op=True)
 
 
 @torch.no_grad()
-def sharded_forward(model, part: NodeRangePartition, x_full: torch.Tensor, group=None, gather_buf=None):
-    """ProtGramDirectGCN.forward restricted to this rank's rows; returns (log_probs, emb) for rows [r0, r1)."""
-    h_full = model._apply_pe(x_full)
+def sharded_forward(model, part: NodeRangePartition, x_full: torch.Tensor, group=None, gather_buf=None,
+                    chunks: int = 1):
+    """ProtGramDirectGCN.forward restricted to this rank's rows; returns (log_probs, emb) for rows [r0, r1).
+
+    Layer 1 reads the replicated input; each later layer reads the previous layer's rows of all ranks,
+    exchanged by all-gather in `chunks` pieces overlapped with the compute (GatherPlan). `gather_buf` is
+    accepted for compatibility and unused (buffers come from the caching allocator)."""
+    h = model._apply_pe(x_full)
+    if model.compute_dtype == torch.bfloat16:
+        h = h.to(torch.bfloat16)
     L = len(model.convs)
+    plan = gather_plan(part, chunks) if (L > 1 and part.world > 1) else None
     h_local = None
     for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
-        h_local = _layer_local(conv, part, h_full, res)
-        if i + 1 < L:
-            if part.world > 1:
-                buf = gather_buf[i] if gather_buf is not None else None
-                h_full = all_gather_rows(h_local, part, group, buf)
-            else:
-                h_full = h_local
+        first = i == 0
+        X = h
+        res_all = h[part.r0:part.r1] if first else h_local
+        F_out = conv.out_channels
+        if plan is not None and i + 1 < L:  # this layer's output is exchanged: compute it in chunks
+            W, cs = part.world, plan.cs
+            send = X.new_empty(plan.chunks * cs, F_out)
+            buf = X.new_empty(plan.chunks * W * cs, F_out)
+            works = []
+            for c in range(plan.chunks):
+                a, b = min(c * cs, part.n_local), min((c + 1) * cs, part.n_local)
+                if b > a:
+                    gk = plan.first[c] if first else plan.remap_chunks[c]
+                    Z = ops.spmm3(gk, X)
+                    _dense_local(conv, part, Z, res, res_all[a:b], a, b, out=send[a:b])
+                works.append(_all_gather_chunk(send[c * cs:(c + 1) * cs], buf[c * W * cs:(c + 1) * W * cs], part,
+                                               group))
+            for w in works:
+                if w is not None:
+                    w.wait()
+            h_local = send[:part.n_local]
+            h = buf
+        else:
+            g = part.local if (first or plan is None) else plan.remap
+            if not first and plan is None and part.world == 1:
+                g = part.local
+            Z = ops.spmm3(g, X)
+            h_local = _dense_local(conv, part, Z, res, res_all, 0, part.n_local)
+            h = h_local
     return model.head(h_local)
 
 

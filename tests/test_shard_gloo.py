@@ -50,7 +50,16 @@ def _cpu_spmm3_t(g, G, flags=None):
 
 
 def _cpu_layer_dense(Z, prm, gate_mode, rows=None, constant=None, res_x=None, W_res=None, b_res=None, act=False,
-                     slope=0.01, flags=None):
+                     slope=0.01, flags=None, out=None):
+    y = _cpu_layer_dense_impl(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def _cpu_layer_dense_impl(Z, prm, gate_mode, rows=None, constant=None, res_x=None, W_res=None, b_res=None, act=False,
+                          slope=0.01):
     M, F = Z.size(0), Z.size(1) // 3
 
     def gate(name):
@@ -94,12 +103,19 @@ def _worker(rank, world, port, out_q):
                     p.uniform_(0.5, 1.5)
         x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
         part = shard.partition(g, rank, world)
-        lp, emb = shard.sharded_forward(model, part, x)
         p = {k: v.detach() for k, v in model.state_dict().items()}
         lp_r, emb_r = oc.model_forward(p, [16, 16, 12, 12], x, *m["in"], *m["out"], *m["und"], n_gram_len=2)
-        ok = (torch.allclose(lp, lp_r[part.r0:part.r1], rtol=1e-5, atol=1e-5)
-              and torch.allclose(emb, emb_r[part.r0:part.r1], rtol=1e-5, atol=1e-5))
-        out_q.put((rank, part.r0, part.r1, bool(ok), float((lp - lp_r[part.r0:part.r1]).abs().max())))
+        ok, err, first = True, 0.0, None
+        for chunks in (1, 3):  # unchunked and chunked (overlapped) layer-boundary exchange
+            lp, emb = shard.sharded_forward(model, part, x, chunks=chunks)
+            ok = ok and (torch.allclose(lp, lp_r[part.r0:part.r1], rtol=1e-5, atol=1e-5)
+                         and torch.allclose(emb, emb_r[part.r0:part.r1], rtol=1e-5, atol=1e-5))
+            if first is None:
+                first = lp
+            else:
+                ok = ok and torch.equal(first, lp)  # chunking changes the schedule, never the values
+            err = max(err, float((lp - lp_r[part.r0:part.r1]).abs().max()))
+        out_q.put((rank, part.r0, part.r1, bool(ok), err))
     finally:
         dist.destroy_process_group()
 

@@ -267,6 +267,14 @@ int pg_directgcn_head_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uin
                            const float* W1, const float* b1, const float* W2, const float* b2, float eps,
                            float* logp, int64_t ldp, float* emb, int64_t lde, void* stream);
 
+/* n-gram transition producer (data_builder.py:38-54 windows as integer keys). For sequence s, positions
+ * p in [offsets[s], offsets[s+1]) of `bytes`: keys[p] = sum_j lut[bytes[p+j]] * K^(n-1-j) for the window
+ * [p, p+n) if it lies inside the sequence, else -1; next_keys[p] = key of window p+1 if the transition
+ * p -> p+1 (window [p+1, p+n+1)) lies inside the sequence, else -1. `lut` [256] maps a byte to its
+ * order-preserving code in [0, K). K^n must fit 63 bits (PG_ERR_ARG otherwise). */
+int pg_ngram_keys(int64_t nseq, const int64_t* offsets, const uint8_t* bytes, const int32_t* lut, int n,
+                  int64_t K, int64_t* keys, int64_t* next_keys, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

@@ -78,6 +78,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
 #define PG_FLAG_DENSE_4WAVES (1u << 9)  /* dense kernel: 4 waves per 128-row tile (64x64 per wave) instead of 8 */
+#define PG_FLAG_SPMM_BLOCK512 (1u << 10)  /* SpMM variant C: 512-thread blocks (more consecutive rows per CU) */
+#define PG_FLAG_SPMM_BLOCK1024 (1u << 11) /* SpMM variant C: 1024-thread blocks */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

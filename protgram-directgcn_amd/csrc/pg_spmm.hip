@@ -245,10 +245,10 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
 // group's own LDS window, and read them back as LDS broadcasts: the TD only carries the feature gathers.
 // A window is private to one row group inside one wave, so wave-local ordering (the compiler's
 // lgkmcnt waits + a wave barrier) replaces block barriers. Same accumulation order: still bit-exact.
-template <int LPR, int NV, int U, int MODE>
-__global__ __launch_bounds__(256) void spmm_win_kernel(SpmmParams p) {
+template <int LPR, int NV, int U, int MODE, int NT = 256>
+__global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
     using R = typename Rec<MODE>::T;
-    constexpr int RPB = 256 / LPR;
+    constexpr int RPB = NT / LPR;
     constexpr int NACC = Shape<MODE>::NACC;
     constexpr int NSLICE = Shape<MODE>::NSLICE;
     constexpr int WIN = LPR;  // records per window (one per lane)
@@ -475,12 +475,21 @@ void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
     // PG_FLAG_BCAST_RECORDS / PG_FLAG_EDGE_LDS select variants A / B (measurement only).
     const bool win = !(flags & (PG_FLAG_EDGE_LDS | PG_FLAG_BCAST_RECORDS));
     if (win && LPR >= 8) {
-        constexpr int RPB = 256 / LPR;
-        const int64_t nb = (p.n_rows + RPB - 1) / RPB;
-        if (flags & PG_FLAG_UNROLL4)
-            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 8, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE>), dim3((unsigned)nb), dim3(256), 0, s, p);
+        // block size: 256 threads (default), 512 / 1024 with PG_FLAG_SPMM_BLOCK512 / _BLOCK1024 -- more
+        // schedule-consecutive rows (which share neighbour rows) on one CU, i.e. in one L1
+        const int nt = (flags & PG_FLAG_SPMM_BLOCK1024) ? 1024 : (flags & PG_FLAG_SPMM_BLOCK512) ? 512 : 256;
+        const int64_t rpb = nt / LPR;
+        const int64_t nb = (p.n_rows + rpb - 1) / rpb;
+        const bool u8 = flags & PG_FLAG_UNROLL4;
+#define PG_WIN(NTv)                                                                                            \
+    do {                                                                                                       \
+        if (u8) hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 8, MODE, NTv>), dim3((unsigned)nb), dim3(NTv), 0, s, p); \
+        else hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE, NTv>), dim3((unsigned)nb), dim3(NTv), 0, s, p);    \
+    } while (0)
+        if (nt == 1024) PG_WIN(1024);
+        else if (nt == 512) PG_WIN(512);
+        else PG_WIN(256);
+#undef PG_WIN
         return;
     }
     const bool lds = (flags & PG_FLAG_EDGE_LDS) && p.row_order == nullptr;  // staging needs contiguous rows

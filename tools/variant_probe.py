@@ -39,6 +39,10 @@ def timeit(fn, reps=20):
 
 variants = {
     "f32_u4": lambda: ops.spmm3(g, x32, flags=0),
+    "f32_b512": lambda: ops.spmm3(g, x32, flags=1024),
+    "f32_b1024": lambda: ops.spmm3(g, x32, flags=2048),
+    "f32_b1024_u8": lambda: ops.spmm3(g, x32, flags=2048 | 4),
+    "f32t_b1024": lambda: ops.spmm3_t(g, G32, flags=2048),
     "bf16_u4": lambda: ops.spmm3(g, x16, flags=0),
     "bf16_u8": lambda: ops.spmm3(g, x16, flags=4),
     "f32t_u4": lambda: ops.spmm3_t(g, G32, flags=0),

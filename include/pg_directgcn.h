@@ -277,6 +277,27 @@ int pg_directgcn_head_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uin
 int pg_ngram_keys(int64_t nseq, const int64_t* offsets, const uint8_t* bytes, const int32_t* lut, int n,
                   int64_t K, int64_t* keys, int64_t* next_keys, void* stream);
 
+/* ---- training-step helpers (the trainer's L2 term over all parameters, trainer :96 / :136) ---------
+ * A tensor list is a device array of descriptors; tensor t is split into pg_multi_chunks(numel_t) chunks of
+ * 64K elements and chunk_ptr[t] = the first chunk of tensor t (exclusive prefix sum, chunk_ptr[ntens] =
+ * nchunks). */
+typedef struct pg_tensor_desc {
+    const float* x;  /* read */
+    float* y;        /* written by pg_multi_axpy_f32 (unused by pg_multi_sqsum_f32) */
+    int64_t numel;
+} pg_tensor_desc_t;
+
+int64_t pg_multi_chunks(int64_t numel);
+
+/* out[0] = sum_t sum_i x_t[i]^2, fixed-order reduction (deterministic). partial: nchunks floats. */
+int pg_multi_sqsum_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks,
+                       float* partial, float* out, void* stream);
+
+/* y_t[i] += a * x_t[i] for every tensor of the list (one launch), a = alpha * (alpha_scale ? *alpha_scale : 1):
+ * alpha_scale is a device scalar (e.g. GradScaler's scale, read without a host sync). */
+int pg_multi_axpy_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks,
+                      float alpha, const float* alpha_scale, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

@@ -5,7 +5,7 @@ constructor and ``forward()`` signatures, ``state_dict`` keys and init. Propagat
 contraction run in hand-written gfx950 HIP kernels behind a C-ABI library (``csrc/``, loaded with
 ctypes); there is no CPU fallback -- without the library the layer raises.
 """
-from . import cluster, ngram, synth  # noqa: F401
+from . import cluster, ngram, synth, train  # noqa: F401
 from ._lib import load_library, library_path, NativeLibraryError  # noqa: F401
 from .data import Data  # noqa: F401
 from .graph import CSRGraph, ShapedAdjacency, build_propagation_csr, csr_from_coo  # noqa: F401

@@ -94,6 +94,9 @@ SIGNATURES = {
     "pg_directgcn_head_bf16": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                               c_vp, c_i64, c_vp, c_i64, c_vp]),
     "pg_ngram_keys": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, ctypes.c_int, c_i64, c_vp, c_vp, c_vp]),
+    "pg_multi_chunks": (c_i64, [c_i64]),
+    "pg_multi_sqsum_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "pg_multi_axpy_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp]),
     "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "pg_gemm_at_b_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,

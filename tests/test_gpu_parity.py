@@ -789,3 +789,57 @@ def test_clustered_subgraphs_on_gpu(pkg, cuda):
         for dd in subs:
             lp, emb = m(dd)
             assert torch.equal(lp_all[dd.original_indices], lp) and torch.equal(emb_all[dd.original_indices], emb)
+
+
+@pytest.mark.parametrize("amp", [False, True])
+def test_train_step_matches_reference_loop(pkg, cuda, amp):
+    """train.train_step (fused L2 value/gradient, gather nll, no host sync) against the reference trainer's
+    loop (protgram_directgcn_trainer.py:91-100: nll_loss + l2_lambda * sum p.norm(2).pow(2), backward, step),
+    3 steps, with and without autocast + GradScaler. SGD: parameter updates are linear in the gradients."""
+    import torch.nn.functional as F
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    lam = 1e-3
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        opt = torch.optim.SGD(m.parameters(), lr=0.05)
+        scaler = torch.amp.GradScaler("cuda", enabled=amp)
+        losses = []
+        for _ in range(3):
+            if fused:
+                losses.append(float(train.train_step(m, data, y, opt, l2_lambda=lam, scaler=scaler)))
+            else:
+                opt.zero_grad()
+                with torch.amp.autocast("cuda", enabled=amp):
+                    out, _ = m(data=data)
+                    loss = F.nll_loss(out, y) + lam * sum(p.norm(2).pow(2) for p in m.parameters() if p.requires_grad)
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
+                losses.append(float(loss))
+        runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-6)
+    for k, v in runs[0][1].items():
+        assert_grad_close(runs[1][1][k], v.cpu(), f"param {k}")
+
+
+def test_multi_tensor_helpers(pkg, cuda):
+    from protgram_directgcn_amd import train
+    g = torch.Generator().manual_seed(0)
+    ts = [torch.randn(n, generator=g).to(cuda) for n in (1, 7, 65536, 65537, 300000)]
+    ref = sum(float((t.double() ** 2).sum()) for t in ts)
+    got = float(train.l2_sqsum(ts))
+    assert abs(got - ref) <= 1e-5 * ref
+    assert float(train.l2_sqsum(ts)) == got  # deterministic
+    ps = [t.clone().requires_grad_(True) for t in ts]
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    train.add_l2_grad(ps, 0.25, scale=torch.tensor(4.0, device=cuda))
+    for p, t in zip(ps, ts):
+        assert torch.allclose(p.grad, 1 + 2.0 * t)

@@ -16,6 +16,8 @@ pkg = load_package()
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 amp = "--amp" in sys.argv
 bf16 = "--bf16" in sys.argv
+fused = "--fused" in sys.argv          # train.train_step instead of the reference loop body
+adam_fused = "--adam-fused" in sys.argv
 dims = [128, 128, 128]
 for a in sys.argv:
     if a.startswith("--dims="):
@@ -31,7 +33,7 @@ y = torch.arange(N, device=dev) // (20 ** (n - 1))
 if bf16:
     model.compute_dtype = torch.bfloat16
 data = pkg.Data(x=x, graph=g)
-opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
+opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0, fused=True if adam_fused else None)
 model.train()
 
 
@@ -39,6 +41,8 @@ scaler = torch.amp.GradScaler("cuda", enabled=amp)
 
 
 def step():
+    if fused:
+        return pkg.train.train_step(model, data, y, opt, l2_lambda=1e-7, scaler=scaler)
     opt.zero_grad()
     with torch.amp.autocast("cuda", enabled=amp):
         out, _ = model(data=data)
@@ -56,4 +60,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step dims={dims} (amp={amp}, bf16={bf16}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

@@ -298,6 +298,22 @@ int pg_multi_sqsum_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* 
 int pg_multi_axpy_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks,
                       float alpha, const float* alpha_scale, void* stream);
 
+/* Adam over a parameter list in one launch (torch.optim.Adam's update, amsgrad = maximize = False, L2-style
+ * weight_decay): p, m (exp_avg), v (exp_avg_sq) updated in place from g; bias corrections from the device
+ * step counter `step` (incremented afterwards unless *found_inf != 0). grad_scale / found_inf: GradScaler's
+ * device scale (gradients are multiplied by 1/scale) and inf flag (update skipped), or NULL. */
+typedef struct pg_adam_desc {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t numel;
+} pg_adam_desc_t;
+
+int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
+                double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
+                const float* found_inf, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

@@ -27,9 +27,19 @@ __global__ __launch_bounds__(256) void sqsum_chunks_kernel(int ntens, const pg_t
     const int64_t beg = (b - chunk_ptr[lo]) * CHUNK;
     const int64_t end = min(beg + CHUNK, t.numel);
     float s = 0.f;
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
-        const float v = t.x[i];
-        s += v * v;
+    if ((reinterpret_cast<uintptr_t>(t.x) & 15) == 0) {  // float4 body (chunks start at multiples of 64K)
+        const int64_t end4 = beg + ((end - beg) & ~int64_t(3));
+        const float4* x4 = reinterpret_cast<const float4*>(t.x);
+        for (int64_t i = beg / 4 + threadIdx.x; i < end4 / 4; i += 256) {
+            const float4 v = x4[i];
+            s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+        for (int64_t i = end4 + threadIdx.x; i < end; i += 256) s += t.x[i] * t.x[i];
+    } else {
+        for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
+            const float v = t.x[i];
+            s += v * v;
+        }
     }
     __shared__ float red[256];
     red[threadIdx.x] = s;
@@ -67,7 +77,69 @@ __global__ __launch_bounds__(256) void axpy_chunks_kernel(int ntens, const pg_te
     const pg_tensor_desc_t t = d[lo];
     const int64_t beg = (b - chunk_ptr[lo]) * CHUNK;
     const int64_t end = min(beg + CHUNK, t.numel);
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256) t.y[i] += alpha * t.x[i];
+    if (((reinterpret_cast<uintptr_t>(t.x) | reinterpret_cast<uintptr_t>(t.y)) & 15) == 0) {
+        const int64_t end4 = beg + ((end - beg) & ~int64_t(3));
+        const float4* x4 = reinterpret_cast<const float4*>(t.x);
+        float4* y4 = reinterpret_cast<float4*>(t.y);
+        for (int64_t i = beg / 4 + threadIdx.x; i < end4 / 4; i += 256) {
+            const float4 xv = x4[i];
+            float4 yv = y4[i];
+            yv.x += alpha * xv.x;
+            yv.y += alpha * xv.y;
+            yv.z += alpha * xv.z;
+            yv.w += alpha * xv.w;
+            y4[i] = yv;
+        }
+        for (int64_t i = end4 + threadIdx.x; i < end; i += 256) t.y[i] += alpha * t.x[i];
+    } else {
+        for (int64_t i = beg + threadIdx.x; i < end; i += 256) t.y[i] += alpha * t.x[i];
+    }
+}
+
+// Adam (torch.optim.Adam, foreach path, amsgrad = maximize = False) for every parameter of a list in one launch:
+//   g  = grad * inv_scale (+ weight_decay * p)
+//   m  = lerp(m, g, 1 - beta1) ; v = v * beta2 + (1 - beta2) * g * g
+//   p += (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps),   bc_k = 1 - beta_k^t  (t = step + 1, in double)
+// Skipped entirely when *found_inf != 0 (GradScaler's device-side flag; no host sync).
+__global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc_t* d, const int64_t* chunk_ptr,
+                                                   double lr, double beta1, double beta2, float eps, float weight_decay,
+                                                   const float* step, const float* grad_scale, const float* found_inf) {
+    if (found_inf && found_inf[0] != 0.f) return;
+    const int64_t b = blockIdx.x;
+    int lo = 0, hi = ntens;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (chunk_ptr[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    const pg_adam_desc_t t = d[lo];
+    const double tt = (double)step[0] + 1.0;
+    const double bc1 = 1.0 - pow(beta1, tt), bc2 = 1.0 - pow(beta2, tt);
+    const float step_size = (float)((lr / bc1) * -1.0);
+    const float bc2s = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2);
+    const float inv = grad_scale ? (float)(1.0 / (double)grad_scale[0]) : 1.f;
+    const int64_t beg = (b - chunk_ptr[lo]) * CHUNK;
+    const int64_t end = min(beg + CHUNK, t.numel);
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
+        float g = t.g[i];
+        if (grad_scale) g = g * inv;
+        float p = t.p[i];
+        if (weight_decay != 0.f) g = g + weight_decay * p;
+        float m = t.m[i];
+        m = (w1 < 0.5f) ? m + w1 * (g - m) : g - (g - m) * (1.f - w1);  // at::lerp
+        float v = t.v[i] * b2;
+        v = v + w2 * g * g;
+        const float denom = sqrtf(v) / bc2s + eps;
+        p = p + step_size * (m / denom);
+        t.p[i] = p;
+        t.m[i] = m;
+        t.v[i] = v;
+    }
+}
+
+__global__ void adam_step_kernel(float* step, const float* found_inf) {
+    if (!(found_inf && found_inf[0] != 0.f)) step[0] += 1.f;
 }
 
 }  // namespace
@@ -98,4 +170,20 @@ int pg_multi_axpy_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* c
     return pg::check_launch("pg_multi_axpy_f32");
 }
 
+int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
+                double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
+                const float* found_inf, void* stream) {
+    PG_REQUIRE(ntens >= 0 && nchunks >= 0 && step, "bad arguments");
+    PG_REQUIRE(beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && lr >= 0 && eps >= 0, "bad hyper-parameters");
+    hipStream_t s = (hipStream_t)stream;
+    if (nchunks > 0) {
+        PG_REQUIRE(descs && chunk_ptr, "null pointer");
+        hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(256), 0, s, ntens, descs, chunk_ptr, lr, beta1, beta2,
+                           (float)eps, (float)weight_decay, (const float*)step, grad_scale, found_inf);
+    }
+    hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(1), 0, s, step, found_inf);
+    return pg::check_launch("pg_adam_f32");
+}
+
 }  // extern "C"
+

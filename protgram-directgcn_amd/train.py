@@ -27,28 +27,36 @@ import torch.nn.functional as F
 from ._lib import check, load_library
 
 
-class TensorList:
-    """Device descriptors ({x, y, numel}) + chunk offsets for a fixed list of fp32 tensors."""
+def _upload(a: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device without a host sync (pinned staging, stream-ordered copy)."""
+    h = torch.from_numpy(a).pin_memory()
+    return h.to(dev, non_blocking=True)
 
-    def __init__(self, xs: List[torch.Tensor], ys: Optional[List[torch.Tensor]] = None):
+
+class TensorList:
+    """Device descriptors + chunk offsets for a list of fp32 tensor groups: field k of descriptor t is the data
+    pointer of fields[k][t]; the last int64 is numel (of fields[0][t])."""
+
+    def __init__(self, *fields: List[torch.Tensor]):
         lib = load_library()
+        xs = fields[0]
         if not xs:
             raise ValueError("empty tensor list")
         dev = xs[0].device
-        for t in xs + (ys or []):
-            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
-                raise ValueError("tensors must be contiguous fp32 on one device")
-        self.xs, self.ys = xs, ys
-        desc = np.zeros((len(xs), 3), dtype=np.int64)
+        for f in fields:
+            for t in f:
+                if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+                    raise ValueError("tensors must be contiguous fp32 on one device")
+        desc = np.zeros((len(xs), len(fields) + 1), dtype=np.int64)
         chunks = np.zeros(len(xs) + 1, dtype=np.int64)
         for i, x in enumerate(xs):
-            desc[i, 0] = x.data_ptr()
-            desc[i, 1] = ys[i].data_ptr() if ys is not None else 0
-            desc[i, 2] = x.numel()
+            for k, f in enumerate(fields):
+                desc[i, k] = f[i].data_ptr()
+            desc[i, -1] = x.numel()
             chunks[i + 1] = chunks[i] + lib.pg_multi_chunks(x.numel())
-        self.key = tuple(int(v) for v in desc[:, :2].reshape(-1))
-        self.desc = torch.from_numpy(desc).to(dev)
-        self.chunk_ptr = torch.from_numpy(chunks).to(dev)
+        self.fields = fields  # keep the tensors alive while the descriptors may be in use
+        self.desc = _upload(desc, dev)
+        self.chunk_ptr = _upload(chunks, dev)
         self.nchunks = int(chunks[-1])
         self.partial = torch.empty(max(self.nchunks, 1), dtype=torch.float32, device=dev)
 
@@ -57,12 +65,16 @@ _LISTS: dict = {}
 
 
 def _tensor_list(xs, ys=None) -> TensorList:
-    key = tuple(t.data_ptr() for t in xs) + (tuple(t.data_ptr() for t in ys) if ys is not None else ())
+    """Parameter-only lists are cached (parameters keep their storage); lists with gradients are rebuilt per
+    call -- caching them would keep every step's freed gradients alive."""
+    if ys is not None:
+        return TensorList(xs, ys)
+    key = tuple(t.data_ptr() for t in xs)
     tl = _LISTS.get(key)
     if tl is None:
         if len(_LISTS) > 64:
             _LISTS.clear()
-        tl = TensorList(xs, ys)
+        tl = TensorList(xs, xs)  # pg_tensor_desc_t = {x, y, numel}: y unused by the sum of squares
         _LISTS[key] = tl
     return tl
 
@@ -103,12 +115,66 @@ def nll_mean(logp: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return -logp.gather(1, y.view(-1, 1)).mean()
 
 
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad = maximize = False; L2-style weight_decay) as ONE HIP launch per step for all
+    parameters of a group (``pg_adam_f32``), instead of the foreach path's ~8 multi-tensor passes.
+
+    GradScaler-aware without host syncs (``_step_supports_amp_scaling``): the scaler hands over its device
+    scale and inf flag (``grad_scale`` / ``found_inf``); gradients are unscaled in-kernel and the whole update
+    (including the step count) is skipped on inf, as torch's fused optimizers do. State per parameter has
+    torch's keys (``step``, ``exp_avg``, ``exp_avg_sq``)."""
+
+    _step_supports_amp_scaling = True
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
+            raise ValueError("invalid Adam hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        grad_scale = getattr(self, "grad_scale", None)
+        found_inf = getattr(self, "found_inf", None)
+        lib = load_library()
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            for p in ps:
+                if p.grad.is_sparse or p.dtype != torch.float32:
+                    raise RuntimeError("train.Adam takes dense fp32 parameters")
+                st = self.state[p]
+                if not st:
+                    st["step"] = group.setdefault("_step", torch.zeros((), dtype=torch.float32, device=p.device))
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            step = group.setdefault("_step", self.state[ps[0]]["step"])
+            grads = [p.grad.contiguous() for p in ps]
+            tl = TensorList(ps, grads, [self.state[p]["exp_avg"] for p in ps],
+                            [self.state[p]["exp_avg_sq"] for p in ps])
+            b1, b2 = group["betas"]
+            dev = ps[0].device
+            gs = grad_scale.to(dev) if grad_scale is not None else None
+            fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
+            check(lib.pg_adam_f32(len(ps), ctypes.c_void_p(tl.desc.data_ptr()), ctypes.c_void_p(tl.chunk_ptr.data_ptr()),
+                                  tl.nchunks, float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                                  float(group["weight_decay"]), ctypes.c_void_p(step.data_ptr()),
+                                  ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
+                                  ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
+                  "pg_adam_f32")
+        return loss
+
+
 def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None, weight: float = 1.0,
                autocast: bool = True) -> torch.Tensor:
     """One step of the reference loop (trainer :91-100, or :129-140 with weight = batch nodes / total nodes).
     Returns the total loss (nll * weight + l2_lambda * sum ||p||^2) as a device scalar."""
     params = [p for p in model.parameters() if p.requires_grad]
-    optimizer.zero_grad(set_to_none=False)
+    optimizer.zero_grad(set_to_none=True)  # autograd then assigns gradients instead of adding into zeros
     use_amp = autocast and scaler is not None and scaler.is_enabled()
     with torch.amp.autocast("cuda", enabled=use_amp):
         lp, _ = model(data=data)

@@ -843,3 +843,43 @@ def test_multi_tensor_helpers(pkg, cuda):
     train.add_l2_grad(ps, 0.25, scale=torch.tensor(4.0, device=cuda))
     for p, t in zip(ps, ts):
         assert torch.allclose(p.grad, 1 + 2.0 * t)
+
+
+def test_fused_adam_matches_torch_adam(pkg, cuda):
+    """train.Adam (one pg_adam_f32 launch) against torch.optim.Adam on identical gradients: 5 steps, two
+    parameter groups, weight decay in one; then a GradScaler step with an inf gradient is skipped entirely."""
+    from protgram_directgcn_amd import train
+    g = torch.Generator().manual_seed(0)
+    shapes = [(128, 128), (128,), (160000, 1), (70001,)]
+    init = [torch.randn(s, generator=g).to(cuda) for s in shapes]
+    grads = [[torch.randn(s, generator=g).to(cuda) * (10.0 ** -k) for s in shapes] for k in range(5)]
+    ps_ref = [t.clone().requires_grad_(True) for t in init]
+    ps_ours = [t.clone().requires_grad_(True) for t in init]
+    groups = lambda ps: [{"params": ps[:2]}, {"params": ps[2:], "weight_decay": 0.01, "lr": 3e-3}]  # noqa: E731
+    o_ref = torch.optim.Adam(groups(ps_ref), lr=1e-3)
+    o_ours = train.Adam(groups(ps_ours), lr=1e-3)
+    for gs in grads:
+        for p, gg in zip(ps_ref, gs):
+            p.grad = gg.clone()
+        for p, gg in zip(ps_ours, gs):
+            p.grad = gg.clone()
+        o_ref.step()
+        o_ours.step()
+    for a, b in zip(ps_ours, ps_ref):
+        d = (a.detach() - b.detach()).abs().max().item()
+        assert d <= 1e-6 * max(1.0, b.detach().abs().max().item()), d
+    for p in ps_ours:
+        st = o_ours.state[p]
+        assert set(st) == {"step", "exp_avg", "exp_avg_sq"} and float(st["step"]) == 5.0
+    # GradScaler: an inf gradient skips the update and the step count, with no host sync in step()
+    scaler = torch.amp.GradScaler("cuda")
+    before = [p.detach().clone() for p in ps_ours]
+    loss = sum((p * 1.0).sum() for p in ps_ours)
+    o_ours.zero_grad()
+    scaler.scale(loss).backward()
+    ps_ours[0].grad[0, 0] = float("inf")
+    scaler.step(o_ours)
+    scaler.update()
+    for p, b in zip(ps_ours, before):
+        assert torch.equal(p.detach(), b)
+    assert float(o_ours.state[ps_ours[0]]["step"]) == 5.0

@@ -18,6 +18,7 @@ amp = "--amp" in sys.argv
 bf16 = "--bf16" in sys.argv
 fused = "--fused" in sys.argv          # train.train_step instead of the reference loop body
 adam_fused = "--adam-fused" in sys.argv
+our_adam = "--our-adam" in sys.argv     # train.Adam (one HIP launch per step)
 dims = [128, 128, 128]
 for a in sys.argv:
     if a.startswith("--dims="):
@@ -33,7 +34,10 @@ y = torch.arange(N, device=dev) // (20 ** (n - 1))
 if bf16:
     model.compute_dtype = torch.bfloat16
 data = pkg.Data(x=x, graph=g)
-opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0, fused=True if adam_fused else None)
+if our_adam:
+    opt = pkg.train.Adam(model.parameters(), lr=1e-3, weight_decay=0.0)
+else:
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=0.0, fused=True if adam_fused else None)
 model.train()
 
 
@@ -60,4 +64,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}, our_adam={our_adam}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

@@ -214,24 +214,11 @@ def edges_normalize(rc, eps: float) -> torch.Tensor:
     return out
 
 
-_PACK_CACHE: dict = {}
-
-
-def _version_key(ts):
-    return tuple(None if t is None else (t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
-
-
 def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
-    """pg_directgcn_pack_f32: [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] + bias sums, cached while the
-    parameters are unchanged: keyed on storage pointer + in-place version counter (optimizer steps,
-    load_state_dict and in-place ops under no_grad all bump it; writes through ``p.data`` do not -- call
-    clear_caches() after those). Entries hold their source tensors, so a key can never match a new tensor
-    that reused a freed address."""
+    """pg_directgcn_pack_f32: [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] + bias sums, packed on every call
+    (~5 us). Deliberately not cached: parameters updated by fused optimizers (torch's fused Adam, raw
+    kernels) keep their version counter, so a version-keyed cache would serve stale weights."""
     srcs = [prm[k] for k in _PACK_KEYS] + [W_res, b_res]
-    key = _version_key(srcs)
-    hit = _PACK_CACHE.get(key)
-    if hit is not None:
-        return hit[1]
     lib = load_library()
     F_out, F_in = prm["W_main_in"].shape
     n = lib.pg_directgcn_packed_floats(F_in, F_out, 1 if W_res is not None else 0)
@@ -242,39 +229,24 @@ def pack_weights(prm: dict, W_res=None, b_res=None) -> torch.Tensor:
     (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
      a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared, a.W_res, a.b_res) = [_p(t) for t in keep]
     check(lib.pg_directgcn_pack_f32(ctypes.byref(a), _p(out), _stream(out)), "pg_directgcn_pack_f32")
-    if len(_PACK_CACHE) >= 32:
-        _PACK_CACHE.pop(next(iter(_PACK_CACHE)))
-    _PACK_CACHE[key] = (srcs, out)
     return out
 
 
-_PACK16_CACHE: dict = {}
-
-
 def pack_weights_bf16(prm: dict, W_res=None, b_res=None):
-    """(fp32 packed operand, its bf16 copy [F_out*K]) for pg_directgcn_dense_bf16; cached like pack_weights."""
+    """(fp32 packed operand, its bf16 copy [F_out*K]) for pg_directgcn_dense_bf16 (packed per call, as
+    pack_weights)."""
     packed = pack_weights(prm, W_res, b_res)
-    srcs = [prm[k] for k in _PACK_KEYS] + [W_res, b_res]
-    key = (packed.data_ptr(), _version_key(srcs))
-    hit = _PACK16_CACHE.get(key)
-    if hit is not None:
-        return packed, hit[1]
     lib = load_library()
     F_out, F_in = prm["W_main_in"].shape
     n = F_out * (4 if W_res is not None else 3) * F_in
     out = torch.empty(n, device=packed.device, dtype=torch.bfloat16)
     check(lib.pg_f32_to_bf16(n, _p(packed), _p(out), _stream(packed)), "pg_f32_to_bf16")
-    if len(_PACK16_CACHE) >= 32:
-        _PACK16_CACHE.pop(next(iter(_PACK16_CACHE)))
-    _PACK16_CACHE[key] = (srcs + [packed], out)
     return packed, out
 
 
 def clear_caches():
-    """Drop the packed-weight and COO->CSR caches (e.g. after writing parameters through ``p.data``)."""
+    """Drop the COO->CSR cache (graphs are cached by the identity + version of their COO tensors)."""
     from .graph import clear_cache
-    _PACK_CACHE.clear()
-    _PACK16_CACHE.clear()
     clear_cache()
 
 

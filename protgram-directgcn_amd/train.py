@@ -166,6 +166,8 @@ class Adam(torch.optim.Optimizer):
                                   ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
                                   ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
                   "pg_adam_f32")
+            for p in ps:  # written in place by the kernel: let autograd / version-keyed caches see it
+                torch.autograd.graph.increment_version(p)
         return loss
 
 

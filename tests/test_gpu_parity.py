@@ -883,3 +883,34 @@ def test_fused_adam_matches_torch_adam(pkg, cuda):
     for p, b in zip(ps_ours, before):
         assert torch.equal(p.detach(), b)
     assert float(o_ours.state[ps_ours[0]]["step"]) == 5.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("writer", ["torch_fused_adam", "pg_adam", "no_version_bump"])
+def test_forward_sees_in_place_parameter_writes(pkg, cuda, writer):
+    """Regression: packed weights are rebuilt on every forward, so parameter writes that leave the version
+    counter alone (torch's fused Adam, raw kernels, .data copies) reach the next forward."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(2)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 32, generator=torch.Generator().manual_seed(3)).to(cuda)
+    torch.manual_seed(0)
+    m = pkg.ProtGramDirectGCN([32, 32, 32], N, 5, 2, 0, 16, 0.5, True).to(cuda).eval()
+    data = pkg.Data(x=x, graph=g)
+    m(data)  # first forward: anything cached would be cached now
+    if writer == "no_version_bump":
+        with torch.no_grad():
+            for p in m.parameters():
+                p.data.mul_(1.5)
+    else:
+        opt = (torch.optim.Adam(m.parameters(), lr=1e-2, fused=True) if writer == "torch_fused_adam"
+               else train.Adam(m.parameters(), lr=1e-2))
+        lp, _ = m(data)
+        lp.sum().backward()
+        opt.step()
+    lp, emb = m(data)
+    torch.manual_seed(0)
+    fresh = pkg.ProtGramDirectGCN([32, 32, 32], N, 5, 2, 0, 16, 0.5, True).to(cuda).eval()
+    fresh.load_state_dict(m.state_dict())
+    lp2, emb2 = fresh(data)
+    assert torch.equal(lp, lp2) and torch.equal(emb, emb2)

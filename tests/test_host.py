@@ -190,19 +190,3 @@ def test_oracle_not_imported_by_product():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
-
-
-def test_pack_cache_holds_its_keys(pkg):
-    """A cached entry keeps its source tensors alive, so a new parameter tensor can never be served the packed
-    weights of a freed one that happened to live at the same address with the same version counter."""
-    from protgram_directgcn_amd import ops
-    srcs = [torch.zeros(2, 2) for _ in range(3)]
-    key = ops._version_key(srcs)
-    ops._PACK_CACHE[key] = (srcs, torch.ones(1))
-    try:
-        ptrs = {t.data_ptr() for t in srcs}
-        del srcs
-        fresh = [torch.zeros(2, 2) for _ in range(3)]
-        assert not ({t.data_ptr() for t in fresh} & ptrs)
-    finally:
-        ops.clear_caches()

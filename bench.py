@@ -164,7 +164,12 @@ def main():
                 traffic = tj["kernel_bytes_per_launch"]
         except (OSError, ValueError):
             traffic = None
-    kname = "pg_spmm3_bf16" if args.bf16 else ("pg_spmm3_fusednorm_f32" if args.fused_norm else "pg_spmm3_f32")
+    if args.bf16:
+        kname = "pg_spmm3_bf16"
+    elif args.fused_norm:
+        kname = "pg_spmm3_fusednorm_f32"
+    else:  # single-GPU inference gates the aggregates in the propagation's store (same gathers, same B_agg)
+        kname = "pg_spmm3_gated_f32" if (world == 1 and ops.PREGATED_INFERENCE) else "pg_spmm3_f32"
     roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

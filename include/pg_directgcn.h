@@ -80,6 +80,10 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_4WAVES (1u << 9)  /* dense kernel: 4 waves per 128-row tile (64x64 per wave) instead of 8 */
 #define PG_FLAG_SPMM_BLOCK512 (1u << 10)  /* SpMM variant C: 512-thread blocks (more consecutive rows per CU) */
 #define PG_FLAG_SPMM_BLOCK1024 (1u << 11) /* SpMM variant C: 1024-thread blocks */
+#define PG_FLAG_DENSE_PF2 (1u << 12)      /* dense kernel: two K tiles of operands in flight (register sets) */
+#define PG_FLAG_DENSE_WS (1u << 13)       /* dense kernel: W-stationary persistent variant (F_out = 128; default when pre-gated) */
+#define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
+#define PG_FLAG_DENSE_TILED (1u << 15)    /* dense kernel: never the W-stationary variant */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -97,6 +101,7 @@ int pg_abi_version(void);
 int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
                  const float* X, int64_t ldx, int64_t F,
                  float* Z, int64_t ldz, uint32_t flags, void* stream);
+
 
 /* Same output as pg_spmm3_f32, with the three propagation weights computed in-kernel from raw counts
  * (graph_utils.py:198-273 closed form; bit-exact to the reference's torch.sparse construction) and
@@ -199,6 +204,15 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stre
 /* The contraction + epilogue. Reads weights/biases from `packed` (the W_* / b_* fields of args are not
  * read); W_res != NULL selects the projected residual. */
 int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
+
+/* pg_spmm3_f32 with the DirectGCN gates applied at the store: Z_q[i] = s_q(i) * (A_q X)[i], s_in = c_all*c_dir*c_in,
+ * s_out = c_all*c_dir*c_out, s_und = c_all*c_und (protgram_directgcn.py:116-133), from the C_* / gate_mode fields
+ * of `gates` (rows must be NULL). The inference producer for pg_directgcn_dense_f32 with
+ * PG_FLAG_DENSE_PREGATED (whose operand is exactly s_q * Z_q); training keeps the ungated Z for the gate
+ * gradients. */
+int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                       const float* X, int64_t ldx, int64_t F, const pg_layer_args_t* gates,
+                       float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

@@ -21,6 +21,9 @@ PG_FLAG_TILED_FC64 = 1 << 5
 PG_FLAG_UNTILED = 1 << 6
 PG_FLAG_BCAST_RECORDS = 1 << 7
 PG_FLAG_DENSE_4WAVES = 1 << 9
+PG_FLAG_DENSE_WS = 1 << 13
+PG_FLAG_DENSE_PREGATED = 1 << 14
+PG_FLAG_DENSE_TILED = 1 << 15
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -69,6 +72,8 @@ SIGNATURES = {
     "pg_last_error": (ctypes.c_char_p, []),
     "pg_abi_version": (ctypes.c_int, []),
     "pg_spmm3_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3_gated_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, ctypes.POINTER(LayerArgs), c_vp,
+                                          c_i64, c_u32, c_vp]),
     "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
                                               c_u32, c_vp]),
     "pg_spmm3_tiled_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),

@@ -22,6 +22,7 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;
 constexpr int LDSW = 36;  // padded LDS row (floats)
@@ -47,6 +48,8 @@ struct DenseP {
     float* Y;
     int64_t ldy;
     int remap;
+    int pregated;  // A segments 0..2 already carry their gates (pg_spmm3_gated_f32): no scaling here
+    int dbg;  // dense_ws timing probes only (flags bits 20-22): 1 no epilogue memory, 2 no DMA, 4 no MFMA
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -57,12 +60,12 @@ __device__ __forceinline__ int seg_of(int k, int F) { return (k >= F) + (k >= 2 
 // one element of the logical A matrix [M, K]
 __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_t m, int k) {
     const int q = seg_of(k, p.F_in);
-    if (q < 3) return p.Z[m * p.ldz + k] * sg[q];
+    if (q < 3) return p.pregated ? p.Z[m * p.ldz + k] : p.Z[m * p.ldz + k] * sg[q];
     return p.res_x[m * p.ld_res + (k - 3 * p.F_in)];
 }
 
-template <int BM, int BN, int NW, bool VEC>
-__global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
+template <int BM, int BN, int NW, bool VEC, int PF = 1>
+__global__ __launch_bounds__(64 * NW, PF == 2 ? 4 : 1) void dense_kernel(DenseP p) {
     constexpr int NT = 64 * NW;  // threads
     constexpr int WN = (BM == 64 && NW == 8) ? 4 : (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
     constexpr int WM = NW / WN;
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
     // MFMA phase; the gate scale / zero-fill is applied at stash time, just before the LDS write.
     float4 ra[A_F4], rb[B_F4];
     const int64_t mlast = p.M - 1;
-    auto fetch = [&](int k0) {
+    auto fetch_to = [&](int k0, float4 (&ra)[A_F4], float4 (&rb)[B_F4]) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
             const int idx = tid + NT * q;
@@ -161,7 +164,8 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
             }
         }
     };
-    auto stash = [&](int buf, int k0) {
+    auto fetch = [&](int k0) { fetch_to(k0, ra, rb); };
+    auto stash_from = [&](int buf, int k0, const float4 (&ra)[A_F4], const float4 (&rb)[B_F4]) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
             const int idx = tid + NT * q;
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
             if (VEC) {
                 const int k = k0 + 4 * (idx & 7);
                 const int seg = seg_of(k, p.F_in);
-                const float sc = k < p.K ? Sg[(idx >> 3) * 4 + seg] : 0.f;  // Sg[.., 3] == 1 (residual)
+                const float sc = k < p.K ? (p.pregated ? 1.f : Sg[(idx >> 3) * 4 + seg]) : 0.f;  // Sg[.., 3] == 1
                 v = scale4(v, sc);
             }
             *reinterpret_cast<float4*>(&As[buf][(idx >> 3) * LDSW + 4 * (idx & 7)]) = v;
@@ -186,13 +190,8 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
         }
     };
 
-    const int ntiles = (p.K + BK - 1) / BK;
-    fetch(0);
-    stash(0, 0);
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-        const int cur = t & 1;
-        if (t + 1 < ntiles) fetch((t + 1) * BK);
+    auto stash = [&](int buf, int k0) { stash_from(buf, k0, ra, rb); };
+    auto mma = [&](int cur) {
         const float* Ab = As[cur];
         const float* Bb = Bs[cur];
 #pragma unroll
@@ -212,8 +211,38 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
                 }
         }
-        if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BK);
+    };
+
+    const int ntiles = (p.K + BK - 1) / BK;
+    if constexpr (PF == 1) {
+        fetch(0);
+        stash(0, 0);
         __syncthreads();
+        for (int t = 0; t < ntiles; ++t) {
+            const int cur = t & 1;
+            if (t + 1 < ntiles) fetch((t + 1) * BK);
+            mma(cur);
+            if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BK);
+            __syncthreads();
+        }
+    } else {
+        // two K tiles in flight: register set 0 / 1 alternate (loop unrolled by 2 for static indexing)
+        float4 ra1[A_F4], rb1[B_F4];
+        fetch(0);
+        stash(0, 0);
+        if (ntiles > 1) fetch_to(BK, ra1, rb1);
+        __syncthreads();
+        for (int t = 0; t < ntiles; t += 2) {
+            if (t + 2 < ntiles) fetch_to((t + 2) * BK, ra, rb);
+            mma(0);
+            if (t + 1 < ntiles) stash_from(1, (t + 1) * BK, ra1, rb1);
+            __syncthreads();
+            if (t + 1 >= ntiles) break;
+            if (t + 3 < ntiles) fetch_to((t + 3) * BK, ra1, rb1);
+            mma(1);
+            if (t + 2 < ntiles) stash_from(0, (t + 2) * BK, ra, rb);
+            __syncthreads();
+        }
     }
 
     // Epilogue: park the accumulator tile in LDS (C/D map of the 32x32 MFMA: col = lane&31,
@@ -310,6 +339,221 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// W-stationary variant (F_out = 128): the packed weights never move after the prologue. Wave w of the
+// 512-thread workgroup owns output columns [16w, 16w+16) over the WHOLE K, held in K/4 VGPRs per lane
+// (v_mfma_f32_16x16x4f32: lane l supplies B[k = l>>4][n = l&15]; with the K permutation of dense_kernel a
+// group of 16 k is one float4 per lane), so there is no K split and no partial-sum reduction. One workgroup
+// per CU walks 32-row tiles (XCD-contiguous deal); each tile's A rows arrive by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction, lane-linear) into a double-buffered image whose
+// 16-byte chunks are XOR-swizzled by row (chunk c of row r at c ^ (r & 15), set through the per-lane SOURCE
+// address), which makes the 16x16x4 A-fragment ds_read_b128 conflict-free. Gates scale the A fragment after
+// the LDS read. One barrier per tile; the epilogue runs from the accumulators with the constant / residual
+// values prefetched before the MFMAs.
+// One LDS-DMA piece: 16 B per lane from a per-lane global address to (wave-uniform base + 16 * lane).
+__device__ __forceinline__ void glds16(const float* src, float* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 0);
+}
+
+template <int F_IN, int KSEG, bool PRE>
+__global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
+    constexpr int K = F_IN * KSEG;
+    constexpr int CH = K / 4;        // 16-B chunks per row
+    constexpr int BMW = 32;          // rows per tile
+    constexpr int NG = K / 16;       // k-groups
+    constexpr int NI = BMW * CH / 64 / 8;  // LDS-DMA instructions per wave per tile
+    static_assert(CH % 16 == 0 && (BMW * CH) % 512 == 0, "tile shape");
+    // two distinct LDS objects (not As[2][..]) so the compiler can tell the DMA target of the next tile from
+    // the image being read, and does not drain the DMA before every ds_read
+    __shared__ __attribute__((aligned(16))) float As0[BMW * K];
+    __shared__ __attribute__((aligned(16))) float As1[BMW * K];
+    constexpr int ELD = 128 + 4;  // epilogue tile row (floats)
+    __shared__ __attribute__((aligned(16))) float Es[BMW * ELD];   // contraction result
+    __shared__ __attribute__((aligned(16))) float Cs[BMW * 128];   // constant rows (LDS-DMA)
+    __shared__ __attribute__((aligned(16))) float Rs[BMW * 128];   // identity-residual rows (LDS-DMA)
+    __shared__ float Sg[2][BMW][4];
+    __shared__ int64_t Crow[2][BMW];
+    __shared__ __attribute__((aligned(16))) float Bs[4][128];  // bias sums (row 3: b_res or 0)
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int lc = lane & 15, kg = lane >> 4;
+    const int col = 16 * wave + lc;
+    const int64_t T = (p.M + BMW - 1) / BMW;
+    Bs[tid >> 7][tid & 127] = (tid >> 7) < 3 || p.proj_res ? p.bsum[(tid >> 7) * p.F_out + (tid & 127)] : 0.f;
+    const int nb = gridDim.x, b = blockIdx.x;
+    int64_t ntl, lo, step;
+    if ((nb & 7) == 0 && nb >= 8) {  // XCD x takes a contiguous range of tiles
+        const int x = b & 7, i = b >> 3, bpx = nb >> 3;
+        const int64_t xlo = T * x / 8, xhi = T * (x + 1) / 8;
+        ntl = (xhi - xlo - i + bpx - 1) / bpx;
+        lo = xlo + i;
+        step = bpx;
+    } else {
+        ntl = (T - b + nb - 1) / nb;
+        lo = b;
+        step = nb;
+    }
+    if (ntl < 0) ntl = 0;
+
+    float4 wr[NG];
+    {
+        const float* src = p.Bp + (int64_t)col * K + 4 * kg;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) wr[g] = ld4(src + 16 * g);
+    }
+    // epilogue role: thread owns columns [4ej, 4ej+4) of rows er and er + 16
+    const int ej = tid & 31, er = tid >> 5;
+    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
+    const bool id_res = p.res_x && !p.proj_res;
+
+    // gates of tile row tid (< BMW), protgram_directgcn.py:116-133: raw loads now, products later
+    struct GateRaw {
+        float ci, co, cd, cu, ca;
+        int64_t cr;
+    };
+    auto gate_load = [&](int64_t tile) {
+        GateRaw g{0.f, 0.f, 0.f, 0.f, 0.f, -1};
+        const int64_t m = tile * BMW + tid;
+        if (m < p.M) {
+            g.cr = p.rows ? p.rows[m] : m;
+            const int64_t r = (p.gate_mode == PG_GATES_SCALAR) ? 0 : g.cr;
+            g.ci = p.C_in[r];
+            g.co = p.C_out[r];
+            g.cd = p.C_dir[r];
+            g.cu = p.C_und[r];
+            g.ca = p.C_all[r];
+        }
+        return g;
+    };
+    auto gate_store = [&](const GateRaw& g, int sbuf) {
+        const float cad = g.ca * g.cd;
+        Sg[sbuf][tid][0] = cad * g.ci;
+        Sg[sbuf][tid][1] = cad * g.co;
+        Sg[sbuf][tid][2] = g.ca * g.cu;
+        Sg[sbuf][tid][3] = 1.f;
+        Crow[sbuf][tid] = g.cr;
+    };
+    auto issue_A = [&](int64_t tile, float* Ad) {
+        const int64_t m0 = tile * BMW;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int idx = (wave * NI + i) * 64 + lane;  // lane-linear chunk of the tile image
+            const int r = idx / CH, pos = idx % CH;
+            const int c = pos ^ (r & 15);
+            const int k = 4 * c;
+            const int64_t m = min(m0 + r, p.M - 1);
+            const float* src = k < 3 * F_IN ? p.Z + m * p.ldz + k : p.res_x + m * p.ld_res + (k - 3 * F_IN);
+            if (!(p.dbg & 2)) glds16(src, Ad + (wave * NI + i) * 256);
+        }
+    };
+    // constant / residual rows of the current tile: 32 rows x 512 B each = 16 pieces of 1 KiB, 2 per wave
+    auto issue_CR = [&](int64_t tile, int sbuf) {
+        const int64_t m0 = tile * BMW;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int piece = wave * 2 + i;           // rows 2*piece, 2*piece + 1
+            const int r = 2 * piece + (lane >> 5);
+            const int64_t cr = Crow[sbuf][r];
+            const int64_t m = min(m0 + r, p.M - 1);
+            if (has_const) glds16(p.constant + (cr >= 0 ? cr : 0) * p.ld_const + 4 * (lane & 31), Cs + piece * 256);
+            if (id_res) glds16(p.res_x + m * p.ld_res + 4 * (lane & 31), Rs + piece * 256);
+        }
+    };
+
+    auto tile_body = [&](int64_t kt, const float* Ab, float* An, int buf) {
+        const int64_t m0 = (lo + kt * step) * BMW;
+        asm volatile("" ::: "memory");  // LDS-DMA wrote Ab (and the previous epilogue's Cs / Rs are consumed)
+        __syncthreads();                // (vmcnt(0): this tile's A rows have landed in every wave)
+        issue_CR(lo + kt * step, buf);  // lands during the MFMAs, read after the second barrier
+        const bool more = kt + 1 < ntl;
+        GateRaw gr{};
+        if (more && tid < BMW) gr = gate_load(lo + (kt + 1) * step);  // consumed after the MFMAs
+        if (more) issue_A(lo + (kt + 1) * step, An);
+        float sa[2][3];  // gates of this lane's A rows (row lc of each 16-row subtile)
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) sa[sb][q] = Sg[buf][16 * sb + lc][q];
+        // chunk (4g + kg) of row 16sb + lc sits at chunk 16(g>>2) + ((4(g&3) + kg) ^ lc): four per-lane base
+        // offsets, the rest is a compile-time ds_read immediate
+        const float* Ar = Ab + lc * K;
+        int aoff[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) aoff[j] = 4 * ((4 * j + kg) ^ lc);
+        auto ldA = [&](int g, int sb) { return ld4(Ar + aoff[g & 3] + (16 * sb * K + 64 * (g >> 2))); };
+        f32x4 acc[2];
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb) acc[sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (!(p.dbg & 4)) {
+            float4 a0 = ldA(0, 0), a1 = ldA(0, 1);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                float4 n0 = a0, n1 = a1;
+                if (g + 1 < NG) {  // one group of fragments ahead; the sched_barrier below stops the scheduler
+                    n0 = ldA(g + 1, 0);  // from hoisting every read of the tile
+                    n1 = ldA(g + 1, 1);
+                }
+                const int q = (16 * g) / F_IN;  // K segment of this group (F_IN % 16 == 0)
+                if (!PRE && q < 3) {  // gate the aggregates; the projected-residual segment is not gated
+                    a0 = scale4(a0, sa[0][q]);
+                    a1 = scale4(a1, sa[1][q]);
+                }
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, wr[g].x, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, wr[g].x, acc[1], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, wr[g].y, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, wr[g].y, acc[1], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, wr[g].z, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, wr[g].z, acc[1], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, wr[g].w, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, wr[g].w, acc[1], 0, 0, 0);
+                a0 = n0;
+                a1 = n1;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // C/D map of 16x16: rows 4*kg + i, column lc
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Es[(16 * sb + 4 * kg + i) * ELD + col] = acc[sb][i];
+        if (more && tid < BMW) gate_store(gr, buf ^ 1);
+        asm volatile("" ::: "memory");  // LDS-DMA wrote Cs / Rs
+        __syncthreads();
+        // epilogue, row-major float4 sweep: y = acc + sum_q s_q b_q + b_res + constant + residual
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int rl = er + 16 * h;
+            if (Crow[buf][rl] < 0 || (p.dbg & 1)) continue;
+            const float4 v = ld4(&Es[rl * ELD + 4 * ej]);
+            const float4 cv = has_const ? ld4(&Cs[rl * 128 + 4 * ej]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 rv = id_res ? ld4(&Rs[rl * 128 + 4 * ej]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 b0 = ld4(&Bs[0][4 * ej]), b1 = ld4(&Bs[1][4 * ej]), b2 = ld4(&Bs[2][4 * ej]),
+                         br = ld4(&Bs[3][4 * ej]);
+            const float s0 = Sg[buf][rl][0], s1 = Sg[buf][rl][1], s2 = Sg[buf][rl][2];
+            const float o[4] = {v.x, v.y, v.z, v.w}, C4[4] = {cv.x, cv.y, cv.z, cv.w}, R4[4] = {rv.x, rv.y, rv.z, rv.w};
+            const float B0[4] = {b0.x, b0.y, b0.z, b0.w}, B1[4] = {b1.x, b1.y, b1.z, b1.w},
+                        B2[4] = {b2.x, b2.y, b2.z, b2.w}, BR[4] = {br.x, br.y, br.z, br.w};
+            float y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float qv = o[e] + (s0 * B0[e] + s1 * B1[e] + s2 * B2[e]) + BR[e] + C4[e] + R4[e];
+                y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
+            }
+            *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
+        }
+    };
+
+    if (ntl > 0) {
+        if (tid < BMW) gate_store(gate_load(lo), 0);
+        issue_A(lo, As0);
+    }
+    for (int64_t kt = 0; kt < ntl; kt += 2) {
+        tile_body(kt, As0, As1, 0);
+        if (kt + 1 < ntl) tile_body(kt + 1, As1, As0, 1);
+    }
+}
+
 __global__ __launch_bounds__(256) void pack_kernel(int F_in, int F_out, int K, const float* W0, const float* W1,
                                                    const float* W2, const float* Ws, const float* Wr,
                                                    const float* bm0, const float* bs0, const float* bm1,
@@ -403,6 +647,8 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.Y = a->Y;
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    p.dbg = (int)((flags >> 20) & 7);
+    p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.vec_out = (a->F_out % 4 == 0) && (a->ldy % 4 == 0) && pg::aligned16(a->Y) &&
                 (!a->constant || (a->ld_const % 4 == 0 && pg::aligned16(a->constant))) &&
                 (!a->res_x || a->W_res || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)));
@@ -422,10 +668,34 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     hipStream_t s = (hipStream_t)stream;
 #define PG_LAUNCH(BMx, BNx, NWx)                                                                                \
     do {                                                                                                           \
-        if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
+        if (vec && pf2) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true, 2>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
+        else if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
         else hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, false>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p);    \
     } while (0)
     const bool w8 = !(flags & PG_FLAG_DENSE_4WAVES);
+    const bool pf2 = (flags & PG_FLAG_DENSE_PF2) != 0;
+    // W-stationary kernel: the default for pre-gated operands (measured 0.161 vs 0.176 ms for the tiled kernel at
+    // B(20,4), F=128); PG_FLAG_DENSE_WS forces it, PG_FLAG_DENSE_TILED forbids it
+    const bool want_ws = (flags & PG_FLAG_DENSE_WS) || (p.pregated && !(flags & PG_FLAG_DENSE_TILED));
+    if (want_ws && a->F_out == 128 && vec && p.vec_out && (a->F_in == 64 || (a->F_in == 128 && !a->W_res)) &&
+        (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)))) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        const int64_t T = (a->M + 31) / 32;
+        const unsigned g = (unsigned)(T < ncu ? T : ncu);
+#define PG_WS(FI, KS)                                                                                     \
+    do {                                                                                                  \
+        if (p.pregated) hipLaunchKernelGGL((dense_ws_kernel<FI, KS, true>), dim3(g), dim3(512), 0, s, p); \
+        else hipLaunchKernelGGL((dense_ws_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
+    } while (0)
+        if (a->F_in == 128) PG_WS(128, 3);
+        else if (!p.proj_res) PG_WS(64, 3);
+        else PG_WS(64, 4);
+#undef PG_WS
+        return pg::check_launch("pg_directgcn_dense_f32");
+    }
     if (bm64 && w8 && wide) {
         PG_LAUNCH(64, 128, 8);  // 8 waves of 32x32 (measured 0.186 ms vs 0.177 for the default at B(20,4))
     } else if (bm64) {

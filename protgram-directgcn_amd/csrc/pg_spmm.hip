@@ -35,7 +35,31 @@ struct SpmmParams {
     int F;
     int accumulate;
     int remap;
+    // optional output gates (pg_spmm3_gated_f32): Z_q[i] *= s_q(i) at the store, s = the DirectGCN gates
+    // s_in = c_all*c_dir*c_in, s_out = c_all*c_dir*c_out, s_und = c_all*c_und (protgram_directgcn.py:116-133)
+    const float *g_in, *g_out, *g_dir, *g_und, *g_all;
+    int gate_scalar;
 };
+
+// Gate inputs of row `row`, loaded when the row starts (so their latency hides behind the row's gathers) and
+// turned into the three gates at the store (1, 1, 1 when the call is not gated). Same products as pg_dense.hip.
+struct GateIn {
+    float ci, co, cd, cu, ca;
+};
+__device__ __forceinline__ GateIn gate_in(const SpmmParams& p, int64_t row, bool live) {
+    GateIn g{1.f, 1.f, 1.f, 1.f, 1.f};
+    if (p.g_all && live) {
+        const int64_t r = p.gate_scalar ? 0 : row;
+        g = GateIn{p.g_in[r], p.g_out[r], p.g_dir[r], p.g_und[r], p.g_all[r]};
+    }
+    return g;
+}
+__device__ __forceinline__ void row_gates(const GateIn& g, float s[3]) {
+    const float cad = __fmul_rn(g.ca, g.cd);
+    s[0] = __fmul_rn(cad, g.ci);
+    s[1] = __fmul_rn(cad, g.co);
+    s[2] = __fmul_rn(g.ca, g.cu);
+}
 
 __device__ __forceinline__ float fb(int v) { return __int_as_float(v); }
 __device__ __forceinline__ float mul(float a, float b) { return __fmul_rn(a, b); }
@@ -124,6 +148,8 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
     if constexpr (MODE == M3RAW) {
         if (live) ni = p.node_norm[row];
     }
+    GateIn gin{1.f, 1.f, 1.f, 1.f, 1.f};
+    if constexpr (Shape<MODE>::NACC == 3) gin = gate_in(p, row, live);
 
     float4 acc[NACC][NV];
 #pragma unroll
@@ -222,6 +248,8 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
     }
 
     if (!live) return;
+    float gs[3] = {1.f, 1.f, 1.f};
+    if constexpr (NACC == 3) row_gates(gin, gs);
     float4* Z4 = reinterpret_cast<float4*>(p.Z) + row * (p.ldz >> 2) + t;
 #pragma unroll
     for (int a = 0; a < NACC; ++a)
@@ -229,6 +257,8 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
         for (int v = 0; v < NV; ++v) {
             float4* dst = Z4 + a * F4 + v * LPR;
             float4 val = acc[a][v];
+            if (NACC == 3 && p.g_all)
+                val = make_float4(mul(val.x, gs[a]), mul(val.y, gs[a]), mul(val.z, gs[a]), mul(val.w, gs[a]));
             if (p.accumulate) {
                 const float4 old = *dst;
                 val = make_float4(add(old.x, val.x), add(old.y, val.y), add(old.z, val.z), add(old.w, val.w));
@@ -245,7 +275,7 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
 // group's own LDS window, and read them back as LDS broadcasts: the TD only carries the feature gathers.
 // A window is private to one row group inside one wave, so wave-local ordering (the compiler's
 // lgkmcnt waits + a wave barrier) replaces block barriers. Same accumulation order: still bit-exact.
-template <int LPR, int NV, int U, int MODE, int NT = 256>
+template <int LPR, int NV, int U, int MODE, int NT = 256, bool GATED = false>
 __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
     using R = typename Rec<MODE>::T;
     constexpr int RPB = NT / LPR;
@@ -273,6 +303,8 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
     if constexpr (MODE == M3RAW) {
         if (live) ni = p.node_norm[row];
     }
+    GateIn gin{1.f, 1.f, 1.f, 1.f, 1.f};
+    if constexpr (GATED && Shape<MODE>::NACC == 3) gin = gate_in(p, row, live);
     float4 acc[NACC][NV];
 #pragma unroll
     for (int a = 0; a < NACC; ++a)
@@ -380,6 +412,8 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
         }
     }
     if (!live) return;
+    float gs[3] = {1.f, 1.f, 1.f};
+    if constexpr (GATED && NACC == 3) row_gates(gin, gs);
     float4* Z4 = reinterpret_cast<float4*>(p.Z) + row * (p.ldz >> 2) + t;
 #pragma unroll
     for (int a = 0; a < NACC; ++a)
@@ -387,6 +421,8 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
         for (int v = 0; v < NV; ++v) {
             float4* dst = Z4 + a * F4 + v * LPR;
             float4 val = acc[a][v];
+            if (GATED && NACC == 3)
+                val = make_float4(mul(val.x, gs[a]), mul(val.y, gs[a]), mul(val.z, gs[a]), mul(val.w, gs[a]));
             if (p.accumulate) {
                 const float4 old = *dst;
                 val = make_float4(add(old.x, val.x), add(old.y, val.y), add(old.z, val.z), add(old.w, val.w));
@@ -411,6 +447,8 @@ __global__ __launch_bounds__(256) void spmm_scalar_kernel(SpmmParams p) {
     const int64_t beg = p.rowptr[row], end = p.rowptr[row + 1];
     float4 ni = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (MODE == M3RAW) ni = p.node_norm[row];
+    GateIn gin{1.f, 1.f, 1.f, 1.f, 1.f};
+    if constexpr (NACC == 3) gin = gate_in(p, row, true);
     for (int f0 = 0; f0 < p.F; f0 += 64) {
         const int f = f0 + lane;
         const bool on = f < p.F;
@@ -440,9 +478,12 @@ __global__ __launch_bounds__(256) void spmm_scalar_kernel(SpmmParams p) {
             }
         }
         if (on) {
+            float gs[3] = {1.f, 1.f, 1.f};
+            if constexpr (NACC == 3) row_gates(gin, gs);
 #pragma unroll
             for (int a = 0; a < NACC; ++a) {
                 float* dst = p.Z + row * p.ldz + a * p.F + f;
+                if (NACC == 3 && p.g_all) acc[a] = mul(acc[a], gs[a]);
                 *dst = p.accumulate ? add(*dst, acc[a]) : acc[a];
             }
         }
@@ -481,6 +522,12 @@ void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
         const int64_t rpb = nt / LPR;
         const int64_t nb = (p.n_rows + rpb - 1) / rpb;
         const bool u8 = flags & PG_FLAG_UNROLL4;
+        if (p.g_all) {  // gated store (pg_spmm3_gated_f32): the default configuration only
+            if constexpr (Shape<MODE>::NACC == 3)
+                hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE, 256, true>), dim3((unsigned)((p.n_rows + 256 / LPR - 1) / (256 / LPR))),
+                                   dim3(256), 0, s, p);
+            return;
+        }
 #define PG_WIN(NTv)                                                                                            \
     do {                                                                                                       \
         if (u8) hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 8, MODE, NTv>), dim3((unsigned)nb), dim3(NTv), 0, s, p); \
@@ -549,6 +596,25 @@ int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order
     if (rc) return rc;
     SpmmParams p{n_rows, rowptr, row_order, edges, X, ldx, Z, ldz, nullptr, 0.f, (int)F, 0, 1};
     return dispatch<M3>(p, flags, (hipStream_t)stream, "pg_spmm3_f32");
+}
+
+int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
+                       const float* X, int64_t ldx, int64_t F, const pg_layer_args_t* gates, float* Z, int64_t ldz,
+                       uint32_t flags, void* stream) {
+    int rc = common_checks(n_rows, rowptr, edges, X, ldx, F, Z, ldz, 3 * F, F);
+    if (rc) return rc;
+    PG_REQUIRE(gates && gates->C_in && gates->C_out && gates->C_directed && gates->C_undirected && gates->C_all,
+               "null gate");
+    PG_REQUIRE(gates->gate_mode == PG_GATES_VECTOR || gates->gate_mode == PG_GATES_SCALAR, "bad gate_mode");
+    PG_REQUIRE(gates->rows == nullptr, "gated propagation takes no original_indices (gate rows = graph rows)");
+    SpmmParams p{n_rows, rowptr, row_order, edges, X, ldx, Z, ldz, nullptr, 0.f, (int)F, 0, 1};
+    p.g_in = gates->C_in;
+    p.g_out = gates->C_out;
+    p.g_dir = gates->C_directed;
+    p.g_und = gates->C_undirected;
+    p.g_all = gates->C_all;
+    p.gate_scalar = gates->gate_mode == PG_GATES_SCALAR;
+    return dispatch<M3>(p, flags, (hipStream_t)stream, "pg_spmm3_gated_f32");
 }
 
 int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edgeraw_t* edges,

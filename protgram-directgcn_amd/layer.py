@@ -142,11 +142,21 @@ class DirectGCNLayer(nn.Module):
                                    "(pass original_indices for subgraphs)")
         if graph.n_rows != M:
             raise ValueError("graph rows != x rows")
-        Z = ops.Propagate3.apply(x, graph, fused_norm)
         constant = self.constant if self.use_vector_coeffs else None
         gate_mode = 0 if self.use_vector_coeffs else 1
+        params = self._dense_params()
+        if (ops.PREGATED_INFERENCE and rows is None and not fused_norm
+                and not (torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)))):
+            # inference: the gates are applied by the propagation's store (pg_spmm3_gated_f32) and the dense kernel
+            # takes the pre-gated operand (W-stationary kernel where the shape allows)
+            prm = dict(zip(ops._DENSE_KEYS, params))
+            Z = ops.spmm3_gated(graph, x, prm, gate_mode)
+            if Z is not None:
+                return ops.layer_dense(Z, prm, gate_mode, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
+                                       act=act, pregated=True)
+        Z = ops.Propagate3.apply(x, graph, fused_norm)
         return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, gate_mode, act, ops.LEAKY_SLOPE,
-                                    *self._dense_params())
+                                    *params)
 
     def forward(self, x: torch.Tensor,
                 edge_index_in: torch.Tensor, edge_weight_in: Optional[torch.Tensor],

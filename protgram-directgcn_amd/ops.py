@@ -21,6 +21,9 @@ from .graph import CSRGraph, ShapedAdjacency
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
 
 BF16_BACKWARD = True  # bf16 mode trains through pg_directgcn_dense_bwd_bf16 / pg_spmm3t_bf16
+# Inference (no autograd) forwards gate the aggregates in the propagation's store (pg_spmm3_gated_f32) and run the
+# dense kernel on the pre-gated operand; False = the training-path kernels in inference too.
+PREGATED_INFERENCE = True
 
 # Optional live timing of the propagation kernel: when set to a list, spmm3 appends one
 # (start, end) pair of HIP events recorded on the launch stream around each propagation launch.
@@ -153,6 +156,31 @@ def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
     return Z
 
 
+def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: Optional[int] = None,
+                out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """pg_spmm3_gated_f32: Z_q = s_q * (A_q x) with the layer's gates applied at the store -- the operand of
+    layer_dense(..., pregated=True). fp32, shared pattern, precomputed weights only; None otherwise (callers
+    then gate inside the dense kernel)."""
+    if _is_bf16(x) or not g.shared or g.edges3 is None:
+        return None
+    lib = load_library()
+    x = _f32c(x)
+    _require_gpu(x)
+    _require_graph_on(g, x)
+    N, F = g.n_rows, x.size(1)
+    if x.size(0) < N:
+        raise ValueError("x has fewer rows than the graph")
+    Z = out if out is not None else torch.empty(N, 3 * F, device=x.device, dtype=torch.float32)
+    a, keep = _layer_args(None, prm, gate_mode, M=N)
+    fl = default_flags() if flags is None else flags
+    ev = _ev_start(x)
+    check(lib.pg_spmm3_gated_f32(N, _p(g.rowptr), _p(g.row_order), _p(g.edges3), _p(x), x.stride(0), F,
+                                 ctypes.byref(a), _p(Z), Z.stride(0), fl, _stream(x)), "pg_spmm3_gated_f32")
+    _ev_end(x, ev)
+    del keep
+    return Z
+
+
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
     """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX."""
     lib = load_library()
@@ -255,9 +283,13 @@ _PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in"
 
 
 def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None,
-                act: bool = False, slope: float = LEAKY_SLOPE, Y=None):
-    """pg_layer_args_t for the forward block; returns (args, keep-alive list)."""
-    M, F_in = Z.size(0), Z.size(1) // 3
+                act: bool = False, slope: float = LEAKY_SLOPE, Y=None, M: Optional[int] = None):
+    """pg_layer_args_t for the forward block; returns (args, keep-alive list). Z=None (gate-only uses) takes the
+    row count from M."""
+    if Z is None:
+        M, F_in = int(M), prm["W_main_in"].size(1)
+    else:
+        M, F_in = Z.size(0), Z.size(1) // 3
     F_out = prm["W_main_in"].size(0)
     keep = []
 
@@ -270,9 +302,11 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
     a = LayerArgs()
     a.M, a.F_in, a.F_out = M, F_in, F_out
-    Zc = _bf16c(Z.detach()) if _is_bf16(Z) else _f32c(Z.detach())
-    keep.append(Zc)
-    a.Z, a.ldz = _p(Zc), Zc.stride(0)
+    b16 = Z is not None and _is_bf16(Z)
+    if Z is not None:
+        Zc = _bf16c(Z.detach()) if b16 else _f32c(Z.detach())
+        keep.append(Zc)
+        a.Z, a.ldz = _p(Zc), Zc.stride(0)
     a.gate_mode = gate_mode
     a.C_in, a.C_out, a.C_directed = c(prm["C_in"]), c(prm["C_out"]), c(prm["C_directed"])
     a.C_undirected, a.C_all = c(prm["C_undirected"]), c(prm["C_all"])
@@ -280,7 +314,7 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     if constant is not None:
         a.constant, a.ld_const = c(constant), constant.size(1)
     if res_x is not None:
-        rx = _bf16c(res_x.detach()) if _is_bf16(Z) else _f32c(res_x.detach())
+        rx = _bf16c(res_x.detach()) if b16 else _f32c(res_x.detach())
         keep.append(rx)
         a.res_x, a.ld_res = _p(rx), rx.stride(0)
     a.W_res = c(W_res)
@@ -294,7 +328,7 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
                 act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, pregated: bool = False) -> torch.Tensor:
     """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header). bf16 Z ->
     pg_directgcn_dense_bf16 (bf16 output)."""
     lib = load_library()
@@ -320,6 +354,8 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
+    if pregated:
+        fl |= _lib.PG_FLAG_DENSE_PREGATED
     check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
     del keep
     return Y

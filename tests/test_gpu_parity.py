@@ -354,11 +354,15 @@ def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
 
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
                                                       (300, 32, 16, False, False, False), (513, 20, 12, True, True, False),
-                                                      (129, 16, 40, True, True, True), (64, 128, 96, False, True, True)])
+                                                      (129, 16, 40, True, True, True), (64, 128, 96, False, True, True),
+                                                      (31, 128, 128, False, True, False), (4097, 64, 128, False, True, False),
+                                                      (2050, 128, 128, False, False, False), (700, 128, 128, True, True, False)])
 def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
-    """pg_directgcn_dense_f32 (all tilings) against the same formula in float64."""
+    """pg_directgcn_dense_f32 (all tilings, the W-stationary kernel, pre-gated operands) against the same formula in
+    float64. Pre-gated: the operand is s_q * Z_q (what pg_spmm3_gated_f32 stores) with PG_FLAG_DENSE_PREGATED."""
     from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_NO_XCD_REMAP
+    from protgram_directgcn_amd._lib import (PG_FLAG_DENSE_4WAVES, PG_FLAG_DENSE_BM64, PG_FLAG_DENSE_TILED,
+                                             PG_FLAG_DENSE_WS, PG_FLAG_NO_XCD_REMAP)
     g = torch.Generator().manual_seed(M + Fin + Fout)
     Ntot = M + 37
     Z = torch.randn(M, 3 * Fin, generator=g)
@@ -399,6 +403,15 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
                               W_res=None if W_res is None else W_res.to(cuda),
                               b_res=None if b_res is None else b_res.to(cuda), act=True, flags=fl)
         assert_close(out, y.float(), f"dense flags={fl}", rtol=2e-5, atol=2e-5)
+    sf = [v.float() for v in s]  # fp32 gates -> the pre-gated operand
+    Zg = torch.cat([Z[:, k * Fin:(k + 1) * Fin] * sf[k] for k in range(3)], 1)
+    for fl, pre in ((0, True), (PG_FLAG_DENSE_TILED, True), (PG_FLAG_DENSE_WS, True), (PG_FLAG_DENSE_WS, False)):
+        out = ops.layer_dense((Zg if pre else Z).to(cuda), dv, gate, rows=None if r is None else r.to(cuda),
+                              constant=None if const is None else const.to(cuda),
+                              res_x=None if xres is None else xres.to(cuda),
+                              W_res=None if W_res is None else W_res.to(cuda),
+                              b_res=None if b_res is None else b_res.to(cuda), act=True, flags=fl, pregated=pre)
+        assert_close(out, y.float(), f"dense flags={fl} pregated={pre}", rtol=2e-5, atol=2e-5)
 
 
 def _dense_case(M, Fin, Fout, proj, vec, rows, seed):
@@ -914,3 +927,31 @@ def test_forward_sees_in_place_parameter_writes(pkg, cuda, writer):
     fresh.load_state_dict(m.state_dict())
     lp2, emb2 = fresh(data)
     assert torch.equal(lp, lp2) and torch.equal(emb, emb2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,F", [("f1_fasta2", 32), ("f1_debruijn2", 128), ("f5_fasta3", 64)])
+@pytest.mark.parametrize("vec", [True, False])
+def test_spmm3_gated_bitexact(pkg, cuda, name, F, vec):
+    """pg_spmm3_gated_f32 == the gates applied to pg_spmm3_f32's output with the same fp32 products
+    ((c_all*c_dir)*c_in etc., then one rounding of s*Z), bit for bit."""
+    from protgram_directgcn_amd import ops
+    fx = load(name)
+    ei, ew = graph(fx)
+    N = int(fx["N"][0])
+    dei, dew = dev_graph(ei, ew, cuda)
+    g = pkg.graph.csr_from_coo(N, dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"])
+    if not g.shared:
+        pytest.skip("non-shared pattern")
+    gen = torch.Generator().manual_seed(F)
+    x = torch.randn(N, F, generator=gen).to(cuda)
+    shape = (N, 1) if vec else (1,)
+    prm = {k: (torch.rand(shape, generator=gen) + 0.5).to(cuda) for k in ("C_in", "C_out", "C_directed", "C_undirected",
+                                                                          "C_all")}
+    prm["W_main_in"] = torch.zeros(F, F, device=cuda)  # shape only
+    Zg = ops.spmm3_gated(g, x, prm, 0 if vec else 1)
+    Z = ops.spmm3(g, x)
+    cad = prm["C_all"] * prm["C_directed"]
+    s = [cad * prm["C_in"], cad * prm["C_out"], prm["C_all"] * prm["C_undirected"]]
+    ref = torch.cat([Z[:, k * F:(k + 1) * F] * s[k].view(-1, 1) for k in range(3)], 1)
+    assert torch.equal(Zg, ref)

@@ -76,3 +76,120 @@ def test_gpu_transitions_match_fixture(pkg, cuda, name, n, nseq, length, seed):
     assert got.num_nodes == int(fx["N"].item())
     assert np.array_equal(got.src.cpu().numpy(), fx["src"]) and np.array_equal(got.dst.cpu().numpy(), fx["dst"])
     assert np.array_equal(got.cnt.cpu().numpy(), fx["cnt"])
+
+
+# ----------------------------------------------------------------------------------------------------------
+# level files, next-node labels, feature pooling (CPU: tables from synth.fasta_edges, the builder restatement)
+# ----------------------------------------------------------------------------------------------------------
+
+def _level(pkg, n, seqs, alphabet=None):
+    from protgram_directgcn_amd import ngram
+    N, s, d, c, ordered = pkg.synth.fasta_edges(n, ngram.preprocess(seqs))
+    return ngram.transitions_from_table(n, s, d, c, ordered, alphabet), ordered
+
+
+def test_transitions_from_table_checks_order(pkg):
+    from protgram_directgcn_amd import ngram
+    with pytest.raises(ValueError):
+        ngram.transitions_from_table(2, [0], [1], [1.0], ["BA", "AB"])  # ids not in sorted string order
+    with pytest.raises(ValueError):
+        ngram.transitions_from_table(2, [0], [1], [1.0], ["AB", "ABC"])  # ragged n-grams
+
+
+def test_level_files_round_trip(pkg, tmp_path):
+    import pyarrow.parquet as pq
+    from protgram_directgcn_amd import ngram
+    t, ordered = _level(pkg, 3, _ragged_sequences())
+    mpath, epath = ngram.write_level(t, str(tmp_path))
+    m = pq.read_table(mpath).to_pandas()  # the builder's schema (data_builder.py:170-177, :268-286)
+    assert list(m.columns) == ["id", "ngram"] and m["ngram"].tolist() == ordered
+    assert m["id"].tolist() == list(range(len(ordered)))
+    e = pq.read_table(epath).to_pandas()
+    assert list(e.columns) == ["source", "target", "weight"] and str(e["weight"].dtype) == "int64"
+    back = ngram.read_level(str(tmp_path), 3)
+    assert back.num_nodes == t.num_nodes and back.node_strings() == ordered
+    assert torch.equal(back.src, t.src) and torch.equal(back.dst, t.dst) and torch.equal(back.cnt, t.cnt)
+    assert torch.equal(back.node_keys, t.node_keys)
+
+
+def test_read_level_written_like_the_builder(pkg, tmp_path):
+    """Files made the way data_builder.py makes them (pandas -> parquet, edges unsorted, int64 counts), a level
+    with no edge file (removed by the builder when empty), and endpoint validation."""
+    import pandas as pd
+    from protgram_directgcn_amd import ngram
+    mpath, epath = ngram.level_paths(str(tmp_path), 2)
+    pd.DataFrame({"id": [0, 1, 2], "ngram": [" A", "AB", "B "]}).to_parquet(mpath, index=False)
+    pd.DataFrame({"source": [1, 0, 1], "target": [2, 1, 0], "weight": [3, 1, 2]}).to_parquet(epath, index=False)
+    t = ngram.read_level(str(tmp_path), 2)
+    assert t.num_nodes == 3 and t.alphabet == " AB"
+    assert t.src.tolist() == [0, 1, 1] and t.dst.tolist() == [1, 0, 2] and t.cnt.tolist() == [1.0, 2.0, 3.0]
+    import os
+    os.remove(epath)
+    assert ngram.read_level(str(tmp_path), 2).src.numel() == 0
+    pd.DataFrame({"source": [0], "target": [7], "weight": [1]}).to_parquet(epath, index=False)
+    with pytest.raises(ValueError):
+        ngram.read_level(str(tmp_path), 2)
+
+
+def test_read_edge_parts_matches_groupby(pkg, tmp_path):
+    from oracle.ngram_cpu import aggregate_parts_ref
+    from protgram_directgcn_amd import ngram
+    rng = np.random.default_rng(3)
+    paths = []
+    for k in range(3):
+        p = tmp_path / f"part-{k}.txt"
+        lines = [f"{a} {b}" for a, b in rng.integers(0, 9, size=(200, 2))]
+        lines.insert(5, "garbage line here")
+        p.write_text("\n".join(lines) + "\n")
+        paths.append(str(p))
+    s, d, c = ngram.read_edge_parts(paths)
+    ref = aggregate_parts_ref(paths)
+    assert s.tolist() == ref["source"].tolist() and d.tolist() == ref["target"].tolist()
+    assert c.tolist() == ref["weight"].tolist()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_next_node_labels_vs_reference_loop(pkg, n):
+    from oracle.ngram_cpu import next_node_labels_ref
+    from protgram_directgcn_amd import ngram
+    t, _ = _level(pkg, n, _ragged_sequences())
+    ties = next_node_labels_ref(t.num_nodes, t.src.numpy(), t.dst.numpy(), t.cnt.numpy())
+    first, C = ngram.next_node_labels(t)
+    assert C == t.num_nodes
+    assert [int(v) for v in first] == [min(s) for s in ties]
+    rnd, _ = ngram.next_node_labels(t, "random", torch.Generator().manual_seed(0))
+    assert all(int(v) in s for v, s in zip(rnd, ties))
+    assert any(len(s) > 1 for s in ties)  # the case exercises ties
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_pool_features_vs_reference_loop(pkg, n):
+    from oracle.ngram_cpu import pool_features_ref
+    from protgram_directgcn_amd import ngram
+    seqs = _ragged_sequences()
+    prev, prev_strings = _level(pkg, n - 1, seqs)
+    cur, cur_strings = _level(pkg, n, seqs, alphabet=prev.alphabet)
+    emb = torch.randn(prev.num_nodes, 24, generator=torch.Generator().manual_seed(n))
+    got = ngram.pool_features(cur, prev, emb)
+    ref = pool_features_ref(cur_strings, prev_strings, emb.numpy())
+    assert torch.equal(got, torch.from_numpy(ref))
+    # the padded builder input makes some prefixes / suffixes absent at level n-1 (one-sided pooling)
+    with pytest.raises(ValueError):
+        ngram.pool_features(prev, cur, emb)
+
+
+@pytest.mark.gpu
+def test_labels_and_pooling_on_gpu(pkg, cuda):
+    from oracle.ngram_cpu import next_node_labels_ref, pool_features_ref
+    from protgram_directgcn_amd import ngram
+    seqs = _ragged_sequences()
+    prev = ngram.ngram_transitions(seqs, 2, device=cuda)
+    cur = ngram.ngram_transitions(seqs, 3, device=cuda)
+    assert cur.alphabet == prev.alphabet
+    lab, _ = ngram.next_node_labels(cur)
+    ties = next_node_labels_ref(cur.num_nodes, cur.src.cpu().numpy(), cur.dst.cpu().numpy(), cur.cnt.cpu().numpy())
+    assert [int(v) for v in lab.cpu()] == [min(s) for s in ties]
+    emb = torch.randn(prev.num_nodes, 32, generator=torch.Generator().manual_seed(1))
+    got = ngram.pool_features(cur, prev, emb.to(cuda))
+    ref = pool_features_ref(cur.node_strings(), prev.node_strings(), emb.numpy())
+    assert torch.equal(got.cpu(), torch.from_numpy(ref))

@@ -28,7 +28,9 @@ W1, b1 = torch.randn(64, 128, device=dev) * 0.1, torch.zeros(64, device=dev)
 W2, b2 = torch.randn(20, 64, device=dev) * 0.1, torch.zeros(20, device=dev)
 dY = torch.randn(N, 128, device=dev)
 for _ in range(reps):
-    Z = ops.spmm3(g, x)                 # spmm_win_kernel<32,1,4,0>: the default propagation
+    Zg = ops.spmm3_gated(g, x, prm, 0)  # spmm_win_kernel<32,1,4,0,256,true>: the inference (bench) propagation
+    ops.layer_dense(Zg, prm, 0, constant=layer.constant.detach(), res_x=x, act=True, pregated=True)  # dense_ws
+    Z = ops.spmm3(g, x)                 # spmm_win_kernel<32,1,4,0>: the training propagation
     ops.spmm3(gt, x)                    # spmm3_tiled_full_kernel (opt-in row tiles)
     ops.spmm3_t(g, Z)                   # spmm_win_kernel<..,2>: transposed propagation (backward)
     Y = ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)

@@ -9,10 +9,13 @@ import sys
 
 
 def classify(k):
-    m = re.search(r"spmm_win_kernel<\d+, \d+, \d+, (\d)>", k)
+    if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0, 256, true>", k):
+        return "spmm3_gated_window"
+    m = re.search(r"spmm_win_kernel<\d+, \d+, \d+, (\d)(, \d+, false)?>", k)
     if m:
         return {"0": "spmm3_window", "1": "spmm3_fusednorm_window", "2": "spmm3t_window"}.get(m.group(1), "spmm_window")
-    for key, short in (("spmm_vec_kernel", "spmm_bcast"), ("spmm3_tiled_full", "spmm_tiled_rows"),
+    for key, short in (("dense_ws_kernel", "dense_ws"), ("spmm_vec_kernel", "spmm_bcast"),
+                       ("spmm3_tiled_full", "spmm_tiled_rows"),
                        ("spmm3_tiled", "spmm_tiled"), ("dgrad_kernel", "dense_dgrad"), ("wgrad_kernel", "dense_wgrad"),
                        ("reduce_splits", "wgrad_reduce"), ("dense_kernel", "dense"), ("head_kernel", "head")):
         if key in k:

@@ -34,8 +34,10 @@ def main():
         kernels[k] = {"read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
                       "FETCH_SIZE_KiB": fetch.get(k), "WRITE_SIZE_KiB": write.get(k),
                       "dispatches": [nf.get(k, 0), nw.get(k, 0)]}
-    # the default propagation kernel: variant C (window), MODE 0 (three precomputed weights)
-    spmm = [k for k in kernels if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0>", k)]
+    # the bench's propagation kernel: variant C (window), MODE 0 (three precomputed weights), gated store
+    # (pg_spmm3_gated_f32, the inference path); the ungated training instance stays under "kernels"
+    spmm = [k for k in kernels if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0, 256, true>", k)]
+    spmm = spmm or [k for k in kernels if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0>", k)]
     res = {"workload": tag, "correction": "read = 2*FETCH_SIZE KiB (gfx950 half-count on 16B/lane reads); "
                                           "write = WRITE_SIZE KiB",
            "kernels": kernels}

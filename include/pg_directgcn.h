@@ -84,6 +84,9 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_WS (1u << 13)       /* dense kernel: W-stationary persistent variant (F_out = 128; default when pre-gated) */
 #define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
 #define PG_FLAG_DENSE_TILED (1u << 15)    /* dense kernel: never the W-stationary variant */
+#define PG_FLAG_DENSE_X3 (1u << 16)       /* dense kernel: W-stationary on bf16 MFMA with exact 3-way bf16 splits of both
+                                            operands (6 products, fp32-level accuracy); F_out = 128, K = 384 or 256,
+                                            no row map. Default for that shape unless another dense variant flag is set */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

@@ -49,7 +49,7 @@ struct DenseP {
     int64_t ldy;
     int remap;
     int pregated;  // A segments 0..2 already carry their gates (pg_spmm3_gated_f32): no scaling here
-    int dbg;  // dense_ws timing probes only (flags bits 20-22): 1 no epilogue memory, 2 no DMA, 4 no MFMA
+    int dbg;  // timing probes only (flags bits 20-23): 1 no epilogue memory, 2 no DMA, 4 no MFMA, 8 no conversion (x3)
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -554,6 +554,352 @@ __global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Split-bf16 W-stationary variant (PG_FLAG_DENSE_X3): fp32 accuracy on the bf16 matrix cores.
+// Every fp32 operand value v is split EXACTLY into three bf16 values v = v0 + v1 + v2 (round-to-nearest-even
+// at each step: v0 = bf16(v), v1 = bf16(v - v0), v2 = v - v0 - v1; both subtractions are exact in fp32 and v2
+// has at most 8 significant bits, so it is a bf16). A (the aggregates) and W (the packed weights) are split,
+// and the product is the sum of the six terms a_i w_j with i + j <= 2 (each an exact product, accumulated in
+// fp32 by v_mfma_f32_16x16x32_bf16); the dropped terms a1 w2, a2 w1, a2 w2 are below 2^-24 |a w|, i.e. the
+// size of one fp32 rounding. Six bf16 MFMAs cost 6 x 16 cycles per 16x16x32 step against 8 x 32 cycles for the
+// same step on v_mfma_f32_16x16x4_f32: 2.67x fewer matrix-core cycles.
+// Tile flow (32 rows, one 512-thread workgroup per CU, wave w owns output columns [16w, 16w+16) with its
+// three W splits in VGPRs): fp32 rows arrive by LDS-DMA in the swizzled image of dense_ws_kernel -> every
+// thread converts 3 of the tile's 1536 16-byte A units into the three bf16 images (gated here when the
+// operand is not pre-gated) -> the next tile's DMA is issued -> 12 MFMA steps -> accumulators parked in LDS
+// (aliasing the consumed bf16 images) -> the same epilogue as dense_ws_kernel.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// bf16 pair (RNE, v_cvt_pk_bf16_f32) and the two values it represents, back in fp32
+__device__ __forceinline__ uint32_t bf2(float a, float b, float& fa, float& fb) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
+    fa = __uint_as_float(u << 16);
+    fb = __uint_as_float(u & 0xffff0000u);
+    return u;
+}
+// exact three-way split of 8 fp32 values into three bf16x8 operands
+__device__ __forceinline__ void split8(const float (&v)[8], uint4& s0, uint4& s1, uint4& s2) {
+    uint32_t w0[4], w1[4], w2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float a = v[2 * i], b = v[2 * i + 1], fa, fb;
+        w0[i] = bf2(a, b, fa, fb);
+        a -= fa;
+        b -= fb;
+        w1[i] = bf2(a, b, fa, fb);
+        a -= fa;
+        b -= fb;
+        w2[i] = bf2(a, b, fa, fb);
+    }
+    s0 = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+    s1 = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+    s2 = make_uint4(w2[0], w2[1], w2[2], w2[3]);
+}
+__device__ __forceinline__ f32x4 mfma_bf(uint4 a, uint4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                   0, 0, 0);
+}
+
+// Workgroup barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (__syncthreads'
+// release fence also waits vmcnt(0), which would drain the next tile's LDS-DMA in flight). LDS-DMA landings are
+// waited for explicitly with s_waitcnt vmcnt before the barriers that publish them.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS reads of LDS-DMA targets through inline asm. hipcc cannot tell which LDS-DMA (counted in vmcnt) wrote the
+// bytes a ds_read touches, so before every such read it waits vmcnt(0) -- draining the DMA of the tiles in
+// flight. These reads carry their own lgkmcnt wait; the DMA they depend on is retired by the explicit counted
+// vmcnt waits + barriers of the tile loop.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void lds_ld4x2(const float* p0, const float* p1, float4& a, float4& b) {
+    f32x4 x, y;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(x), "=&v"(y)
+                 : "v"(lds_addr(p0)), "v"(lds_addr(p1))
+                 : "memory");
+    a = make_float4(x[0], x[1], x[2], x[3]);
+    b = make_float4(y[0], y[1], y[2], y[3]);
+}
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_stf(float* p, float v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st16(void* p, uint4 v) {
+    const u32x4_t w = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(p)), "v"(w) : "memory");
+}
+__device__ __forceinline__ void lds_ld4x4(const float* p0, const float* p1, const float* p2, const float* p3,
+                                          float4 (&o)[4]) {
+    f32x4 x0, x1, x2, x3;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(lds_addr(p0)), "v"(lds_addr(p1)), "v"(lds_addr(p2)), "v"(lds_addr(p3))
+        : "memory");
+    o[0] = make_float4(x0[0], x0[1], x0[2], x0[3]);
+    o[1] = make_float4(x1[0], x1[1], x1[2], x1[3]);
+    o[2] = make_float4(x2[0], x2[1], x2[2], x2[3]);
+    o[3] = make_float4(x3[0], x3[1], x3[2], x3[3]);
+}
+// gate inputs C_in, C_out, C_dir, C_und, C_all of row r: p points at Gi[gbuf][0][r], rows BMW floats apart
+template <int STRIDE_BYTES>
+__device__ __forceinline__ void lds_gates5(const float* p, float (&g)[5]) {
+    asm volatile(
+        "ds_read_b32 %0, %5\n\tds_read_b32 %1, %5 offset:%c6\n\tds_read_b32 %2, %5 offset:%c7\n\t"
+        "ds_read_b32 %3, %5 offset:%c8\n\tds_read_b32 %4, %5 offset:%c9\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(g[0]), "=&v"(g[1]), "=&v"(g[2]), "=&v"(g[3]), "=&v"(g[4])
+        : "v"(lds_addr(p)), "n"(STRIDE_BYTES), "n"(2 * STRIDE_BYTES), "n"(3 * STRIDE_BYTES), "n"(4 * STRIDE_BYTES)
+        : "memory");
+}
+
+// One LDS-DMA piece of 4 B per lane (lanes write consecutive dwords from wave-uniform base lds_base).
+__device__ __forceinline__ void glds4(const float* src, float* lds_base) {
+    __builtin_amdgcn_global_load_lds(src, lds_base, 4, 0, 0);
+}
+
+template <int F_IN, int KSEG, bool PRE>
+__global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
+    constexpr int K = F_IN * KSEG;
+    constexpr int CH = K / 4;     // fp32 16-B chunks per row
+    constexpr int NU = K / 8;     // bf16 16-B units per row (one MFMA operand of one lane for one k step)
+    constexpr int NS = K / 32;    // MFMA k steps
+    constexpr int BMW = 32;       // rows per tile (two 16x16 MFMA row blocks)
+    constexpr int NI = BMW * CH / 64 / 8;  // A-row LDS-DMA instructions per wave per tile
+    constexpr int NG = 3;                  // gate-input LDS-DMA instructions per tile (wave 0)
+    constexpr int NCR = 4;                 // constant + residual LDS-DMA instructions per wave per tile
+    constexpr int NCV = (BMW * NU + 511) / 512;  // units converted per thread per tile
+    static_assert(CH % 16 == 0 && NU % 16 == 0 && (BMW * CH) % 512 == 0 && BMW * 128 / 4 == 1024, "tile shape");
+    __shared__ __attribute__((aligned(16))) float Af[BMW * K];          // fp32 rows (LDS-DMA target)
+    __shared__ __attribute__((aligned(16))) uint4 As[3][BMW * NU];      // bf16 splits; Es aliases them
+    __shared__ __attribute__((aligned(16))) float Cs[BMW * 128];        // constant rows (LDS-DMA)
+    __shared__ __attribute__((aligned(16))) float Rs[BMW * 128];        // residual rows (LDS-DMA)
+    __shared__ __attribute__((aligned(16))) float Gi[2][8][BMW];        // gate inputs C_in..C_all (LDS-DMA)
+    __shared__ __attribute__((aligned(16))) float Bs[4][128];
+    constexpr int ELD = 128 + 4;
+    static_assert(BMW * ELD * 4 <= 3 * BMW * NU * 16, "epilogue tile must fit in the split images");
+    float* Es = reinterpret_cast<float*>(&As[0][0]);
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int lc = lane & 15, kg = lane >> 4;
+    const int col = 16 * wave + lc;
+    const int64_t T = (p.M + BMW - 1) / BMW;
+    Bs[tid >> 7][tid & 127] = (tid >> 7) < 3 || p.proj_res ? p.bsum[(tid >> 7) * p.F_out + (tid & 127)] : 0.f;
+    const int nb = gridDim.x, b = blockIdx.x;
+    int64_t ntl, lo, step;
+    if ((nb & 7) == 0 && nb >= 8) {  // XCD x takes a contiguous range of tiles
+        const int x = b & 7, i = b >> 3, bpx = nb >> 3;
+        const int64_t xlo = T * x / 8, xhi = T * (x + 1) / 8;
+        ntl = (xhi - xlo - i + bpx - 1) / bpx;
+        lo = xlo + i;
+        step = bpx;
+    } else {
+        ntl = (T - b + nb - 1) / nb;
+        lo = b;
+        step = nb;
+    }
+    if (ntl < 0) ntl = 0;
+
+    // W splits of this lane: k step s uses fp32 chunks 8s + kg and 8s + kg + 4 of column `col` (the same k
+    // permutation as the A units below)
+    uint4 w0[NS], w1[NS], w2[NS];
+    {
+        const float* src = p.Bp + (int64_t)col * K + 4 * kg;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const float4 x0 = ld4(src + 32 * s), x1 = ld4(src + 32 * s + 16);
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            split8(v, w0[s], w1[s], w2[s]);
+        }
+    }
+    const int ej = tid & 31, er = tid >> 5;  // epilogue: columns [4ej, 4ej+4) of rows er and er + 16
+    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
+    const bool id_res = p.res_x && !p.proj_res;
+
+    // Every operand of a tile -- A rows, gate inputs, constant and residual rows -- arrives by LDS-DMA, so no
+    // register-destination load is ever pending behind a DMA (the compiler would drain the DMA to wait for it),
+    // and every wave issues the same number of pieces per tile (absent operands fetch a valid dummy row), so
+    // the counted waits below are compile-time constants.
+    // Per-lane offsets are recomputed at every issue from an opaque copy of the lane id (32-bit offsets from
+    // per-tile uniform bases): hoisted out of the tile loop they would hold ~20 VGPRs next to the W splits.
+    auto issue_A = [&](int64_t tile, float* Ad) {
+        const int64_t m0 = tile * BMW;
+        const int rmax = (int)min((int64_t)(BMW - 1), p.M - 1 - m0);
+        const float* zb = p.Z + m0 * p.ldz;
+        const float* xb = KSEG > 3 ? p.res_x + m0 * p.ld_res : zb;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int idx = (wave * NI + i) * 64 + ln;
+            const int r = idx / CH, pos = idx - r * CH;
+            const int k = 4 * (pos ^ (r & 15));
+            const int rr = min(r, rmax);
+            const float* src = (KSEG == 3 || k < 3 * F_IN) ? zb + (rr * (int)p.ldz + k)
+                                                          : xb + (rr * (int)p.ld_res + (k - 3 * F_IN));
+            if (!(p.dbg & 2)) glds16(src, Ad + (wave * NI + i) * 256);
+        }
+    };
+    // gate inputs of the tile's rows (wave 0 only): piece i, lanes 0-31 / 32-63 fetch C_x for x = 2i / 2i + 1
+    auto issue_G = [&](int64_t tile, int gbuf) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int64_t r = p.gate_mode == PG_GATES_SCALAR ? 0 : min(tile * BMW + (ln & 31), p.M - 1);
+        // per-lane choice among uniform pointers by arithmetic (an indexed choice becomes a kernarg load, whose
+        // wait would drain the DMA in flight)
+        const float* c0 = p.C_in;
+        const float* c1 = p.C_out;
+        const float* c2 = p.C_dir;
+        const float* c3 = p.C_und;
+        const float* c4 = p.C_all;
+        asm volatile("" : "+s"(c0), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(c4));
+        const bool hi = ln >= 32;
+        glds4((hi ? c1 : c0) + r, &Gi[gbuf][0][0]);
+        glds4((hi ? c3 : c2) + r, &Gi[gbuf][2][0]);
+        glds4(c4 + r, &Gi[gbuf][4][0]);
+    };
+    auto issue_CR = [&](int64_t tile) {
+        const int64_t m0 = tile * BMW;
+        const int rmax = (int)min((int64_t)(BMW - 1), p.M - 1 - m0);
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // wave w: rows 4w .. 4w + 3
+            const int piece = 2 * wave + i;
+            const int rr = min(2 * piece + (ln >> 5), rmax);
+            const float* cb = has_const ? p.constant + m0 * p.ld_const + (rr * (int)p.ld_const) : p.Z + m0 * p.ldz;
+            const float* rb = id_res ? p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res) : p.Z + m0 * p.ldz;
+            glds16(cb + 4 * (ln & 31), Cs + piece * 256);
+            glds16(rb + 4 * (ln & 31), Rs + piece * 256);
+        }
+    };
+    // s_in = c_all c_dir c_in, s_out = c_all c_dir c_out, s_und = c_all c_und (protgram_directgcn.py:116-133)
+    auto gates = [&](int gbuf, int r, float& s0, float& s1, float& s2) {
+        float c[5];
+        lds_gates5<BMW * 4>(&Gi[gbuf][0][r], c);
+        const float ci = c[0], co = c[1], cd = c[2], cu = c[3], ca = c[4];
+        const float cad = ca * cd;
+        s0 = cad * ci;
+        s1 = cad * co;
+        s2 = ca * cu;
+    };
+    auto tile_of = [&](int64_t kt) { return lo + min(kt, ntl - 1) * step; };  // clamped: dummy tiles past the end
+
+    // fp32 -> three bf16 images of tile kt; thread j converts unit u of row r (rows vary fastest: conflict-free)
+    auto convert = [&](const float* Af, int gb) {
+#pragma unroll
+        for (int i = 0; i < NCV; ++i) {
+            if (p.dbg & 8) break;
+            const int j = tid + 512 * i;
+            if (BMW * NU % 512 != 0 && j >= BMW * NU) break;
+            const int r = j & (BMW - 1), u = j / BMW;
+            const int s = u >> 2, g = u & 3;
+            const int c0 = 8 * s + g;
+            float4 x0, x1;
+            lds_ld4x2(&Af[r * K + 4 * (c0 ^ (r & 15))], &Af[r * K + 4 * ((c0 + 4) ^ (r & 15))], x0, x1);
+            float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            if (!PRE) {
+                const int q = (32 * s) / F_IN;  // K segment of this step (F_IN % 32 == 0)
+                if (q < 3) {
+                    float sg[3];
+                    gates(gb, r, sg[0], sg[1], sg[2]);
+                    const float sc = sg[q];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] *= sc;
+                }
+            }
+            uint4 s0, s1, s2;
+            split8(v, s0, s1, s2);
+            const int pos = r * NU + (u ^ (r & 15));
+            lds_st16(&As[0][pos], s0);
+            lds_st16(&As[1][pos], s1);
+            lds_st16(&As[2][pos], s2);
+            __builtin_amdgcn_sched_barrier(0);  // one unit's temporaries live at a time (W holds 3 * K / 8 VGPRs)
+        }
+    };
+    // Tile loop (four barriers per tile): wait for tile kt's A rows and gates -> convert them into the bf16
+    // images -> issue CR(kt), G(kt+1), A(kt+1) (the fp32 buffer is free) -> MFMAs -> accumulators to Es (aliasing
+    // the consumed images) -> wait for CR(kt) only (G / A(kt+1) stay in flight) -> epilogue. Counted waits:
+    // every wave issues NCR + NI pieces per tile, wave 0 also NG.
+    constexpr int WAIT_W0 = NG + NI, WAIT_WN = NI;
+    if (ntl > 0) {
+        if (wave == 0) issue_G(tile_of(0), 0);
+        issue_A(tile_of(0), Af);
+    }
+    for (int64_t kt = 0; kt < ntl; ++kt) {
+        const int buf = (int)(kt & 1);
+        const int64_t m0 = (lo + kt * step) * BMW;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile kt have landed
+        lds_barrier();  // every wave's pieces have landed; the previous epilogue is done with Es / Cs / Rs
+        convert(Af, buf);
+        lds_barrier();  // bf16 images ready; Af is free
+        if (!(p.dbg & 32)) issue_CR(tile_of(kt));
+        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(kt + 1), buf ^ 1);
+        issue_A(tile_of(kt + 1), Af);
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        const int rb0 = lc * NU, rb1 = (16 + lc) * NU;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (p.dbg & 4) break;
+            const int up = (4 * s + kg) ^ lc;  // (16 + lc) & 15 == lc
+            const uint4 a00 = As[0][rb0 + up], a01 = As[1][rb0 + up], a02 = As[2][rb0 + up];
+            const uint4 a10 = As[0][rb1 + up], a11 = As[1][rb1 + up], a12 = As[2][rb1 + up];
+            acc[0] = mfma_bf(a02, w0[s], acc[0]);  // small terms first
+            acc[1] = mfma_bf(a12, w0[s], acc[1]);
+            acc[0] = mfma_bf(a01, w1[s], acc[0]);
+            acc[1] = mfma_bf(a11, w1[s], acc[1]);
+            acc[0] = mfma_bf(a00, w2[s], acc[0]);
+            acc[1] = mfma_bf(a10, w2[s], acc[1]);
+            acc[0] = mfma_bf(a01, w0[s], acc[0]);
+            acc[1] = mfma_bf(a11, w0[s], acc[1]);
+            acc[0] = mfma_bf(a00, w1[s], acc[0]);
+            acc[1] = mfma_bf(a10, w1[s], acc[1]);
+            acc[0] = mfma_bf(a00, w0[s], acc[0]);
+            acc[1] = mfma_bf(a10, w0[s], acc[1]);
+            __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every step's reads (VGPRs)
+        }
+        lds_barrier();  // every wave is done reading the bf16 images: Es may overwrite them
+#pragma unroll
+        for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lds_stf(&Es[(16 * sb + 4 * kg + i) * ELD + col], acc[sb][i]);
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W0) : "memory");  // CR(kt)
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_WN) : "memory");
+        lds_barrier();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int rl = er + 16 * h;
+            if (m0 + rl >= p.M || (p.dbg & 64)) continue;
+            float4 v, cv, rv, bb[4];
+            lds_ld4x2(&Cs[rl * 128 + 4 * ej], &Rs[rl * 128 + 4 * ej], cv, rv);
+            lds_ld4x4(&Es[rl * ELD + 4 * ej], &Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], bb);
+            v = bb[0];
+            const float4 b0 = bb[1], b1 = bb[2], b2 = bb[3];
+            float4 br;
+            lds_ld4x2(&Bs[3][4 * ej], &Bs[3][4 * ej], br, br);
+            if (!has_const) cv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!id_res) rv = make_float4(0.f, 0.f, 0.f, 0.f);
+            float s0, s1, s2;
+            gates(buf, rl, s0, s1, s2);
+            const float o[4] = {v.x, v.y, v.z, v.w}, C4[4] = {cv.x, cv.y, cv.z, cv.w}, R4[4] = {rv.x, rv.y, rv.z, rv.w};
+            const float B0[4] = {b0.x, b0.y, b0.z, b0.w}, B1[4] = {b1.x, b1.y, b1.z, b1.w},
+                        B2[4] = {b2.x, b2.y, b2.z, b2.w}, BR[4] = {br.x, br.y, br.z, br.w};
+            float y[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float qv = o[e] + (s0 * B0[e] + s1 * B1[e] + s2 * B2[e]) + BR[e] + C4[e] + R4[e];
+                y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
+            }
+            if (!(p.dbg & 1)) *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tile's DMA must land before the LDS is freed
+}
+
 __global__ __launch_bounds__(256) void pack_kernel(int F_in, int F_out, int K, const float* W0, const float* W1,
                                                    const float* W2, const float* Ws, const float* Wr,
                                                    const float* bm0, const float* bs0, const float* bm1,
@@ -647,7 +993,7 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.Y = a->Y;
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
-    p.dbg = (int)((flags >> 20) & 7);
+    p.dbg = (int)((flags >> 20) & 255);
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.vec_out = (a->F_out % 4 == 0) && (a->ldy % 4 == 0) && pg::aligned16(a->Y) &&
                 (!a->constant || (a->ld_const % 4 == 0 && pg::aligned16(a->constant))) &&
@@ -677,6 +1023,35 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     // W-stationary kernel: the default for pre-gated operands (measured 0.161 vs 0.176 ms for the tiled kernel at
     // B(20,4), F=128); PG_FLAG_DENSE_WS forces it, PG_FLAG_DENSE_TILED forbids it
     const bool want_ws = (flags & PG_FLAG_DENSE_WS) || (p.pregated && !(flags & PG_FLAG_DENSE_TILED));
+    const bool ws_shape_ok = a->F_out == 128 && vec && p.vec_out &&
+                             (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)));
+    // split-bf16 W-stationary kernel (fp32-accurate, bf16 matrix cores): K = 384 (F_in 128) or 256 (F_in 64 with
+    // the projected residual). The default wherever its shape applies (B(20,4), F=128: 0.140 ms ungated and 0.145
+    // pre-gated, against 0.188 tiled and 0.162 fp32 W-stationary; max |err| vs float64 1.4e-5 against 1.8e-5 for
+    // the fp32 MFMA kernels); any explicit tiling / W-stationary flag selects that kernel instead.
+    const uint32_t other_variant = PG_FLAG_DENSE_TILED | PG_FLAG_DENSE_WS | PG_FLAG_DENSE_BM64 | PG_FLAG_DENSE_BM128 |
+                                   PG_FLAG_DENSE_4WAVES | PG_FLAG_DENSE_PF2;
+    const bool want_x3 = (flags & PG_FLAG_DENSE_X3) || !(flags & other_variant);
+    if (want_x3 && !(flags & PG_FLAG_DENSE_TILED) && ws_shape_ok && a->ldz < (1 << 24) &&
+        a->rows == nullptr &&
+        (!a->res_x || a->ld_res < (1 << 24)) &&
+        ((a->F_in == 128 && !a->W_res) || (a->F_in == 64 && a->W_res))) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        const int64_t T = (a->M + 31) / 32;
+        const unsigned g = (unsigned)(T < ncu ? T : ncu);
+#define PG_X3(FI, KS)                                                                                     \
+    do {                                                                                                  \
+        if (p.pregated) hipLaunchKernelGGL((dense_x3_kernel<FI, KS, true>), dim3(g), dim3(512), 0, s, p); \
+        else hipLaunchKernelGGL((dense_x3_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
+    } while (0)
+        if (a->F_in == 128) PG_X3(128, 3);
+        else PG_X3(64, 4);
+#undef PG_X3
+        return pg::check_launch("pg_directgcn_dense_f32");
+    }
     if (want_ws && a->F_out == 128 && vec && p.vec_out && (a->F_in == 64 || (a->F_in == 128 && !a->W_res)) &&
         (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)))) {
         int dev = 0, ncu = 256;

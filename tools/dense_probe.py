@@ -51,9 +51,23 @@ def run(fl):
 
 
 ref = run(0).clone()
+# float64 reference on the first R rows: error of every variant against the exact formula
+R = 8192
+s64 = {k: prm[k][:R].double().view(-1, 1) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all")}
+sg = [s64["C_all"] * s64["C_directed"] * s64["C_in"], s64["C_all"] * s64["C_directed"] * s64["C_out"],
+      s64["C_all"] * s64["C_undirected"]]
+Wd = [(prm[a] + prm["W_shared"]).double() for a in ("W_main_in", "W_main_out", "W_undirected")]
+bd = [(prm[a] + prm[b]).double() for a, b in (("b_main_in", "b_dir_shared_in"), ("b_main_out", "b_dir_shared_out"),
+                                              ("b_undirected", "b_undirected_shared"))]
+Zd = Z[:R].double()
+y64 = sum(sg[q] * (Zd[:, q * F:(q + 1) * F] @ Wd[q].t() + bd[q]) for q in range(3)) + const[:R].double() + x[:R].double()
+y64 = torch.nn.functional.leaky_relu(y64, 0.01)
 for k, fl in variants.items():
-    d = (run(fl) - ref).abs().max().item()
-    print(f"{k:10s} max|d| vs default {d:.3e}")
+    out = run(fl)
+    d = (out - ref).abs().max().item()
+    e = (out[:R].double() - y64).abs()
+    print(f"{k:10s} max|d| vs default {d:.3e}   vs float64: max abs {e.max().item():.3e}, "
+          f"max abs/(1+|y|) {(e / (1 + y64.abs())).max().item():.3e}, mean abs {e.mean().item():.3e}")
 
 
 def timeit(fn, reps=20):

@@ -8,8 +8,11 @@ identity residuals), C=20 classes, eval mode, fp32. One step = one full model fo
 decoder, log_softmax, L2-normalised embeddings), inputs resident in HBM.
   edges/s = 3 * nnz * L / t_step   (each adjacency entry counted once per layer)
 
---gpus N (torchrun, one process per GPU): node-range partition of the same graph across the N ranks,
-RCCL all-gather of the layer-1 output rows between the layers ("scaling": "strong": total work fixed).
+--gpus N (torchrun, one process per GPU; "scaling": "strong": total work fixed). Default --partition halo:
+rank p owns a contiguous chunk of the graph's locality schedule and recomputes the 1-hop halo of its rows
+in layer 1 (shard.halo_partition): no collective on the data path, since the graph fits every GPU's HBM
+(the north star's RCCL halo exchange is for graphs that outgrow it). --partition exchange: node-range rows
+and an RCCL all-gather of the layer-1 output rows between the layers (shard.sharded_forward).
 Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
 over ranks is reported. Rank 0 prints one JSON line.
 
@@ -48,6 +51,9 @@ def parse():
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
     ap.add_argument("--chunks", type=int, default=4, help="N>1: layer-boundary all-gather in this many pieces, "
                     "overlapped with the compute (1 = one exchange after the layer)")
+    ap.add_argument("--partition", choices=("halo", "exchange"), default="halo",
+                    help="N>1: 'halo' = each rank recomputes the (L-1)-hop halo of its rows (no collective on the data "
+                    "path; the graph fits every GPU's HBM); 'exchange' = node-range rows + RCCL all-gather per layer")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     return ap.parse_args()
@@ -112,10 +118,18 @@ def main():
         x = x.to(torch.bfloat16)  # inputs resident in HBM in the compute dtype
     data = pkg.Data(x=x, graph=g)
 
-    part = shard.partition(g, rank, world) if world > 1 else None
+    part = hp = None
+    if world > 1 and args.partition == "halo":
+        hp = shard.halo_partition(g, rank, world, L)
+        halo_in = shard.halo_inputs(model, hp, x)  # this rank's resident inputs in its node order (setup)
+        log(f"[bench] halo partition: rank 0 computes {hp.layer_rows} rows per layer (N={N})")
+    elif world > 1:
+        part = shard.partition(g, rank, world)
 
     def step():
         with torch.no_grad():
+            if hp is not None:
+                return shard.halo_forward(model, hp, halo_in)
             if part is None:
                 return model(data)
             return shard.sharded_forward(model, part, x, chunks=args.chunks)
@@ -147,7 +161,10 @@ def main():
     value = edges_per_step * args.steps / elapsed
 
     # roofline of the dominant kernel (SURVEY §8d B_agg, per launch = this rank's rows)
-    if part is None:
+    if hp is not None:  # launches alternate over the layers' row prefixes: their mean B_agg
+        el = 2 if args.bf16 else 4
+        launch_bytes = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in hp.graphs) // len(hp.graphs)
+    elif part is None:
         launch_bytes = g.algorithmic_bytes(Fd, elem=2 if args.bf16 else 4)
         launch_nnz, launch_rows = g.nnz, N
     else:
@@ -169,7 +186,7 @@ def main():
     elif args.fused_norm:
         kname = "pg_spmm3_fusednorm_f32"
     else:  # single-GPU inference gates the aggregates in the propagation's store (same gathers, same B_agg)
-        kname = "pg_spmm3_gated_f32" if (world == 1 and ops.PREGATED_INFERENCE) else "pg_spmm3_f32"
+        kname = "pg_spmm3_gated_f32" if ((world == 1 or hp is not None) and ops.PREGATED_INFERENCE) else "pg_spmm3_f32"
     roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -194,8 +211,10 @@ def main():
                        "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
                        "layers": L, "layer_dims": dims, "classes": C,
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
-                       "parallelism": f"node_range_x{world}" if world > 1 else "single",
-                       "exchange_chunks": args.chunks if world > 1 else None},
+                       "parallelism": ("single" if world == 1 else f"halo_recompute_x{world}" if hp is not None
+                                       else f"node_range_x{world}"),
+                       "exchange_chunks": args.chunks if part is not None else None,
+                       "halo_rows_rank0": hp.layer_rows if hp is not None else None},
             "nodes_per_sec": round(N * L * args.steps / elapsed, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,

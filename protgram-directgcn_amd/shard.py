@@ -331,3 +331,156 @@ def gather_node_params(model, part: NodeRangePartition, group=None):
             full = all_gather_rows(flat[part.r0:part.r1].contiguous(), part, group)
             flat.copy_(full)
 
+
+
+# ------------------------------------------------------------------------------------------------
+# Halo-recompute partition: communication-free multi-GPU forward for graphs that fit one GPU's HBM
+# ------------------------------------------------------------------------------------------------
+# The north star asks for the RCCL halo exchange "only when the n-gram graph outgrows one GPU's 288 GB HBM".
+# Below that size every rank can hold the whole graph and input, so instead of exchanging layer outputs it
+# recomputes the (L-1)-hop halo of its rows:
+#   S_p            = rows owned by rank p (outputs of the last layer)
+#   need[L-1]      = S_p,   need[i] = need[i+1] u N(need[i+1])     (N = CSR neighbours)
+#   layer i (0-based) computes rows need[i]; layer 0 gathers from the replicated input.
+# The rank relabels the nodes so that every need[i] is a prefix of its own node order (S_p first, then the
+# 1-hop halo, then the 2-hop halo, ..., then the rest), which makes each layer a plain single-GPU launch over
+# the first |need[i]| rows: the same kernels (pg_spmm3_gated_f32 + the W-stationary dense kernel + the head)
+# with contiguous per-node parameters, no row map and no collective on the data path. Each row's entries keep
+# their CSR order, so every output row is bit-identical to the single-GPU forward.
+# Ownership: contiguous chunks of the graph's locality schedule (CSRGraph.row_order) -- for an n-gram graph the
+# schedule groups rows sharing the middle (n-2)-gram, whose neighbourhoods overlap, so the halo of a chunk is
+# ~(1-(1-1/P)^3) N rows at L=2 instead of the ~N of a node-id range (whose neighbours span every id).
+@dataclass
+class HaloPartition:
+    rank: int
+    world: int
+    n: int
+    perm: torch.Tensor          # int64 [n]: local id -> global id (owned rows first)
+    layer_rows: List[int]       # rows computed by layer i (prefix lengths, non-increasing); last = owned
+    graphs: List[CSRGraph]      # layer i: CSR of local rows [0, layer_rows[i]) with local column ids
+    cache: dict = field(default_factory=dict)
+
+    @property
+    def owned(self) -> int:
+        return self.layer_rows[-1]
+
+    @property
+    def global_rows(self) -> torch.Tensor:
+        """Global ids of the rows this rank outputs (in its output order)."""
+        return self.perm[:self.owned]
+
+
+def halo_owner(g: CSRGraph, world: int) -> torch.Tensor:
+    """Node -> rank: balanced contiguous chunks of the locality schedule (node ids when there is none)."""
+    n = g.n_rows
+    dev = g.rowptr.device
+    pos = torch.arange(n, dtype=torch.int64, device=dev)
+    owner = torch.empty(n, dtype=torch.int64, device=dev)
+    if g.row_order is not None:
+        owner[g.row_order.to(torch.int64)] = pos * world // max(n, 1)
+    else:
+        owner.copy_(pos * world // max(n, 1))
+    return owner
+
+
+def halo_partition(g: CSRGraph, rank: int, world: int, layers: int,
+                   owner: Optional[torch.Tensor] = None) -> HaloPartition:
+    """This rank's halo-recompute layout for an L-layer forward (see the section comment)."""
+    if not g.shared:
+        raise NotImplementedError("halo partition needs the shared-pattern CSR")
+    if layers < 1:
+        raise ValueError("layers must be >= 1")
+    n = g.n_rows
+    dev = g.rowptr.device
+    if owner is None:
+        owner = halo_owner(g, world)
+    owner = owner.to(device=dev, dtype=torch.int64)
+    if owner.numel() != n or (n and (int(owner.min()) < 0 or int(owner.max()) >= world)):
+        raise ValueError("owner must assign every node a rank in [0, world)")
+    rp = g.rowptr
+    counts = rp[1:] - rp[:-1]
+    row_of = torch.repeat_interleave(torch.arange(n, device=dev), counts)
+    col = g.edges3[:, 0].to(torch.int64)
+    # depth: 0 = owned, k = needed first by layer L-1-k, L = never computed (input gather source only)
+    depth = torch.full((n,), layers, dtype=torch.int64, device=dev)
+    need = owner == rank
+    depth[need] = 0
+    for k in range(1, layers):
+        nb = torch.zeros(n, dtype=torch.bool, device=dev)
+        nb[col[need[row_of]]] = True
+        new = nb & ~need
+        depth[new] = k
+        need = need | nb
+    perm = torch.sort(depth, stable=True).indices  # by depth, node id order inside a depth
+    inv = torch.empty(n, dtype=torch.int64, device=dev)
+    inv[perm] = torch.arange(n, dtype=torch.int64, device=dev)
+    dcount = torch.bincount(depth, minlength=layers + 1).cpu()
+    cum = torch.cumsum(dcount, 0).tolist()
+    layer_rows = [int(cum[layers - 1 - i]) for i in range(layers)]  # layer i computes depths <= L-1-i
+    # CSR of the largest prefix (layer 0) in local ids; later layers are zero-copy prefixes of it
+    R0 = layer_rows[0]
+    old = perm[:R0]
+    cnt = counts[old]
+    lrp = torch.zeros(R0 + 1, dtype=torch.int64, device=dev)
+    lrp[1:] = torch.cumsum(cnt, 0)
+    tot = int(lrp[-1])
+    src = (torch.arange(tot, dtype=torch.int64, device=dev) - torch.repeat_interleave(lrp[:-1], cnt)
+           + torch.repeat_interleave(rp[old], cnt))
+    e = g.edges3[src].clone()
+    e[:, 0] = inv[e[:, 0].to(torch.int64)].to(torch.int32)
+    gorder = None
+    if g.row_order is not None:  # the global schedule's relative order, restricted to each prefix
+        gorder = inv[g.row_order.to(torch.int64)]
+    graphs = []
+    for i, R in enumerate(layer_rows):
+        order = None
+        if gorder is not None:
+            order = gorder[gorder < R].to(torch.int32)
+        e1 = int(lrp[R])
+        graphs.append(CSRGraph(n_rows=R, shared=True, rowptr=lrp[:R + 1], edges3=e[:e1], symmetric=False, nnz=e1,
+                               row_order=order, n_cols=n if i == 0 else layer_rows[i - 1]))
+    return HaloPartition(rank, world, n, perm, layer_rows, graphs)
+
+
+@torch.no_grad()
+def halo_inputs(model, hp: HaloPartition, x_full: torch.Tensor):
+    """The rank's resident inputs in its own node order: the input features (all n rows: layer 0 gathers from
+    anywhere) and, per layer, the per-node parameters (gates, constant) of the rows it computes. Built once per
+    parameter set, like the parameter shards of the exchange path; rebuild after the parameters change."""
+    x_p = x_full.index_select(0, hp.perm.to(x_full.device))
+    layers = []
+    for conv, R in zip(model.convs, hp.layer_rows):
+        prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+        if conv.use_vector_coeffs:
+            rows = hp.perm[:R].to(conv.constant.device)
+            for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+                prm[k] = prm[k].index_select(0, rows).contiguous()
+            const = conv.constant.detach().index_select(0, rows).contiguous()
+        else:
+            const = None
+        layers.append((prm, const))
+    return x_p, layers
+
+
+@torch.no_grad()
+def halo_forward(model, hp: HaloPartition, inputs) -> tuple:
+    """ProtGramDirectGCN.forward (eval) for this rank's rows, without communication. Returns (log_probs, emb)
+    for the rows hp.global_rows, in that order."""
+    x_p, layers = inputs
+    if len(layers) != len(model.convs) or len(hp.graphs) != len(model.convs):
+        raise ValueError("halo partition / inputs were built for a different number of layers")
+    h = model._apply_pe(x_p)
+    if model.compute_dtype == torch.bfloat16:
+        h = h.to(torch.bfloat16)
+    for conv, res, g, (prm, const) in zip(model.convs, model.res_projs, hp.graphs, layers):
+        gate_mode = 0 if conv.use_vector_coeffs else 1
+        W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
+        R = g.n_rows
+        Z = ops.spmm3_gated(g, h, prm, gate_mode)
+        if Z is not None:
+            h = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=h[:R], W_res=W_res, b_res=b_res, act=True,
+                                pregated=True)
+        else:  # bf16 mode: gates applied in the dense kernel
+            Z = ops.spmm3(g, h)
+            h = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=h[:R], W_res=W_res, b_res=b_res, act=True)
+    return model.head(h)

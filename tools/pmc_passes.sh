@@ -14,7 +14,7 @@ TCC_HIT TCC_MISS TCC_REQ TCC_BUSY
 TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ TCP_PENDING_STALL_CYCLES TCP_TCR_TCP_STALL_CYCLES
 TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TD_TD_BUSY
 TA_DATA_STALLED_BY_TC_CYCLES
-SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
+SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
 P
 fi
 i=0

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/round
 mkdir -p $O
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/bench -o b --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/bench -o b --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/bench.log 2>&1
 echo "bench trace done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/fetch -o k --output-format csv -- python3 $R/tools/kprobe.py 3 > $O/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/write -o k --output-format csv -- python3 $R/tools/kprobe.py 3 > $O/write.log 2>&1

@@ -86,7 +86,9 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_TILED (1u << 15)    /* dense kernel: never the W-stationary variant */
 #define PG_FLAG_DENSE_X3 (1u << 16)       /* dense kernel: W-stationary on bf16 MFMA with exact 3-way bf16 splits of both
                                             operands (6 products, fp32-level accuracy); F_out = 128, K = 384 or 256,
-                                            no row map. Default for that shape unless another dense variant flag is set */
+                                            no row map. Default for that shape unless another dense variant flag is set;
+                                            F_in = 128 runs the 16-row software-pipelined kernel */
+#define PG_FLAG_DENSE_X3_32 (1u << 17)    /* split-bf16 dense kernel: the 32-row unpipelined tile loop instead */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

@@ -355,6 +355,15 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_base) {
     __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 0);
 }
 
+// epilogue sum of the W-stationary kernels with every rounding step explicit (no contraction choices left to the
+// compiler), so the 32-row and the pipelined 16-row split-bf16 kernels round identically:
+//   acc + (s0 b0 + s1 b1 + s2 b2) + b_res + constant + residual
+__device__ __forceinline__ float epi_sum(float acc, float s0, float s1, float s2, float b0, float b1, float b2,
+                                         float br, float cst, float res) {
+    const float gb = __fmaf_rn(s2, b2, __fmaf_rn(s1, b1, __fmul_rn(s0, b0)));
+    return __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(acc, gb), br), cst), res);
+}
+
 template <int F_IN, int KSEG, bool PRE>
 __global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
     constexpr int K = F_IN * KSEG;
@@ -537,7 +546,7 @@ __global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
             float y[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float qv = o[e] + (s0 * B0[e] + s1 * B1[e] + s2 * B2[e]) + BR[e] + C4[e] + R4[e];
+                const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                 y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
             }
             *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
@@ -645,6 +654,24 @@ __device__ __forceinline__ void lds_ld4x4(const float* p0, const float* p1, cons
     o[2] = make_float4(x2[0], x2[1], x2[2], x2[3]);
     o[3] = make_float4(x3[0], x3[1], x3[2], x3[3]);
 }
+// epilogue operands in one LDS round trip: three float4 (constant, residual, accumulators) and the five gate
+// inputs of the row (g points at Gi[slot][0][r], rows STRIDE_BYTES apart)
+template <int STRIDE_BYTES>
+__device__ __forceinline__ void lds_epi(const float* p0, const float* p1, const float* p2, const float* g, float4& a,
+                                        float4& b, float4& c, float (&gv)[5]) {
+    f32x4 x0, x1, x2;
+    asm volatile(
+        "ds_read_b128 %0, %8\n\tds_read_b128 %1, %9\n\tds_read_b128 %2, %10\n\t"
+        "ds_read_b32 %3, %11\n\tds_read_b32 %4, %11 offset:%c12\n\tds_read_b32 %5, %11 offset:%c13\n\t"
+        "ds_read_b32 %6, %11 offset:%c14\n\tds_read_b32 %7, %11 offset:%c15\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(gv[0]), "=&v"(gv[1]), "=&v"(gv[2]), "=&v"(gv[3]), "=&v"(gv[4])
+        : "v"(lds_addr(p0)), "v"(lds_addr(p1)), "v"(lds_addr(p2)), "v"(lds_addr(g)), "n"(STRIDE_BYTES),
+          "n"(2 * STRIDE_BYTES), "n"(3 * STRIDE_BYTES), "n"(4 * STRIDE_BYTES)
+        : "memory");
+    a = make_float4(x0[0], x0[1], x0[2], x0[3]);
+    b = make_float4(x1[0], x1[1], x1[2], x1[3]);
+    c = make_float4(x2[0], x2[1], x2[2], x2[3]);
+}
 // gate inputs C_in, C_out, C_dir, C_und, C_all of row r: p points at Gi[gbuf][0][r], rows BMW floats apart
 template <int STRIDE_BYTES>
 __device__ __forceinline__ void lds_gates5(const float* p, float (&g)[5]) {
@@ -661,7 +688,13 @@ __device__ __forceinline__ void glds4(const float* src, float* lds_base) {
     __builtin_amdgcn_global_load_lds(src, lds_base, 4, 0, 0);
 }
 
-template <int F_IN, int KSEG, bool PRE>
+// bf16 split image layout of one 32-row tile: [k step s][row r][4 units], unit g of row r stored at slot
+// g ^ ((-(r >> 2)) & 3). A wave's MFMA read of step s (lane: row lc or 16 + lc, unit kg) is then one per-lane
+// address plus s * 2 KB, and every ds_read_b128 lane group (0-3,12-15,20-27 | 4-11,16-19,28-31 | ...) and every
+// 8-lane ds_write_b128 group of the split pass hits 16 distinct 16-B bank slots.
+__device__ __forceinline__ int a_unit(int s, int r, int g) { return 128 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
+
+template <int F_IN, int KSEG, bool PRE, bool STAMP = false>
 __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
     constexpr int K = F_IN * KSEG;
     constexpr int CH = K / 4;     // fp32 16-B chunks per row
@@ -809,12 +842,12 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
                     gates(gb, r, sg[0], sg[1], sg[2]);
                     const float sc = sg[q];
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] *= sc;
+                    for (int e = 0; e < 8; ++e) v[e] = __fmul_rn(v[e], sc);  // rounded: never contracted into the split
                 }
             }
             uint4 s0, s1, s2;
             split8(v, s0, s1, s2);
-            const int pos = r * NU + (u ^ (r & 15));
+            const int pos = a_unit(s, r, g);
             lds_st16(&As[0][pos], s0);
             lds_st16(&As[1][pos], s1);
             lds_st16(&As[2][pos], s2);
@@ -830,24 +863,56 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
         if (wave == 0) issue_G(tile_of(0), 0);
         issue_A(tile_of(0), Af);
     }
+    bool prev_full = false;  // the previous epilogue issued exactly 2 Y stores per thread
+    // timing probe (STAMP instance, flags bit 27): per-phase s_memtime cycle sums of wave 0, written to Y row b
+    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
+    auto stamp = [&](int i) {
+        if constexpr (STAMP) {
+            uint64_t t;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (i >= 0) tsum[i] += t - tprev;
+            tprev = t;
+        }
+    };
+    stamp(-1);
     for (int64_t kt = 0; kt < ntl; ++kt) {
         const int buf = (int)(kt & 1);
         const int64_t m0 = (lo + kt * step) * BMW;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile kt have landed
+        // this wave's pieces of tile kt have landed; the previous tile's two Y stores per thread (the youngest
+        // vector-memory operations: vmcnt counts loads, stores and LDS-DMA in issue order) may stay in flight
+        if (prev_full) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();  // every wave's pieces have landed; the previous epilogue is done with Es / Cs / Rs
+        stamp(0);
+        if (!(p.dbg & 32)) issue_CR(tile_of(kt));  // Cs / Rs are free: their DMA overlaps the split pass
+        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(kt + 1), buf ^ 1);  // Gi[buf ^ 1]: tile kt-1 is done
         convert(Af, buf);
         lds_barrier();  // bf16 images ready; Af is free
-        if (!(p.dbg & 32)) issue_CR(tile_of(kt));
-        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(kt + 1), buf ^ 1);
+        stamp(1);
         issue_A(tile_of(kt + 1), Af);
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-        const int rb0 = lc * NU, rb1 = (16 + lc) * NU;
+        // operands of k step s for row blocks 0 / 1 sit at one per-lane address + s * 2 KB (+ 1 KB for block 1):
+        // immediate ds_read offsets, and step s + 1's six operands are read while step s's MFMAs run
+        const uint4* ab0 = &As[0][a_unit(0, lc, kg)];
+        const uint4* ab2 = &As[2][a_unit(0, lc, kg)];
+        uint4 op[2][6];
+        auto ld_ops = [&](int s, uint4 (&o)[6]) {
+            o[0] = ab0[128 * s];
+            o[1] = ab0[BMW * NU + 128 * s];
+            o[2] = ab2[128 * s];
+            o[3] = ab0[64 + 128 * s];
+            o[4] = ab0[BMW * NU + 64 + 128 * s];
+            o[5] = ab2[64 + 128 * s];
+        };
+        if (!(p.dbg & 4)) ld_ops(0, op[0]);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if (p.dbg & 4) break;
-            const int up = (4 * s + kg) ^ lc;  // (16 + lc) & 15 == lc
-            const uint4 a00 = As[0][rb0 + up], a01 = As[1][rb0 + up], a02 = As[2][rb0 + up];
-            const uint4 a10 = As[0][rb1 + up], a11 = As[1][rb1 + up], a12 = As[2][rb1 + up];
+            if (s + 1 < NS) ld_ops(s + 1, op[(s + 1) & 1]);
+            const uint4 a00 = op[s & 1][0], a01 = op[s & 1][1], a02 = op[s & 1][2];
+            const uint4 a10 = op[s & 1][3], a11 = op[s & 1][4], a12 = op[s & 1][5];
             acc[0] = mfma_bf(a02, w0[s], acc[0]);  // small terms first
             acc[1] = mfma_bf(a12, w0[s], acc[1]);
             acc[0] = mfma_bf(a01, w1[s], acc[0]);
@@ -860,16 +925,19 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             acc[1] = mfma_bf(a10, w1[s], acc[1]);
             acc[0] = mfma_bf(a00, w0[s], acc[0]);
             acc[1] = mfma_bf(a10, w0[s], acc[1]);
-            __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting every step's reads (VGPRs)
+            __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting later steps' reads (VGPRs)
         }
+        stamp(2);
         lds_barrier();  // every wave is done reading the bf16 images: Es may overwrite them
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) lds_stf(&Es[(16 * sb + 4 * kg + i) * ELD + col], acc[sb][i]);
+        stamp(3);
         if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W0) : "memory");  // CR(kt)
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_WN) : "memory");
         lds_barrier();
+        stamp(4);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int rl = er + 16 * h;
@@ -891,13 +959,296 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             float y[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float qv = o[e] + (s0 * B0[e] + s1 * B1[e] + s2 * B2[e]) + BR[e] + C4[e] + R4[e];
+                const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                 y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
             }
             if (!(p.dbg & 1)) *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
         }
+        prev_full = m0 + BMW <= p.M && !(p.dbg & (1 | 64));
+        stamp(5);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tile's DMA must land before the LDS is freed
+    if constexpr (STAMP) {
+        if (tid < 6 && (int64_t)b < p.M) p.Y[(int64_t)b * p.ldy + tid] = (float)tsum[tid];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Software-pipelined split-bf16 W-stationary kernel (the default for F_in = 128, F_out = 128, no row map).
+// Same arithmetic as dense_x3_kernel (identical products and accumulation order per output element, hence
+// bit-identical results), on 16-row tiles so that every stage has its own LDS buffer:
+//   tile t:  LDS-DMA A(t) -> Af[t&1] (iteration t-2) | split(t) -> As[t&1] (iteration t-1) | MFMA(t) (iteration t)
+//            | accumulators -> Es, constant/residual rows -> Cs/Rs (top of t+1) | epilogue(t) (end of t+1)
+// Iteration i: [wait A(i+1)] B1 [Es <- acc(i-1); DMA CR(i-1), A(i+2), G(i+2)] then waves 0-3 run MFMA(i) and then
+// split(i+1) while waves 4-7 (the other wave of each SIMD) run split(i+1) and then MFMA(i), so each SIMD's
+// matrix pipe and its VALU/LDS split work overlap; [wait CR(i-1)] B2 [epilogue(i-1)]. Two barriers per tile.
+// LDS: Af 2 x 24 KB, As 2 x 36 KB, Cs/Rs 16 KB, Es 8.3 KB, gate inputs 4 x 512 B, bias sums 2 KB.
+__device__ __forceinline__ int a_unit16(int s, int r, int g) { return 64 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
+
+template <bool PRE, bool STAMP = false>
+__global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
+    constexpr int F_IN = 128, K = 384;
+    constexpr int CH = K / 4;    // fp32 16-B chunks per row
+    constexpr int NU = K / 8;    // bf16 16-B units per row
+    constexpr int NS = K / 32;   // MFMA k steps
+    constexpr int BM = 16;       // rows per tile
+    constexpr int NI = BM * CH / 64 / 8;  // A-row LDS-DMA pieces per wave per tile (3)
+    constexpr int NG = 2;                 // gate-input pieces per tile (wave 0)
+    constexpr int NCR = 2;                // constant + residual pieces per wave per tile
+    constexpr int ELD = 128 + 4;
+    static_assert(BM * CH % 512 == 0 && NI == 3, "tile shape");
+    __shared__ __attribute__((aligned(16))) float Af0[BM * K];  // separate objects: the compiler tells the DMA
+    __shared__ __attribute__((aligned(16))) float Af1[BM * K];  // target apart from the buffer being read
+    __shared__ __attribute__((aligned(16))) uint4 As[2][3][BM * NU];
+    __shared__ __attribute__((aligned(16))) float Cs[BM * 128];
+    __shared__ __attribute__((aligned(16))) float Rs[BM * 128];
+    __shared__ __attribute__((aligned(16))) float Es[BM * ELD];
+    __shared__ __attribute__((aligned(16))) float Gi[4][8][BM];
+    __shared__ __attribute__((aligned(16))) float Bs[4][128];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int lc = lane & 15, kg = lane >> 4;
+    const int col = 16 * wave + lc;
+    const bool mfma_first = wave < 4;  // waves w and w + 4 share a SIMD
+    const int64_t T = (p.M + BM - 1) / BM;
+    Bs[tid >> 7][tid & 127] = (tid >> 7) < 3 || p.proj_res ? p.bsum[(tid >> 7) * p.F_out + (tid & 127)] : 0.f;
+    const int nb = gridDim.x, b = blockIdx.x;
+    int64_t ntl, lo, step;
+    if ((nb & 7) == 0 && nb >= 8) {  // XCD x takes a contiguous range of tiles
+        const int x = b & 7, i = b >> 3, bpx = nb >> 3;
+        const int64_t xlo = T * x / 8, xhi = T * (x + 1) / 8;
+        ntl = (xhi - xlo - i + bpx - 1) / bpx;
+        lo = xlo + i;
+        step = bpx;
+    } else {
+        ntl = (T - b + nb - 1) / nb;
+        lo = b;
+        step = nb;
+    }
+    if (ntl < 0) ntl = 0;
+
+    uint4 w0[NS], w1[NS], w2[NS];
+    {
+        const float* src = p.Bp + (int64_t)col * K + 4 * kg;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const float4 x0 = ld4(src + 32 * s), x1 = ld4(src + 32 * s + 16);
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            split8(v, w0[s], w1[s], w2[s]);
+        }
+    }
+    const int ej = tid & 31, er = tid >> 5;  // epilogue: columns [4ej, 4ej+4) of row er
+    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
+    const bool id_res = p.res_x && !p.proj_res;
+    auto tile_of = [&](int64_t kt) { return lo + max((int64_t)0, min(kt, ntl - 1)) * step; };
+
+    auto issue_A = [&](int64_t tile, float* Ad) {
+        const int64_t m0 = tile * BM;
+        const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
+        const float* zb = p.Z + m0 * p.ldz;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int idx = (wave * NI + i) * 64 + ln;
+            const int r = idx / CH, pos = idx - r * CH;
+            const int k = 4 * (pos ^ r);
+            const int rr = min(r, rmax);
+            if (!(p.dbg & 2)) glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
+        }
+    };
+    // gate inputs of a tile (wave 0): piece 0 = C_in | C_out | C_dir | C_und (16 lanes each), piece 1 = C_all
+    auto issue_G = [&](int64_t tile, int slot) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int64_t r = p.gate_mode == PG_GATES_SCALAR ? 0 : min(tile * BM + (ln & 15), p.M - 1);
+        const float* c0 = p.C_in;
+        const float* c1 = p.C_out;
+        const float* c2 = p.C_dir;
+        const float* c3 = p.C_und;
+        const float* c4 = p.C_all;
+        asm volatile("" : "+s"(c0), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(c4));
+        const int q = ln >> 4;
+        const float* cq = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
+        glds4(cq + r, &Gi[slot][0][0]);
+        glds4(c4 + r, &Gi[slot][4][0]);
+    };
+    auto issue_CR = [&](int64_t tile) {  // wave w: rows 2w, 2w + 1
+        const int64_t m0 = tile * BM;
+        const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int rr = min(2 * wave + (ln >> 5), rmax);
+        const float* cb = has_const ? p.constant + m0 * p.ld_const + (rr * (int)p.ld_const) : p.Z + m0 * p.ldz;
+        const float* rb = id_res ? p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res) : p.Z + m0 * p.ldz;
+        glds16(cb + 4 * (ln & 31), Cs + wave * 256);
+        glds16(rb + 4 * (ln & 31), Rs + wave * 256);
+    };
+    auto gates = [&](int slot, int r, float& s0, float& s1, float& s2) {
+        float c[5];
+        lds_gates5<BM * 4>(&Gi[slot][0][r], c);
+        const float cad = c[4] * c[2];
+        s0 = cad * c[0];
+        s1 = cad * c[1];
+        s2 = c[4] * c[3];
+    };
+    // fp32 tile -> three bf16 images; thread j converts units j and j + 512 (row j & 15, unit j >> 4): waves 0-3
+    // two units, waves 4-7 one; all of a thread's fp32 reads in one LDS round trip
+    auto split_tile = [&](const float* Af, int ab, int gslot) {
+        if (p.dbg & 8) return;
+        const int r = tid & 15;
+        const bool two = tid + 512 < BM * NU;  // wave-uniform
+        const int u0 = tid >> 4, u1 = u0 + 32;
+        const int c00 = 8 * (u0 >> 2) + (u0 & 3), c10 = 8 * (u1 >> 2) + (u1 & 3);
+        float4 x[4];
+        if (two) lds_ld4x4(&Af[r * K + 4 * (c00 ^ r)], &Af[r * K + 4 * ((c00 + 4) ^ r)], &Af[r * K + 4 * (c10 ^ r)],
+                           &Af[r * K + 4 * ((c10 + 4) ^ r)], x);
+        else lds_ld4x2(&Af[r * K + 4 * (c00 ^ r)], &Af[r * K + 4 * ((c00 + 4) ^ r)], x[0], x[1]);
+        float sg[3] = {1.f, 1.f, 1.f};
+        if (!PRE) gates(gslot, r, sg[0], sg[1], sg[2]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i == 1 && !two) break;
+            const int u = i ? u1 : u0;
+            const int s = u >> 2, g = u & 3;
+            const float4 a = x[2 * i], c = x[2 * i + 1];
+            float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+            if (!PRE) {
+                const float sc = sg[(32 * s) / F_IN];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = __fmul_rn(v[e], sc);  // rounded: never contracted into the split
+            }
+            uint4 s0, s1, s2;
+            split8(v, s0, s1, s2);
+            const int pos = a_unit16(s, r, g);
+            lds_st16(&As[ab][0][pos], s0);
+            lds_st16(&As[ab][1][pos], s1);
+            lds_st16(&As[ab][2][pos], s2);
+        }
+    };
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    auto mfma_tile = [&](int ab) {
+        const uint4* a0 = &As[ab][0][a_unit16(0, lc, kg)];
+        const uint4* a1 = &As[ab][1][a_unit16(0, lc, kg)];
+        const uint4* a2 = &As[ab][2][a_unit16(0, lc, kg)];
+        uint4 op[2][3];
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (p.dbg & 4) return;
+        op[0][0] = a0[0];
+        op[0][1] = a1[0];
+        op[0][2] = a2[0];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s + 1 < NS) {
+                op[(s + 1) & 1][0] = a0[64 * (s + 1)];
+                op[(s + 1) & 1][1] = a1[64 * (s + 1)];
+                op[(s + 1) & 1][2] = a2[64 * (s + 1)];
+            }
+            const uint4 x0 = op[s & 1][0], x1 = op[s & 1][1], x2 = op[s & 1][2];
+            acc = mfma_bf(x2, w0[s], acc);  // small terms first (the order of dense_x3_kernel)
+            acc = mfma_bf(x1, w1[s], acc);
+            acc = mfma_bf(x0, w2[s], acc);
+            acc = mfma_bf(x1, w0[s], acc);
+            acc = mfma_bf(x0, w1[s], acc);
+            acc = mfma_bf(x0, w0[s], acc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
+    auto stamp = [&](int i) {
+        if constexpr (STAMP) {
+            uint64_t t;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (i >= 0) tsum[i] += t - tprev;
+            tprev = t;
+        }
+    };
+
+    // prologue: A(0), G(0) and A(1), G(1) in flight; split(0) once A(0) has landed
+    if (ntl > 0) {
+        issue_A(tile_of(0), Af0);
+        if (wave == 0) issue_G(tile_of(0), 0);
+        issue_A(tile_of(1), Af1);
+        if (wave == 0) issue_G(tile_of(1), 1);
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + NG) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        lds_barrier();
+        split_tile(Af0, 0, 0);
+    }
+    // bias sums of this thread's epilogue columns (Bs was published by the prologue barrier)
+    float4 bq[4];
+    if (ntl > 0) lds_ld4x4(&Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], &Bs[3][4 * ej], bq);
+    stamp(-1);
+    bool y_pending = false;  // the previous epilogue left exactly one Y store per thread in flight
+    for (int64_t i = 0; i <= ntl && ntl > 0; ++i) {
+        const int ab = (int)(i & 1);
+        if (y_pending) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // A(i+1), G(i+1) have landed
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();  // B1: A(i+1) and split(i) visible; epilogue(i-2) done with Es / Cs / Rs; As[ab ^ 1] free
+        stamp(0);
+        if (i >= 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lds_stf(&Es[(4 * kg + e) * ELD + col], acc[e]);
+        }
+        if (!(p.dbg & 32)) issue_CR(tile_of(i - 1));
+        issue_A(tile_of(i + 2), ab ? Af1 : Af0);  // Af[(i + 2) & 1] = Af[ab]: split(i) is done with it
+        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
+        stamp(1);
+        const bool do_mfma = i < ntl, do_split = i + 1 < ntl;
+        if (mfma_first) {
+            if (do_mfma) mfma_tile(ab);
+            stamp(2);
+            if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
+            stamp(3);
+        } else {
+            if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
+            stamp(3);
+            if (do_mfma) mfma_tile(ab);
+            stamp(2);
+        }
+        // CR(i-1) has landed: younger are A(i+2) (+ G(i+2) on wave 0)
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + NG) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        lds_barrier();  // B2: Es and Cs / Rs visible
+        stamp(4);
+        y_pending = false;
+        if (i >= 1) {
+            const int64_t m0 = tile_of(i - 1) * BM;
+            const int gs = (int)((i - 1) & 3);
+            if (m0 + er < p.M && !(p.dbg & 64)) {
+                float4 cv, rv, ov;
+                float c[5];
+                lds_epi<BM * 4>(&Cs[er * 128 + 4 * ej], &Rs[er * 128 + 4 * ej], &Es[er * ELD + 4 * ej], &Gi[gs][0][er],
+                                cv, rv, ov, c);
+                if (!has_const) cv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!id_res) rv = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float cad = c[4] * c[2];
+                const float s0 = cad * c[0], s1 = cad * c[1], s2 = c[4] * c[3];
+                const float o[4] = {ov.x, ov.y, ov.z, ov.w}, C4[4] = {cv.x, cv.y, cv.z, cv.w},
+                            R4[4] = {rv.x, rv.y, rv.z, rv.w};
+                const float B0[4] = {bq[0].x, bq[0].y, bq[0].z, bq[0].w}, B1[4] = {bq[1].x, bq[1].y, bq[1].z, bq[1].w},
+                            B2[4] = {bq[2].x, bq[2].y, bq[2].z, bq[2].w}, BR[4] = {bq[3].x, bq[3].y, bq[3].z, bq[3].w};
+                float y[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
+                    y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
+                }
+                if (!(p.dbg & 1)) {
+                    *reinterpret_cast<float4*>(p.Y + (m0 + er) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
+                    y_pending = true;
+                }
+            }
+        }
+        stamp(5);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles' DMA must land before the LDS is freed
+    if constexpr (STAMP) {
+        if (tid < 6 && (int64_t)b < p.M) p.Y[(int64_t)b * p.ldy + tid] = (float)tsum[tid];
+    }
 }
 
 __global__ __launch_bounds__(256) void pack_kernel(int F_in, int F_out, int K, const float* W0, const float* W1,
@@ -1047,7 +1398,22 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         if (p.pregated) hipLaunchKernelGGL((dense_x3_kernel<FI, KS, true>), dim3(g), dim3(512), 0, s, p); \
         else hipLaunchKernelGGL((dense_x3_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
     } while (0)
-        if (a->F_in == 128) PG_X3(128, 3);
+        const bool pipelined = a->F_in == 128 && !(flags & PG_FLAG_DENSE_X3_32);
+        if (pipelined) {  // 16-row software-pipelined kernel
+            const int64_t T16 = (a->M + 15) / 16;
+            const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
+            const bool st = (p.dbg & 128) != 0;  // timing probe: phase cycle sums in Y rows 0..grid-1
+            if (p.pregated) {
+                if (st) hipLaunchKernelGGL((dense_x3p_kernel<true, true>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<true>), dim3(g16), dim3(512), 0, s, p);
+            } else {
+                if (st) hipLaunchKernelGGL((dense_x3p_kernel<false, true>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<false>), dim3(g16), dim3(512), 0, s, p);
+            }
+        } else if (p.dbg & 128) {
+            if (a->F_in == 128 && p.pregated) hipLaunchKernelGGL((dense_x3_kernel<128, 3, true, true>), dim3(g), dim3(512), 0, s, p);
+            else if (a->F_in == 128) hipLaunchKernelGGL((dense_x3_kernel<128, 3, false, true>), dim3(g), dim3(512), 0, s, p);
+        } else if (a->F_in == 128) PG_X3(128, 3);
         else PG_X3(64, 4);
 #undef PG_X3
         return pg::check_launch("pg_directgcn_dense_f32");

@@ -31,7 +31,7 @@ Z = torch.randn(N, 3 * F, device=dev)
 x = torch.randn(N, F, device=dev)
 Y = torch.empty(N, F, device=dev)
 
-variants = {"default": 0, "pre": 1 << 14, "ws": 1 << 13, "ws_pre": (1 << 13) | (1 << 14)}
+variants = {"default": 0, "pre": 1 << 14, "x3_32": 1 << 17, "x3_32_pre": (1 << 17) | (1 << 14)}
 for a in sys.argv[3:]:
     k, v = a.split("=")
     variants[k] = int(v, 0)
@@ -89,3 +89,16 @@ for _ in range(4):
         res[k].append(timeit(lambda: run(fl)))
 for k, v in res.items():
     print(f"{k:10s} " + " ".join(f"{t:.4f}" for t in v) + f"   min {min(v):.4f}")
+
+# phase stamps of the pipelined split-bf16 kernel (flags bit 27 = dbg 128): per-block wave-0 cycle sums in Y rows
+for pre in (False, True):
+    fl = (1 << 27) | (PRE if pre else 0)
+    run(fl)
+    torch.cuda.synchronize()
+    st = Y[:256, :6].double()
+    names = ["top wait+B1", "Es + DMA issue", "MFMA(i)", "split(i+1)", "CR wait+B2", "epilogue(i-1)"]
+    tot = st.sum(1)
+    print(f"stamps ({'pre-gated' if pre else 'ungated'}): cycles per block, mean over blocks (total {tot.mean():.0f}, "
+          f"max {tot.max():.0f})")
+    for i, nm in enumerate(names):
+        print(f"   {nm:28s} {st[:, i].mean():10.0f}  ({100 * st[:, i].mean() / tot.mean():5.1f} %)")

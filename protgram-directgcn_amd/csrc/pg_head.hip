@@ -13,6 +13,7 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int HB = 64;  // rows per block
 
@@ -202,6 +203,136 @@ __global__ __launch_bounds__(256) void head_kernel(HeadP p) {
     }
 }
 
+// The model's own head shape (F = 128 -> H = 64 -> C <= 32; ProtGramDirectGCN's decoder is F -> F/2 -> C):
+// one 32-row tile per 256-thread block, no persistent loop, small enough (LDS 30 KB, <= 128 VGPRs) for four
+// blocks per CU, so one block's loads, MFMAs and softmax overlap the others'. Decoder products on
+// v_mfma_f32_16x16x4f32 with a K permutation (lane (i, q) supplies k = 4q + 16m + t for t = 0..3 as four
+// consecutive MFMAs, the weights in the same order); both weight fragments stay in registers for the block.
+// Rows of the LDS tiles are padded by 8 floats: the (row, 4q) float4 reads of one ds_read_b128 lane group hit 16
+// distinct 16-B bank slots.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void head_f128_kernel(HeadP p) {
+    constexpr int BM = 32, F = 128, H = 64, CP = 32;
+    constexpr int HLD = F + 8, ZLD = H + 8, LLD = CP + 1;
+    __shared__ __attribute__((aligned(16))) float Hs[BM * HLD];
+    __shared__ __attribute__((aligned(16))) float Zs[BM * ZLD];
+    __shared__ __attribute__((aligned(16))) float Ls[BM * LLD];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int li = lane & 15, q = lane >> 4;
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    // 1. h tile (4 float4 per thread, 512-B rows), then the weight fragments while the loads are in flight
+    float4 hv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int r = (tid >> 5) + 8 * k;
+        const int64_t m = m0 + r;
+        if (m >= p.M) {
+            hv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if (p.hb) {  // bf16 mode: widened exactly
+            const uint2 w = *reinterpret_cast<const uint2*>(p.hb + m * p.ldh + 4 * (tid & 31));
+            hv[k] = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+        } else {
+            hv[k] = ld4(p.h + m * p.ldh + 4 * (tid & 31));
+        }
+    }
+    float4 w1f[8], w2f[4];
+    {
+        const float* w1row = p.W1 + (int64_t)(16 * wave + li) * F + 4 * q;  // decoder 1: wave w owns hidden 16w..16w+15
+#pragma unroll
+        for (int m = 0; m < 8; ++m) w1f[m] = ld4(w1row + 16 * m);
+        const int c = 16 * (wave >> 1) + li;  // decoder 2: row block wave & 1, classes 16 (wave >> 1) + li
+        const bool cok = c < p.C;
+        const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * H + 4 * q;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) w2f[m] = cok ? ld4(w2row + 16 * m) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float b1v = p.b1[16 * wave + li];
+    const int c2 = 16 * (wave >> 1) + li;
+    const float b2v = c2 < p.C ? p.b2[c2] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(&Hs[((tid >> 5) + 8 * k) * HLD + 4 * (tid & 31)]) = hv[k];
+    __syncthreads();
+    // 2. embeddings: 8 threads per row, 16 columns each
+    {
+        const int r = tid >> 3, part = tid & 7;
+        float4 v[4];
+        float ss = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[k] = ld4(&Hs[r * HLD + 16 * part + 4 * k]);
+            ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+        }
+        ss += __shfl_xor(ss, 1, 8);
+        ss += __shfl_xor(ss, 2, 8);
+        ss += __shfl_xor(ss, 4, 8);
+        const int64_t m = m0 + r;
+        if (m < p.M) {
+            const float inv = 1.0f / (sqrtf(ss) + p.eps);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *reinterpret_cast<float4*>(p.emb + m * p.lde + 16 * part + 4 * k) =
+                    make_float4(v[k].x * inv, v[k].y * inv, v[k].z * inv, v[k].w * inv);
+        }
+    }
+    // 3. z = relu(h W1^T + b1): wave w computes hidden columns 16w..16w+15 for both 16-row blocks
+    {
+        f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb) {
+                const float4 a = ld4(&Hs[(16 * rb + li) * HLD + 4 * q + 16 * m]);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w1f[m].x, acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w1f[m].y, acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w1f[m].z, acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w1f[m].w, acc[rb], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float z = acc[rb][i] + b1v;
+                Zs[(16 * rb + 4 * q + i) * ZLD + 16 * wave + li] = z > 0.f ? z : 0.f;
+            }
+    }
+    __syncthreads();
+    // 4. logits = z W2^T + b2: wave w -> rows 16 (w & 1).., classes 16 (w >> 1)..
+    {
+        const int rb = wave & 1;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 a = ld4(&Zs[(16 * rb + li) * ZLD + 4 * q + 16 * m]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, w2f[m].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, w2f[m].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, w2f[m].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, w2f[m].w, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ls[(16 * rb + 4 * q + i) * LLD + c2] = acc[i] + b2v;
+    }
+    __syncthreads();
+    // 5. log_softmax (max-shifted, as torch): 8 threads per row
+    {
+        const int r = tid >> 3, part = tid & 7;
+        const int64_t m = m0 + r;
+        float mx = -INFINITY;
+        for (int c = part; c < p.C; c += 8) mx = fmaxf(mx, Ls[r * LLD + c]);
+        mx = fmaxf(mx, __shfl_xor(mx, 1, 8));
+        mx = fmaxf(mx, __shfl_xor(mx, 2, 8));
+        mx = fmaxf(mx, __shfl_xor(mx, 4, 8));
+        float se = 0.f;
+        for (int c = part; c < p.C; c += 8) se += expf(Ls[r * LLD + c] - mx);
+        se += __shfl_xor(se, 1, 8);
+        se += __shfl_xor(se, 2, 8);
+        se += __shfl_xor(se, 4, 8);
+        const float lse = mx + logf(se);
+        if (m < p.M)
+            for (int c = part; c < p.C; c += 8) p.logp[m * p.ldp + c] = Ls[r * LLD + c] - lse;
+    }
+}
+
 // General shapes: one wave per row, VALU.
 __global__ __launch_bounds__(256) void head_generic_kernel(HeadP p) {
     extern __shared__ float sm[];  // per wave: F + H + C floats
@@ -268,7 +399,9 @@ int head_launch(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, cons
         const int64_t per_block = (ntiles + slots - 1) / slots;
         return (unsigned)((ntiles + per_block - 1) / per_block);
     };
-    if (vec && F <= 128 && H <= 64 && C <= 32) {
+    if (vec && F == 128 && H == 64 && C <= 32 && ldh % 4 == 0 && lde % 4 == 0) {
+        hipLaunchKernelGGL(head_f128_kernel, dim3((unsigned)((M + 31) / 32)), dim3(256), 0, s, p);
+    } else if (vec && F <= 128 && H <= 64 && C <= 32) {
         hipLaunchKernelGGL((head_kernel<128, 64, 32>), dim3(grid_of(2)), dim3(256), 0, s, p);
     } else if (vec && F <= 256 && H <= 128 && C <= 64) {
         hipLaunchKernelGGL((head_kernel<256, 128, 64>), dim3(grid_of(1)), dim3(256), 0, s, p);

@@ -279,7 +279,8 @@ def test_full_size_4gram_layer_vs_oracle(pkg, cuda, n, F):
         assert torch.equal(Z[:, j * F:(j + 1) * F].cpu(), oc.propagate(ei, x, w[j])), j
 
 
-@pytest.mark.parametrize("F,H,C", [(128, 64, 20), (32, 16, 5), (256, 128, 50), (16, 8, 400), (34, 17, 3), (12, 6, 1)])
+@pytest.mark.parametrize("F,H,C", [(128, 64, 20), (128, 64, 32), (128, 64, 1), (32, 16, 5), (256, 128, 50), (16, 8, 400),
+                                   (34, 17, 3), (12, 6, 1)])
 def test_head_kernel_vs_torch(pkg, cuda, F, H, C):
     import torch.nn.functional as Fn
     from protgram_directgcn_amd import ops

@@ -14,6 +14,10 @@ def classify(k):
     m = re.search(r"spmm_win_kernel<\d+, \d+, \d+, (\d)(, \d+, false)?>", k)
     if m:
         return {"0": "spmm3_window", "1": "spmm3_fusednorm_window", "2": "spmm3t_window"}.get(m.group(1), "spmm_window")
+    if "dense_x3p_kernel" in k:  # pipelined split-bf16 dense kernel: <pregated, stamp>
+        return "dense_x3p_pregated" if "<true" in k else "dense_x3p"
+    if "head_f128_kernel" in k:
+        return "head_f128"
     if "dense_x3_kernel" in k:  # split-bf16 W-stationary dense kernel: <F_IN, KSEG, pregated>
         return "dense_x3_pregated" if k.rstrip(")").find("true>") >= 0 else "dense_x3"
     for key, short in (("dense_ws_kernel", "dense_ws"), ("spmm_vec_kernel", "spmm_bcast"),

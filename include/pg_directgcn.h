@@ -207,7 +207,10 @@ int64_t pg_directgcn_packed_floats(int64_t F_in, int64_t F_out, int has_res_proj
 int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stream);
 
 /* The contraction + epilogue. Reads weights/biases from `packed` (the W_* / b_* fields of args are not
- * read); W_res != NULL selects the projected residual. */
+ * read); W_res != NULL selects the projected residual. packed == NULL: the kernel forms W_q + W_shared and the
+ * bias sums from the W_* / b_* fields itself (the pack kernel's fp32 adds, so the result is identical), which
+ * only the pipelined split-bf16 kernel does (F_in = F_out = 128, no W_res, no row map, 16-B aligned weights);
+ * any other case returns PG_ERR_UNSUPPORTED without launching (callers then pack and call again). */
 int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
 
 /* pg_spmm3_f32 with the DirectGCN gates applied at the store: Z_q[i] = s_q(i) * (A_q X)[i], s_in = c_all*c_dir*c_in,

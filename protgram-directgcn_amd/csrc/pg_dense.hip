@@ -50,6 +50,11 @@ struct DenseP {
     int remap;
     int pregated;  // A segments 0..2 already carry their gates (pg_spmm3_gated_f32): no scaling here
     int dbg;  // timing probes only (flags bits 20-23): 1 no epilogue memory, 2 no DMA, 4 no MFMA, 8 no conversion (x3)
+    // unpacked weights (packed == NULL; the pipelined split-bf16 kernel forms W_q + W_shared and the bias sums
+    // itself, with the pack kernel's fp32 adds)
+    int rawW;
+    const float *Wq0, *Wq1, *Wq2, *Wsh;
+    const float *bm0, *bs0, *bm1, *bs1, *bm2, *bs2;
 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -1012,7 +1017,16 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     const int col = 16 * wave + lc;
     const bool mfma_first = wave < 4;  // waves w and w + 4 share a SIMD
     const int64_t T = (p.M + BM - 1) / BM;
-    Bs[tid >> 7][tid & 127] = (tid >> 7) < 3 || p.proj_res ? p.bsum[(tid >> 7) * p.F_out + (tid & 127)] : 0.f;
+    {
+        const int q = tid >> 7, n = tid & 127;
+        float bv = 0.f;
+        if (p.rawW) {
+            if (q < 3) bv = q == 0 ? p.bm0[n] + p.bs0[n] : q == 1 ? p.bm1[n] + p.bs1[n] : p.bm2[n] + p.bs2[n];
+        } else if (q < 3 || p.proj_res) {
+            bv = p.bsum[q * p.F_out + n];
+        }
+        Bs[q][n] = bv;
+    }
     const int nb = gridDim.x, b = blockIdx.x;
     int64_t ntl, lo, step;
     if ((nb & 7) == 0 && nb >= 8) {  // XCD x takes a contiguous range of tiles
@@ -1029,7 +1043,17 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     if (ntl < 0) ntl = 0;
 
     uint4 w0[NS], w1[NS], w2[NS];
-    {
+    if (p.rawW) {  // W_q + W_shared, k step s lies in segment q = s / 4
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const float* wq = s < 4 ? p.Wq0 : s < 8 ? p.Wq1 : p.Wq2;
+            const int64_t o = (int64_t)col * F_IN + (32 * s) % F_IN + 4 * kg;
+            const float4 a0 = ld4(wq + o), a1 = ld4(wq + o + 16), h0 = ld4(p.Wsh + o), h1 = ld4(p.Wsh + o + 16);
+            const float v[8] = {a0.x + h0.x, a0.y + h0.y, a0.z + h0.z, a0.w + h0.w,
+                                a1.x + h1.x, a1.y + h1.y, a1.z + h1.z, a1.w + h1.w};
+            split8(v, w0[s], w1[s], w2[s]);
+        }
+    } else {
         const float* src = p.Bp + (int64_t)col * K + 4 * kg;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
@@ -1306,7 +1330,7 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* a, float* packed, void* stream)
 }
 
 int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32_t flags, void* stream) {
-    PG_REQUIRE(a != nullptr && packed != nullptr, "null args");
+    PG_REQUIRE(a != nullptr, "null args");
     PG_REQUIRE(a->M >= 0 && a->F_in > 0 && a->F_out > 0 && a->F_in < (1 << 20) && a->F_out < (1 << 20),
                "bad shape M=%lld F_in=%lld F_out=%lld", (long long)a->M, (long long)a->F_in, (long long)a->F_out);
     if (a->M == 0) return PG_OK;
@@ -1326,7 +1350,24 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.Z = a->Z;
     p.ldz = a->ldz;
     p.Bp = packed;
-    p.bsum = packed + (int64_t)p.F_out * p.K;
+    p.bsum = packed ? packed + (int64_t)p.F_out * p.K : nullptr;
+    if (!packed) {  // unpacked weights: only the pipelined split-bf16 kernel takes them (checked at dispatch)
+        PG_REQUIRE(a->W_main_in && a->W_main_out && a->W_undirected && a->W_shared && a->b_main_in &&
+                       a->b_dir_shared_in && a->b_main_out && a->b_dir_shared_out && a->b_undirected &&
+                       a->b_undirected_shared,
+                   "packed == NULL needs the raw weights and biases in the args");
+        p.rawW = 1;
+        p.Wq0 = a->W_main_in;
+        p.Wq1 = a->W_main_out;
+        p.Wq2 = a->W_undirected;
+        p.Wsh = a->W_shared;
+        p.bm0 = a->b_main_in;
+        p.bs0 = a->b_dir_shared_in;
+        p.bm1 = a->b_main_out;
+        p.bs1 = a->b_dir_shared_out;
+        p.bm2 = a->b_undirected;
+        p.bs2 = a->b_undirected_shared;
+    }
     p.gate_mode = a->gate_mode;
     p.C_in = a->C_in;
     p.C_out = a->C_out;
@@ -1399,6 +1440,10 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         else hipLaunchKernelGGL((dense_x3_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
     } while (0)
         const bool pipelined = a->F_in == 128 && !(flags & PG_FLAG_DENSE_X3_32);
+        if (p.rawW && !(pipelined && pg::aligned16(a->W_main_in) && pg::aligned16(a->W_main_out) &&
+                        pg::aligned16(a->W_undirected) && pg::aligned16(a->W_shared)))
+            return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
+                                                     "split-bf16 kernel (F_in = F_out = 128, no row map)");
         if (pipelined) {  // 16-row software-pipelined kernel
             const int64_t T16 = (a->M + 15) / 16;
             const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
@@ -1418,6 +1463,9 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
 #undef PG_X3
         return pg::check_launch("pg_directgcn_dense_f32");
     }
+    if (p.rawW)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
+                                                 "split-bf16 kernel (F_in = F_out = 128, no row map)");
     if (want_ws && a->F_out == 128 && vec && p.vec_out && (a->F_in == 64 || (a->F_in == 128 && !a->W_res)) &&
         (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)))) {
         int dev = 0, ncu = 256;

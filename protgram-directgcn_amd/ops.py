@@ -342,7 +342,6 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
             out.copy_(Y)
             return out
         return Y
-    packed = pack_weights(prm, W_res, b_res)
     M = Z.size(0)
     F_out = prm["W_main_in"].size(0)
     if out is not None:
@@ -356,6 +355,18 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     fl = default_flags() if flags is None else flags
     if pregated:
         fl |= _lib.PG_FLAG_DENSE_PREGATED
+    if W_res is None and rows is None:
+        # unpacked weights: the pipelined split-bf16 kernel sums W_q + W_shared itself (no pack launch); any other
+        # kernel choice answers PG_ERR_UNSUPPORTED without launching, and the packed call below runs instead
+        raw = [_f32c(prm[k].detach()) for k in _PACK_KEYS]
+        (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
+         a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared) = [_p(t) for t in raw]
+        rc = lib.pg_directgcn_dense_f32(ctypes.byref(a), None, fl, _stream(Z))
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_directgcn_dense_f32")
+            del keep, raw
+            return Y
+    packed = pack_weights(prm, W_res, b_res)
     check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
     del keep
     return Y

@@ -275,20 +275,14 @@ __global__ __launch_bounds__(256) void spmm_vec_kernel(SpmmParams p) {
 // group's own LDS window, and read them back as LDS broadcasts: the TD only carries the feature gathers.
 // A window is private to one row group inside one wave, so wave-local ordering (the compiler's
 // lgkmcnt waits + a wave barrier) replaces block barriers. Same accumulation order: still bit-exact.
-template <int LPR, int NV, int U, int MODE, int NT = 256, bool GATED = false>
-__global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
+template <int LPR, int NV, int U, int MODE, bool GATED>
+__device__ __forceinline__ void win_row(const SpmmParams& p, int64_t pos, bool live,
+                                        typename Rec<MODE>::T* __restrict__ mywin) {
     using R = typename Rec<MODE>::T;
-    constexpr int RPB = NT / LPR;
     constexpr int NACC = Shape<MODE>::NACC;
     constexpr int NSLICE = Shape<MODE>::NSLICE;
     constexpr int WIN = LPR;  // records per window (one per lane)
-    __shared__ __attribute__((aligned(16))) R win[RPB][WIN];
-
-    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
-    const int grp = threadIdx.x / LPR;
     const int t = threadIdx.x % LPR;
-    const int64_t pos = lb * RPB + grp;
-    const bool live = pos < p.n_rows;
     const int64_t row = (live && p.row_order) ? (int64_t)p.row_order[pos] : pos;
     const R* __restrict__ E = reinterpret_cast<const R*>(p.edges);
     const float4* __restrict__ X4 = reinterpret_cast<const float4*>(p.X);
@@ -311,7 +305,6 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[a][v] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-    R* mywin = win[grp];
     // prefetch the first window into registers
     R nxt = (beg + t < end) ? E[beg + t] : R{};
     for (int64_t w0 = beg; w0 < end; w0 += WIN) {
@@ -431,6 +424,39 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
         }
 }
 
+template <int LPR, int NV, int U, int MODE, int NT = 256, bool GATED = false>
+__global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
+    using R = typename Rec<MODE>::T;
+    constexpr int RPB = NT / LPR;
+    __shared__ __attribute__((aligned(16))) R win[RPB][LPR];
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int grp = threadIdx.x / LPR;
+    const int64_t pos = lb * RPB + grp;
+    win_row<LPR, NV, U, MODE, GATED>(p, pos, pos < p.n_rows, win[grp]);
+}
+
+// Persistent, CU-chunked variant (PG_FLAG_SPMM_CU_CHUNKS): gridDim.x = 8 XCDs x 32 CUs x S blocks. Hardware
+// block b is taken to run on XCD b % 8 and CU (b / 8) % 32 (round-robin placement of a grid that is resident
+// at once); each CU walks one contiguous chunk of the schedule, its S blocks interleaved 8-row group by group,
+// so the rows resident on one CU at a time are schedule neighbours and share source rows in its L1. If the
+// placement differs, the work split is still a bijection (only the locality changes).
+template <int LPR, int NV, int U, int MODE, bool GATED = false>
+__global__ __launch_bounds__(256) void spmm_win_cu_kernel(SpmmParams p, int S) {
+    using R = typename Rec<MODE>::T;
+    constexpr int RPB = 256 / LPR;
+    __shared__ __attribute__((aligned(16))) R win[RPB][LPR];
+    const int b = blockIdx.x, x = b & 7, i = b >> 3, c = i & 31, k = i >> 5;
+    const int64_t n = p.n_rows;
+    const int64_t unit = 8 * 32;  // (XCD, CU) chunks
+    const int64_t q = (int64_t)x * 32 + c;
+    const int64_t lo = n * q / unit, hi = n * (q + 1) / unit;
+    const int grp = threadIdx.x / LPR;
+    for (int64_t g0 = lo + (int64_t)k * RPB; g0 < hi; g0 += (int64_t)S * RPB) {
+        const int64_t pos = g0 + grp;
+        win_row<LPR, NV, U, MODE, GATED>(p, pos, pos < hi, win[grp]);
+    }
+}
+
 // Fallback for feature widths that are not a multiple of 4 (or too wide for the vector path):
 // one wave per row, features in chunks of 64 (one per lane), records re-read per chunk.
 template <int MODE>
@@ -522,6 +548,16 @@ void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
         const int64_t rpb = nt / LPR;
         const int64_t nb = (p.n_rows + rpb - 1) / rpb;
         const bool u8 = flags & PG_FLAG_UNROLL4;
+        if (flags & PG_FLAG_SPMM_CU_CHUNKS) {  // persistent CU-chunked schedule (LPR = 32: 5 blocks per CU)
+            const int S = 5;
+            if (p.g_all) {
+                if constexpr (Shape<MODE>::NACC == 3)
+                    hipLaunchKernelGGL((spmm_win_cu_kernel<LPR, NV, 4, MODE, true>), dim3(256 * S), dim3(256), 0, s, p, S);
+            } else {
+                hipLaunchKernelGGL((spmm_win_cu_kernel<LPR, NV, 4, MODE, false>), dim3(256 * S), dim3(256), 0, s, p, S);
+            }
+            return;
+        }
         if (p.g_all) {  // gated store (pg_spmm3_gated_f32): the default configuration only
             if constexpr (Shape<MODE>::NACC == 3)
                 hipLaunchKernelGGL((spmm_win_kernel<LPR, NV, 4, MODE, 256, true>), dim3((unsigned)((p.n_rows + 256 / LPR - 1) / (256 / LPR))),

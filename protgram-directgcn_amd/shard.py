@@ -394,52 +394,59 @@ def halo_partition(g: CSRGraph, rank: int, world: int, layers: int,
     dev = g.rowptr.device
     if owner is None:
         owner = halo_owner(g, world)
-    owner = owner.to(device=dev, dtype=torch.int64)
+    # The index work (halo sets, relabelling, the permuted CSR) runs on the host and the result moves to the
+    # device once: it is setup, and the host path is the one the CPU tests exercise.
+    owner = owner.to(device="cpu", dtype=torch.int64)
     if owner.numel() != n or (n and (int(owner.min()) < 0 or int(owner.max()) >= world)):
         raise ValueError("owner must assign every node a rank in [0, world)")
-    rp = g.rowptr
+    host = torch.device("cpu")
+    rp = g.rowptr.to(host)
+    edges3 = g.edges3.to(host)
     counts = rp[1:] - rp[:-1]
-    row_of = torch.repeat_interleave(torch.arange(n, device=dev), counts)
-    col = g.edges3[:, 0].to(torch.int64)
+    row_of = torch.repeat_interleave(torch.arange(n), counts)
+    col = edges3[:, 0].to(torch.int64)
     # depth: 0 = owned, k = needed first by layer L-1-k, L = never computed (input gather source only)
-    depth = torch.full((n,), layers, dtype=torch.int64, device=dev)
+    depth = torch.full((n,), layers, dtype=torch.int64)
     need = owner == rank
     depth[need] = 0
     for k in range(1, layers):
-        nb = torch.zeros(n, dtype=torch.bool, device=dev)
+        nb = torch.zeros(n, dtype=torch.bool)
         nb[col[need[row_of]]] = True
         new = nb & ~need
         depth[new] = k
         need = need | nb
     perm = torch.sort(depth, stable=True).indices  # by depth, node id order inside a depth
-    inv = torch.empty(n, dtype=torch.int64, device=dev)
-    inv[perm] = torch.arange(n, dtype=torch.int64, device=dev)
-    dcount = torch.bincount(depth, minlength=layers + 1).cpu()
+    inv = torch.empty(n, dtype=torch.int64)
+    inv[perm] = torch.arange(n, dtype=torch.int64)
+    dcount = torch.bincount(depth, minlength=layers + 1)
     cum = torch.cumsum(dcount, 0).tolist()
     layer_rows = [int(cum[layers - 1 - i]) for i in range(layers)]  # layer i computes depths <= L-1-i
     # CSR of the largest prefix (layer 0) in local ids; later layers are zero-copy prefixes of it
     R0 = layer_rows[0]
     old = perm[:R0]
     cnt = counts[old]
-    lrp = torch.zeros(R0 + 1, dtype=torch.int64, device=dev)
+    lrp = torch.zeros(R0 + 1, dtype=torch.int64)
     lrp[1:] = torch.cumsum(cnt, 0)
     tot = int(lrp[-1])
-    src = (torch.arange(tot, dtype=torch.int64, device=dev) - torch.repeat_interleave(lrp[:-1], cnt)
+    src = (torch.arange(tot, dtype=torch.int64) - torch.repeat_interleave(lrp[:-1], cnt)
            + torch.repeat_interleave(rp[old], cnt))
-    e = g.edges3[src].clone()
+    e = edges3[src]
     e[:, 0] = inv[e[:, 0].to(torch.int64)].to(torch.int32)
+    if tot and (int(e[:, 0].min()) < 0 or int(e[:, 0].max()) >= n):
+        raise RuntimeError("halo_partition: relabelled column ids out of range")
     gorder = None
     if g.row_order is not None:  # the global schedule's relative order, restricted to each prefix
-        gorder = inv[g.row_order.to(torch.int64)]
+        gorder = inv[g.row_order.to(host, torch.int64)]
+    lrp_d, e_d = lrp.to(dev), e.to(dev)
     graphs = []
     for i, R in enumerate(layer_rows):
         order = None
         if gorder is not None:
-            order = gorder[gorder < R].to(torch.int32)
+            order = gorder[gorder < R].to(torch.int32).to(dev)
         e1 = int(lrp[R])
-        graphs.append(CSRGraph(n_rows=R, shared=True, rowptr=lrp[:R + 1], edges3=e[:e1], symmetric=False, nnz=e1,
-                               row_order=order, n_cols=n if i == 0 else layer_rows[i - 1]))
-    return HaloPartition(rank, world, n, perm, layer_rows, graphs)
+        graphs.append(CSRGraph(n_rows=R, shared=True, rowptr=lrp_d[:R + 1], edges3=e_d[:e1], symmetric=False,
+                               nnz=e1, row_order=order, n_cols=n if i == 0 else layer_rows[i - 1]))
+    return HaloPartition(rank, world, n, perm.to(dev), layer_rows, graphs)
 
 
 @torch.no_grad()

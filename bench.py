@@ -192,6 +192,12 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": launch_bytes, "avg_launch_ms": round(spmm_avg_ms, 4),
                 "launches_timed": len(spmm_ms)}
+    if traffic:  # the PMC-measured HBM bytes over the same launch time: the kernel's actual DRAM bandwidth
+        roofline["traffic_gbs"] = round(traffic / (spmm_avg_ms * 1e-3) / 1e9, 1)
+        roofline["traffic_frac"] = round(roofline["traffic_gbs"] / HBM_PEAK_GBS, 4)
+        roofline["note"] = ("achieved/frac: SURVEY 8(d) no-reuse gather model (every X-row gather counted as HBM); "
+                            "X re-reads are served by L1/L2/MALL, so frac > 1. traffic_*: measured DRAM bytes. "
+                            "Bound in practice: the L2-served row-gather rate (DESIGN.md 4)")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -121,17 +121,40 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
     const float inv = grad_scale ? (float)(1.0 / (double)grad_scale[0]) : 1.f;
     const int64_t beg = (b - chunk_ptr[lo]) * CHUNK;
     const int64_t end = min(beg + CHUNK, t.numel);
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
-        float g = t.g[i];
+    auto upd = [&](float g, float& p, float& m, float& v) {
         if (grad_scale) g = g * inv;
-        float p = t.p[i];
         if (weight_decay != 0.f) g = g + weight_decay * p;
-        float m = t.m[i];
         m = (w1 < 0.5f) ? m + w1 * (g - m) : g - (g - m) * (1.f - w1);  // at::lerp
-        float v = t.v[i] * b2;
+        v = v * b2;
         v = v + w2 * g * g;
         const float denom = sqrtf(v) / bc2s + eps;
         p = p + step_size * (m / denom);
+    };
+    // 16-B accesses when all four arrays allow it (the same per-element arithmetic), scalar tail
+    const bool vec = ((reinterpret_cast<uintptr_t>(t.g) | reinterpret_cast<uintptr_t>(t.p) |
+                       reinterpret_cast<uintptr_t>(t.m) | reinterpret_cast<uintptr_t>(t.v)) & 15) == 0;
+    int64_t i0 = beg;
+    if (vec) {
+        const int64_t n4 = (end - beg) >> 2;
+        for (int64_t k = threadIdx.x; k < n4; k += 256) {
+            const int64_t i = beg + 4 * k;
+            const float4 g = *reinterpret_cast<const float4*>(t.g + i);
+            float4 p = *reinterpret_cast<const float4*>(t.p + i);
+            float4 m = *reinterpret_cast<const float4*>(t.m + i);
+            float4 v = *reinterpret_cast<const float4*>(t.v + i);
+            upd(g.x, p.x, m.x, v.x);
+            upd(g.y, p.y, m.y, v.y);
+            upd(g.z, p.z, m.z, v.z);
+            upd(g.w, p.w, m.w, v.w);
+            *reinterpret_cast<float4*>(t.p + i) = p;
+            *reinterpret_cast<float4*>(t.m + i) = m;
+            *reinterpret_cast<float4*>(t.v + i) = v;
+        }
+        i0 = beg + 4 * n4;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < end; i += 256) {
+        float p = t.p[i], m = t.m[i], v = t.v[i];
+        upd(t.g[i], p, m, v);
         t.p[i] = p;
         t.m[i] = m;
         t.v[i] = v;

@@ -162,7 +162,8 @@ class Adam(torch.optim.Optimizer):
             fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
             check(lib.pg_adam_f32(len(ps), ctypes.c_void_p(tl.desc.data_ptr()), ctypes.c_void_p(tl.chunk_ptr.data_ptr()),
                                   tl.nchunks, float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                  float(group["weight_decay"]), ctypes.c_void_p(step.data_ptr()),
+                                  float(group["weight_decay"]) + float(getattr(self, "_l2_extra", 0.0)),
+                                  ctypes.c_void_p(step.data_ptr()),
                                   ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
                                   ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
                   "pg_adam_f32")
@@ -184,16 +185,26 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
     l2 = l2_sqsum(params) if l2_lambda else None
     scaled = scaler is not None and scaler.is_enabled()
     (scaler.scale(loss) if scaled else loss).backward()
-    if l2_lambda:
+    # train.Adam takes the L2 gradient 2 * l2_lambda * p as extra weight decay inside its one launch (added to
+    # the unscaled gradient before the moments, exactly where the gradient sum would put it); other optimizers
+    # get it added to p.grad by one pg_multi_axpy_f32 launch
+    fold = bool(l2_lambda) and isinstance(optimizer, Adam)
+    if l2_lambda and not fold:
         add_l2_grad(params, l2_lambda, scale=scaler._scale if scaled else None)  # device-side scale: no sync
-    else:  # the reference's 0 * l2 term still gives every parameter a (zero) gradient, so it is stepped
+    else:  # the reference's (0 *) l2 term gives every parameter a gradient, so it is stepped
         for p in params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-    if scaled:
-        scaler.step(optimizer)
-        scaler.update()
-    else:
-        optimizer.step()
+    if fold:
+        optimizer._l2_extra = 2.0 * l2_lambda
+    try:
+        if scaled:
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            optimizer.step()
+    finally:
+        if fold:
+            optimizer._l2_extra = 0.0
     total = loss.detach()
     return total + l2_lambda * l2 if l2 is not None else total

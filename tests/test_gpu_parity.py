@@ -858,6 +858,46 @@ def test_train_step_matches_reference_loop(pkg, cuda, amp):
         assert_grad_close(runs[1][1][k], v.cpu(), f"param {k}")
 
 
+@pytest.mark.parametrize("amp", [False, True])
+def test_train_step_adam_folded_l2_matches_reference_loop(pkg, cuda, amp):
+    """train.train_step with train.Adam, where the L2 gradient 2*lambda*p rides in the Adam launch as extra weight
+    decay (no separate gradient pass), against the reference loop with torch.optim.Adam (L2 term in the loss,
+    weight_decay 0): 3 steps, with and without autocast + GradScaler."""
+    import torch.nn.functional as F
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    lam = 1e-3
+    runs = []
+    for ours in (False, True):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        opt = train.Adam(m.parameters(), lr=1e-3) if ours else torch.optim.Adam(m.parameters(), lr=1e-3)
+        scaler = torch.amp.GradScaler("cuda", enabled=amp)
+        losses = []
+        for _ in range(3):
+            if ours:
+                losses.append(float(train.train_step(m, data, y, opt, l2_lambda=lam, scaler=scaler)))
+                assert getattr(opt, "_l2_extra", 0.0) == 0.0  # the fold is per call
+            else:
+                opt.zero_grad()
+                with torch.amp.autocast("cuda", enabled=amp):
+                    out, _ = m(data=data)
+                    loss = F.nll_loss(out, y) + lam * sum(p.norm(2).pow(2) for p in m.parameters() if p.requires_grad)
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
+                losses.append(float(loss))
+        runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-5)
+    for k, v in runs[0][1].items():  # Adam normalises each step to ~lr: compare on that scale
+        err = float((runs[1][1][k] - v).abs().max())
+        assert err <= 5e-5, (k, err)
+
+
 def test_multi_tensor_helpers(pkg, cuda):
     from protgram_directgcn_amd import train
     g = torch.Generator().manual_seed(0)

@@ -358,7 +358,8 @@ def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
                                                       (129, 16, 40, True, True, True), (64, 128, 96, False, True, True),
                                                       (31, 128, 128, False, True, False), (4097, 64, 128, False, True, False),
                                                       (2050, 128, 128, False, False, False), (700, 128, 128, True, True, False),
-                                                      (1500, 64, 128, True, True, False), (17, 128, 128, False, True, False),
+                                                      (1500, 64, 128, True, True, False), (17, 128, 128, False, True, False), (1, 128, 128, False, True, False),
+                                                      (5, 128, 128, False, False, False),
                                                       (8200, 128, 128, False, True, False), (4111, 128, 128, True, True, False)])
 def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
     """pg_directgcn_dense_f32 (all tilings, the fp32 and split-bf16 W-stationary kernels, pre-gated operands) against

@@ -258,15 +258,18 @@ def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
     w = [torch.from_numpy(e[:nnz_keep, 1 + j].copy().view(np.float32)) for j in range(3)]
     xc = x.cpu()
     times = []
+    reps = 3
     with torch.no_grad():
         for i, conv in enumerate(model.convs[:layers]):
             p = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
-            for rep in range(2):  # 1 warm-up + 1 timed per layer
+            ts = []
+            for rep in range(reps + 1):  # 1 warm-up + `reps` timed runs per layer, median
                 t0 = time.perf_counter()
                 y = oc.layer_forward(p, xc, ei, w[0], ei, w[1], ei, w[2])
                 dt = time.perf_counter() - t0
                 if rep:
-                    times.append(dt)
+                    ts.append(dt)
+            times.append(sorted(ts)[len(ts) // 2])
             xc = torch.nn.functional.leaky_relu(y + xc)
     t = sum(times)
     val = 3 * nnz_keep * len(times) / t
@@ -276,10 +279,19 @@ def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
     what = (f"full graph (N={N}, 3x{e.shape[0]} entries)" if full else
             f"row sample: first {int(rows[-1]) + 1 if nnz_keep else 0} of {N} destination rows (3x{nnz_keep} of "
             f"3x{e.shape[0]} entries; a full propagate would materialise {e.shape[0] * F * 4 / 1e9:.0f} GB)")
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {"value": round(val, 1), "unit": "edges/s", "cores": threads, "kind": "port",
             "sample": f"{len(times)} DirectGCN layer forward(s), {what}; oracle = reference CPU algorithm "
-                      f"(6 Linear + 6 index_select/mul/scatter_add_), torch {torch.__version__} CPU, {threads} threads, "
-                      f"one timed run per layer after 1 warm-up",
+                      f"(6 Linear + 6 index_select/mul/scatter_add_), torch {torch.__version__} CPU, {threads} threads "
+                      f"of {os.cpu_count()} host CPUs ({cpu_model}), median of {reps} timed runs per layer after 1 warm-up",
             "seconds": round(t, 3)}
 
 

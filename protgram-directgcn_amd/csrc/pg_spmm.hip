@@ -35,11 +35,20 @@ struct SpmmParams {
     int F;
     int accumulate;
     int remap;
+    int store_sc1;  // Z stores with sc1: written through and dropped from the XCD's L2 (keeps L2 for the X rows)
     // optional output gates (pg_spmm3_gated_f32): Z_q[i] *= s_q(i) at the store, s = the DirectGCN gates
     // s_in = c_all*c_dir*c_in, s_out = c_all*c_dir*c_out, s_und = c_all*c_und (protgram_directgcn.py:116-133)
     const float *g_in, *g_out, *g_dir, *g_und, *g_all;
     int gate_scalar;
 };
+
+typedef float pg_f32x4_t __attribute__((ext_vector_type(4)));
+// 16-B store that leaves the line out of the XCD's L2 (MI355X_MICROARCH.md: plain / nt stores keep the line in
+// L2, sc1 stores drop it; a 16-B sc1 store costs what a plain one does)
+__device__ __forceinline__ void store_sc1(float4* dst, float4 v) {
+    const pg_f32x4_t w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
+}
 
 // Gate inputs of row `row`, loaded when the row starts (so their latency hides behind the row's gathers) and
 // turned into the three gates at the store (1, 1, 1 when the call is not gated). Same products as pg_dense.hip.
@@ -420,7 +429,8 @@ __device__ __forceinline__ void win_row(const SpmmParams& p, int64_t pos, bool l
                 const float4 old = *dst;
                 val = make_float4(add(old.x, val.x), add(old.y, val.y), add(old.z, val.z), add(old.w, val.w));
             }
-            *dst = val;
+            if (p.store_sc1) store_sc1(dst, val);
+            else *dst = val;
         }
 }
 
@@ -590,6 +600,7 @@ template <int MODE>
 int dispatch(SpmmParams p, uint32_t flags, hipStream_t s, const char* name) {
     if (p.n_rows == 0) return PG_OK;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    p.store_sc1 = (flags & PG_FLAG_SPMM_SC1) ? 1 : 0;
     const bool vec_ok = (p.F % 4 == 0) && (p.ldx % 4 == 0) && (p.ldz % 4 == 0) && pg::aligned16(p.X) &&
                         pg::aligned16(p.Z);
     const int F = p.F;

@@ -88,6 +88,8 @@ typedef struct pg_edge1 {
                                             operands (6 products, fp32-level accuracy); F_out = 128, K = 384 or 256,
                                             no row map. Default for that shape unless another dense variant flag is set;
                                             F_in = 128 runs the 16-row software-pipelined kernel */
+#define PG_FLAG_SPMM_OCC6 (1u << 28)      /* SpMM variant C compiled for >= 6 waves per SIMD (measurement) */
+#define PG_FLAG_SPMM_OCC8 (1u << 29)      /* SpMM variant C compiled for 8 waves per SIMD (measurement) */
 #define PG_FLAG_SPMM_SC1 (1u << 19)       /* SpMM variant C: Z stores with sc1 (dropped from L2 instead of kept) */
 #define PG_FLAG_SPMM_CU_CHUNKS (1u << 18) /* SpMM variant C: persistent grid, each CU walks a contiguous schedule chunk */
 #define PG_FLAG_DENSE_X3_32 (1u << 17)    /* split-bf16 dense kernel: the 32-row unpipelined tile loop instead */

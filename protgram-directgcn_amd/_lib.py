@@ -28,6 +28,8 @@ PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_DENSE_X3_32 = 1 << 17
 PG_FLAG_SPMM_CU_CHUNKS = 1 << 18
 PG_FLAG_SPMM_SC1 = 1 << 19
+PG_FLAG_SPMM_OCC6 = 1 << 28
+PG_FLAG_SPMM_OCC8 = 1 << 29
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 

@@ -1,4 +1,12 @@
-// DirectGCN dense contraction + gated combine on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// DirectGCN dense contraction + gated combine on gfx950 MFMA. Kernels (dispatch in pg_directgcn_dense_f32):
+//  * dense_x3p_kernel (default, F_in = F_out = 128, no row map): split-bf16 W-stationary, software-pipelined on
+//    16-row tiles (v_mfma_f32_16x16x32_bf16, exact three-way bf16 splits: fp32-level accuracy); reads the
+//    unpacked weights when `packed` is NULL;
+//  * dense_x3_kernel: the same on 32-row tiles without the pipeline (F_in = 64 with a projected residual, or
+//    PG_FLAG_DENSE_X3_32);
+//  * dense_ws_kernel: fp32 W-stationary (v_mfma_f32_16x16x4f32), PG_FLAG_DENSE_WS;
+//  * dense_kernel: the tiled fp32 GEMM described below (every other shape, row maps, projected residuals).
+// Tiled fp32 kernel (v_mfma_f32_32x32x2_f32):
 //
 // After the fused propagation Z = [A_in X | A_out X | A_und X] (pg_spmm.hip), the layer output of
 // src/models/protgram_directgcn.py:100-133 is, with A(xW) = (Ax)W,
@@ -7,7 +15,7 @@
 // i.e. ONE GEMM with K = 3*F_in (4*F_in with the model's projected residual as a 4th segment).
 //
 //  pg_directgcn_pack_f32  -- packs B = [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] ([F_out, K]) and the
-//                            bias sums ([3, F_out]) once; callers cache it while the weights are unchanged.
+//                            bias sums ([3, F_out]); packed on every call (parameters can change in place).
 //  pg_directgcn_dense_f32 -- A-loader scales Z by the per-row gate (gates computed once per block into LDS,
 //                            gathered through original_indices when given); epilogue adds the gated bias
 //                            sums, the per-node constant, the residual and leaky_relu, then stores y once.

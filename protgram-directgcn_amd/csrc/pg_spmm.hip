@@ -445,6 +445,19 @@ __global__ __launch_bounds__(NT) void spmm_win_kernel(SpmmParams p) {
     win_row<LPR, NV, U, MODE, GATED>(p, pos, pos < p.n_rows, win[grp]);
 }
 
+// Occupancy probe (PG_FLAG_SPMM_OCC6 / OCC8): the default window kernel compiled for >= W waves per SIMD (the
+// register allocator then targets 512 / W VGPRs)
+template <int LPR, int NV, int U, int MODE, bool GATED, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, 8))) void spmm_win_occ_kernel(SpmmParams p) {
+    using R = typename Rec<MODE>::T;
+    constexpr int RPB = 256 / LPR;
+    __shared__ __attribute__((aligned(16))) R win[RPB][LPR];
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int grp = threadIdx.x / LPR;
+    const int64_t pos = lb * RPB + grp;
+    win_row<LPR, NV, U, MODE, GATED>(p, pos, pos < p.n_rows, win[grp]);
+}
+
 // Persistent, CU-chunked variant (PG_FLAG_SPMM_CU_CHUNKS): gridDim.x = 8 XCDs x 32 CUs x S blocks. Hardware
 // block b is taken to run on XCD b % 8 and CU (b / 8) % 32 (round-robin placement of a grid that is resident
 // at once); each CU walks one contiguous chunk of the schedule, its S blocks interleaved 8-row group by group,
@@ -558,6 +571,21 @@ void launch_vec_u(const SpmmParams& p, uint32_t flags, hipStream_t s) {
         const int64_t rpb = nt / LPR;
         const int64_t nb = (p.n_rows + rpb - 1) / rpb;
         const bool u8 = flags & PG_FLAG_UNROLL4;
+        if (flags & (PG_FLAG_SPMM_OCC6 | PG_FLAG_SPMM_OCC8)) {
+            const unsigned nbo = (unsigned)((p.n_rows + 256 / LPR - 1) / (256 / LPR));
+            const bool w8 = flags & PG_FLAG_SPMM_OCC8;
+            if (p.g_all) {
+                if constexpr (Shape<MODE>::NACC == 3) {
+                    if (w8) hipLaunchKernelGGL((spmm_win_occ_kernel<LPR, NV, 4, MODE, true, 8>), dim3(nbo), dim3(256), 0, s, p);
+                    else hipLaunchKernelGGL((spmm_win_occ_kernel<LPR, NV, 4, MODE, true, 6>), dim3(nbo), dim3(256), 0, s, p);
+                }
+            } else if (w8) {
+                hipLaunchKernelGGL((spmm_win_occ_kernel<LPR, NV, 4, MODE, false, 8>), dim3(nbo), dim3(256), 0, s, p);
+            } else {
+                hipLaunchKernelGGL((spmm_win_occ_kernel<LPR, NV, 4, MODE, false, 6>), dim3(nbo), dim3(256), 0, s, p);
+            }
+            return;
+        }
         if (flags & PG_FLAG_SPMM_CU_CHUNKS) {  // persistent CU-chunked schedule (LPR = 32: 5 blocks per CU)
             const int S = 5;
             if (p.g_all) {

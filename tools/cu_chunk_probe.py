@@ -13,6 +13,7 @@ from __graft_entry__ import load_package  # noqa: E402
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
 from protgram_directgcn_amd._lib import PG_FLAG_SPMM_CU_CHUNKS as CU, PG_FLAG_SPMM_SC1 as SC1  # noqa: E402
+from protgram_directgcn_amd._lib import PG_FLAG_SPMM_OCC6 as OCC6, PG_FLAG_SPMM_OCC8 as OCC8  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 F = 128
@@ -29,10 +30,13 @@ with torch.no_grad():
 prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
 v = {"plain": lambda: ops.spmm3(g, x, flags=0), "plain_cu": lambda: ops.spmm3(g, x, flags=CU),
      "gated": lambda: ops.spmm3_gated(g, x, prm, 0, flags=0), "gated_cu": lambda: ops.spmm3_gated(g, x, prm, 0, flags=CU),
-     "plain_sc1": lambda: ops.spmm3(g, x, flags=SC1), "gated_sc1": lambda: ops.spmm3_gated(g, x, prm, 0, flags=SC1)}
+     "plain_sc1": lambda: ops.spmm3(g, x, flags=SC1), "gated_sc1": lambda: ops.spmm3_gated(g, x, prm, 0, flags=SC1),
+     "gated_occ6": lambda: ops.spmm3_gated(g, x, prm, 0, flags=OCC6),
+     "gated_occ8": lambda: ops.spmm3_gated(g, x, prm, 0, flags=OCC8)}
 print("plain bit-exact:", torch.equal(v["plain"](), v["plain_cu"]()), " gated bit-exact:",
       torch.equal(v["gated"](), v["gated_cu"]()), " sc1 bit-exact:", torch.equal(v["plain"](), v["plain_sc1"]()),
-      torch.equal(v["gated"](), v["gated_sc1"]()))
+      torch.equal(v["gated"](), v["gated_sc1"]()), " occ bit-exact:", torch.equal(v["gated"](), v["gated_occ6"]()),
+      torch.equal(v["gated"](), v["gated_occ8"]()))
 
 
 def timeit(fn, reps=20):

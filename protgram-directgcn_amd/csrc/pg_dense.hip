@@ -26,6 +26,7 @@
 // lane feeds its MFMAs with one ds_read_b128 per operand per 4 MFMAs by permuting K identically for A
 // and B inside each group of 8 (MFMA k-step s of lane half h uses k = 4h + s): same sum, other order.
 #include "pg_common.h"
+#include "pg_split3.h"
 
 namespace {
 
@@ -590,39 +591,10 @@ __global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
 // thread converts 3 of the tile's 1536 16-byte A units into the three bf16 images (gated here when the
 // operand is not pre-gated) -> the next tile's DMA is issued -> 12 MFMA steps -> accumulators parked in LDS
 // (aliasing the consumed bf16 images) -> the same epilogue as dense_ws_kernel.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
-// bf16 pair (RNE, v_cvt_pk_bf16_f32) and the two values it represents, back in fp32
-__device__ __forceinline__ uint32_t bf2(float a, float b, float& fa, float& fb) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
-    fa = __uint_as_float(u << 16);
-    fb = __uint_as_float(u & 0xffff0000u);
-    return u;
-}
-// exact three-way split of 8 fp32 values into three bf16x8 operands
-__device__ __forceinline__ void split8(const float (&v)[8], uint4& s0, uint4& s1, uint4& s2) {
-    uint32_t w0[4], w1[4], w2[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float a = v[2 * i], b = v[2 * i + 1], fa, fb;
-        w0[i] = bf2(a, b, fa, fb);
-        a -= fa;
-        b -= fb;
-        w1[i] = bf2(a, b, fa, fb);
-        a -= fa;
-        b -= fb;
-        w2[i] = bf2(a, b, fa, fb);
-    }
-    s0 = make_uint4(w0[0], w0[1], w0[2], w0[3]);
-    s1 = make_uint4(w1[0], w1[1], w1[2], w1[3]);
-    s2 = make_uint4(w2[0], w2[1], w2[2], w2[3]);
-}
-__device__ __forceinline__ f32x4 mfma_bf(uint4 a, uint4 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
-                                                   0, 0, 0);
-}
+// bf2 / split8 / mfma_bf: pg_split3.h (shared with the split-bf16 weight gradient of pg_dense_bwd.hip)
+using pgx3::bf2;
+using pgx3::mfma_bf;
+using pgx3::split8;
 
 // Workgroup barrier for LDS hand-offs only: drains this wave's LDS ops, not its global loads (__syncthreads'
 // release fence also waits vmcnt(0), which would drain the next tile's LDS-DMA in flight). LDS-DMA landings are

@@ -26,6 +26,7 @@
 
 #include "pg_bf16_util.h"
 #include "pg_common.h"
+#include "pg_split3.h"
 
 namespace {
 
@@ -487,6 +488,135 @@ __global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
             const int i = i0 + 4 * cc + (qe & 3);
             if (i < p.P) out[(int64_t)p.P * p.N + (qe >> 2) * p.P + i] = v;
         }
+    }
+}
+
+// Split-bf16 weight gradient for the model's shape (P = F_out = 128, N = 3 F_in = 384, no projected residual):
+// the partial C[P x N] = A^T diag(s) B of one row split on v_mfma_f32_16x16x32_bf16 with exact three-way bf16
+// splits of both operands (pg_split3.h: six products, fp32-level accuracy; 2.7x fewer matrix-core cycles than
+// wgrad_kernel's fp32 MFMA). Two 512-thread blocks per split compute the 128 x 384 partial, one column half
+// each, so A is read twice (wgrad_kernel reads it once per 128-column tile). Per 32-row step a staging thread
+// owns one 8-row x 4-column fp32 block (threads 0-127: A = dpre, columns 0..127; threads 128-319: B = s_q Z_q,
+// the half's 192 columns), loaded into registers one step ahead; it splits each column's 8 rows (one MFMA
+// k-group) into three bf16 units and stores them transposed, [column][row group], swizzled so that every
+// ds_read_b128 lane group and 8-lane write group hits distinct bank slots. Wave w then owns output rows
+// 16w..16w+15: three A-split operands, and for each of the 12 column blocks three B-split operands and six
+// MFMAs. The A threads also sum the bias gradients (s_q dpre per column, in row order) and the first half's
+// block reduces them over its 4 row groups in fixed order.
+constexpr int WX_P = 128, WX_N = 384, WX_H = WX_N / 2, WX_NC = WX_P + WX_H;
+__device__ __forceinline__ int wx_unit(int col, int g) { return 4 * col + (g ^ ((-(col >> 2)) & 3)); }
+
+// grid (splits, 2): blockIdx.y picks the half of the 384 output columns (A is read twice, not three times)
+__global__ __launch_bounds__(512) void wgrad_x3_kernel(WgradP p) {
+    __shared__ __attribute__((aligned(16))) uint4 Us[3][WX_NC * 4];
+    __shared__ __attribute__((aligned(16))) float Db[4][4][WX_P];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 15, kk = lane >> 4;
+    const int half = blockIdx.y;
+    const int64_t r0 = (int64_t)blockIdx.x * p.rows_per_split;
+    const int64_t rend = min(r0 + p.rows_per_split, p.M);
+    // staging roles (wave-uniform): waves 0-1 stage A (128 columns), waves 2-4 B (this half's 192 columns),
+    // waves 5-7 only run MFMAs
+    const bool isA = tid < 128, isB = tid >= 128 && tid < 320;
+    const int u = isA ? tid : tid - 128;
+    const int g = isA ? (u >> 5) : (u / 48);
+    const int j = isA ? (u & 31) : (u % 48);
+    const int col0 = (isA ? 0 : WX_P) + 4 * j;                  // staged column
+    const int gcol = isA ? 4 * j : WX_H * half + 4 * j;          // column in A or in Z
+    const int seg = isA ? 3 : gcol / p.F_in;
+    const float* src = isA ? p.A + gcol : p.Z + gcol;
+    const int64_t ld = isA ? p.lda : p.ldz;
+    const bool stage = isA || isB;
+    float4 x[8];
+    float gv[8][3];  // A: (s_in, s_out, s_und) per row; B: [e][0] = the row's scale of this segment
+    auto load = [&](int64_t base) {
+        if (!stage) return;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int64_t m = base + 8 * g + e;
+            const bool ok = m < rend;
+            const int64_t mm = ok ? m : r0;
+            x[e] = ok ? ld4(src + mm * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (isA) {
+                const float4 s = p.gates ? ld4(p.gates + mm * 4) : make_float4(1.f, 1.f, 1.f, 1.f);
+                gv[e][0] = s.x;
+                gv[e][1] = s.y;
+                gv[e][2] = s.z;
+            } else {
+                gv[e][0] = p.gates ? p.gates[mm * 4 + seg] : 1.f;
+            }
+        }
+    };
+    float db[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) db[t][0] = db[t][1] = db[t][2] = db[t][3] = 0.f;
+    auto split_store = [&]() {
+        if (!stage) return;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float xv = c == 0 ? x[e].x : c == 1 ? x[e].y : c == 2 ? x[e].z : x[e].w;
+                v[e] = isA ? xv : __fmul_rn(xv, gv[e][0]);
+            }
+            uint4 s0, s1, s2;
+            pgx3::split8(v, s0, s1, s2);
+            const int pos = wx_unit(col0 + c, g);
+            Us[0][pos] = s0;
+            Us[1][pos] = s1;
+            Us[2][pos] = s2;
+        }
+        if (isA) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float sv[4] = {gv[e][0], gv[e][1], gv[e][2], 1.f};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    db[t][0] += sv[t] * x[e].x;
+                    db[t][1] += sv[t] * x[e].y;
+                    db[t][2] += sv[t] * x[e].z;
+                    db[t][3] += sv[t] * x[e].w;
+                }
+            }
+        }
+    };
+    pgx3::f32x4_t acc[WX_H / 16];
+#pragma unroll
+    for (int jb = 0; jb < WX_H / 16; ++jb) acc[jb] = pgx3::f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int ua = wx_unit(16 * wave + li, kk);
+    const int64_t nsteps = (rend - r0 + WROWS - 1) / WROWS;
+    if (nsteps > 0) load(r0);
+    for (int64_t t = 0; t < nsteps; ++t) {
+        split_store();
+        __syncthreads();  // the split images of step t are complete
+        if (t + 1 < nsteps) load(r0 + (t + 1) * WROWS);  // in flight during the MFMAs
+        const uint4 a0 = Us[0][ua], a1 = Us[1][ua], a2 = Us[2][ua];
+#pragma unroll
+        for (int jb = 0; jb < WX_H / 16; ++jb) {
+            const int ub = wx_unit(WX_P + 16 * jb + li, kk);
+            acc[jb] = pgx3::mfma_x3(a0, a1, a2, Us[0][ub], Us[1][ub], Us[2][ub], acc[jb]);
+            __builtin_amdgcn_sched_barrier(0);  // one column block's operands live at a time
+        }
+        __syncthreads();  // every wave is done with the images before the next split overwrites them
+    }
+    float* out = p.part + (int64_t)blockIdx.x * p.part_stride;
+#pragma unroll
+    for (int jb = 0; jb < WX_H / 16; ++jb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            out[(int64_t)(16 * wave + 4 * kk + e) * WX_N + WX_H * half + 16 * jb + li] = acc[jb][e];
+    if (half != 0) return;  // the bias gradients come from the first half's blocks
+    if (isA) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Db[g][t][4 * j + c] = db[t][c];
+    }
+    __syncthreads();
+    {
+        const int t = tid >> 7, c = tid & 127;  // 4 x 128 = 512 sums, row groups in fixed order
+        const float v = ((Db[0][t][c] + Db[1][t][c]) + Db[2][t][c]) + Db[3][t][c];
+        out[(int64_t)WX_P * WX_N + t * WX_P + c] = v;
     }
 }
 
@@ -992,6 +1122,9 @@ SplitPlan split_rows(int64_t M, int64_t tiles) {
 
 int64_t up4(int64_t v) { return (v + 3) / 4 * 4; }
 
+// the split-bf16 weight gradient (wgrad_x3_kernel, opt-in: PG_FLAG_DENSE_X3) takes the model's shape
+bool wgrad_x3_shape(int64_t F_in, int64_t F_out, bool proj) { return F_in == 128 && F_out == 128 && !proj; }
+
 BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
     BwdPlan b{};
     b.K = (int)((proj ? 4 : 3) * F_in);
@@ -1112,8 +1245,14 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         w.rows_per_split = pl.rows_per_split;
         w.part_stride = pl.part_stride;
         w.part = part;
-        dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
-        hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
+        // the split-bf16 wgrad measured slower than the fp32 one (0.270 vs 0.190 ms at B(20,4)): one split step of
+        // register prefetch at one block per CU leaves it latency bound, so it is opt-in
+        if (wgrad_x3_shape(F_in, F_out, proj) && (flags & PG_FLAG_DENSE_X3)) {
+            hipLaunchKernelGGL(wgrad_x3_kernel, dim3((unsigned)pl.splits, 2), dim3(512), 0, s, w);
+        } else {
+            dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
+            hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
+        }
     }
     // F_out % 4 == 0, so part_stride == F_out*K + 4*F_out == the dW buffer
     launch_reduce(pl.part_stride / 4, pl.splits, pl.part_stride, part, g->dW, s);

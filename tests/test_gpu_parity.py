@@ -508,6 +508,15 @@ def test_dense_backward_vs_float64(pkg, cuda, monkeypatch, M, Fin, Fout, proj, v
         assert_grad_close(brg.grad, brd.grad, "db_res")
 
 
+@pytest.mark.parametrize("M,rows", [(1000, False), (3001, True)])
+def test_dense_backward_x3_wgrad_vs_float64(pkg, cuda, monkeypatch, M, rows):
+    """The opt-in split-bf16 weight gradient (PG_FLAG_DENSE_X3 in the backward flags) through the same float64
+    autograd check as the default fp32 one."""
+    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_X3
+    monkeypatch.setenv("PG_SPMM_FLAGS", hex(PG_FLAG_DENSE_X3))
+    test_dense_backward_vs_float64(pkg, cuda, monkeypatch, M, 128, 128, False, True, rows, True)
+
+
 def test_dense_backward_deterministic(pkg, cuda):
     from protgram_directgcn_amd import ops
     Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(20000, 128, 128, False, True, False, 3)

@@ -7,8 +7,10 @@
 // (v_mfma_f32_32x32x2_f32, B operands straight from the L1/L2-resident weights), and finishes the row
 // softmax in LDS. Replaces 6+ framework launches and two re-reads of h.
 // Fast path: F <= 256, H <= 128, C <= 64 (F, H multiples of 4); other shapes use a one-wave-per-row
-// fallback kernel.
+// fallback kernel. The model's own shape (F = 128 -> 64 -> C <= 32) runs head_x3_kernel (split-bf16 decoder 1;
+// head_f128_kernel, its fp32-MFMA predecessor, with -DPG_HEAD_FP32).
 #include "pg_common.h"
+#include "pg_split3.h"
 
 namespace {
 
@@ -333,6 +335,152 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
 }
 
+// Split-bf16 variant of head_f128_kernel (the default for its shape): decoder 1 (K = 128, 75 % of the head's
+// matrix work) on v_mfma_f32_16x16x32_bf16 with exact three-way bf16 splits of h and W1 (pg_split3.h: six
+// products per k step, fp32-level accuracy) -- 48 bf16 MFMAs per wave instead of 64 fp32 16x16x4 ones at twice
+// the cycles each. The h tile never goes through LDS as fp32: each thread keeps its 4 rows x 4 columns in
+// registers, reduces the row norms across the row's 32 lanes, writes the embeddings, and stores its three bf16
+// splits (half a 16-B operand unit per row) into row-swizzled images. Decoder 2 and the softmax as head_f128.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void head_x3_kernel(HeadP p) {
+    constexpr int BM = 32, F = 128, H = 64, CP = 32;
+    constexpr int ZLD = H + 8, LLD = CP + 1;
+    constexpr int NU = F / 8;  // bf16 operand units per row
+    __shared__ __attribute__((aligned(16))) uint4 As[3][BM * NU];  // 24 KB; Zs aliases it after decoder 1
+    __shared__ __attribute__((aligned(16))) float Ls[BM * LLD];
+    float* Zs = reinterpret_cast<float*>(&As[0][0]);
+    static_assert(BM * ZLD * 4 <= 3 * BM * NU * 16, "Zs fits the split images");
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int li = lane & 15, q = lane >> 4;
+    const int64_t m0 = (int64_t)blockIdx.x * BM;
+    const int c4 = tid & 31;  // this thread's float4 column of every row it holds
+    // 1. h rows (tid >> 5) + 8k, columns 4 c4 .. 4 c4 + 3
+    float4 hv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t m = m0 + (tid >> 5) + 8 * k;
+        if (m >= p.M) {
+            hv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if (p.hb) {  // bf16 mode: widened exactly
+            const uint2 w = *reinterpret_cast<const uint2*>(p.hb + m * p.ldh + 4 * c4);
+            hv[k] = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+        } else {
+            hv[k] = ld4(p.h + m * p.ldh + 4 * c4);
+        }
+    }
+    // W1 splits: wave w owns hidden columns 16w + li; k step s takes k = 32 s + 8 q .. + 7
+    uint4 w0[4], w1[4], w2[4];
+    {
+        const float* w1row = p.W1 + (int64_t)(16 * wave + li) * F + 8 * q;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const float4 x0 = ld4(w1row + 32 * s), x1 = ld4(w1row + 32 * s + 4);
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            pgx3::split8(v, w0[s], w1[s], w2[s]);
+        }
+    }
+    float4 w2f[4];
+    {
+        const int c = 16 * (wave >> 1) + li;
+        const bool cok = c < p.C;
+        const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * H + 4 * q;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) w2f[m] = cok ? ld4(w2row + 16 * m) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float b1v = p.b1[16 * wave + li];
+    const int c2 = 16 * (wave >> 1) + li;
+    const float b2v = c2 < p.C ? p.b2[c2] : 0.f;
+    // 2. embeddings from registers (row norm: 4-column partials, butterfly over the row's 32 lanes) and the
+    //    split images
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int r = (tid >> 5) + 8 * k;
+        const float4 v = hv[k];
+        float ss = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) ss += __shfl_xor(ss, o, 32);
+        const int64_t m = m0 + r;
+        if (m < p.M) {
+            const float inv = 1.0f / (sqrtf(ss) + p.eps);
+            *reinterpret_cast<float4*>(p.emb + m * p.lde + 4 * c4) = make_float4(v.x * inv, v.y * inv, v.z * inv, v.w * inv);
+        }
+        uint32_t s0[2], s1[2], s2[2];
+        {
+            float fa, fb;
+            float a = v.x, b = v.y;
+            s0[0] = pgx3::bf2(a, b, fa, fb); a -= fa; b -= fb;
+            s1[0] = pgx3::bf2(a, b, fa, fb); a -= fa; b -= fb;
+            s2[0] = pgx3::bf2(a, b, fa, fb);
+            a = v.z; b = v.w;
+            s0[1] = pgx3::bf2(a, b, fa, fb); a -= fa; b -= fb;
+            s1[1] = pgx3::bf2(a, b, fa, fb); a -= fa; b -= fb;
+            s2[1] = pgx3::bf2(a, b, fa, fb);
+        }
+        const int u = c4 >> 1;
+        uint2* d0 = reinterpret_cast<uint2*>(&As[0][r * NU + (u ^ (r & 15))]) + (c4 & 1);
+        uint2* d1 = reinterpret_cast<uint2*>(&As[1][r * NU + (u ^ (r & 15))]) + (c4 & 1);
+        uint2* d2 = reinterpret_cast<uint2*>(&As[2][r * NU + (u ^ (r & 15))]) + (c4 & 1);
+        *d0 = make_uint2(s0[0], s0[1]);
+        *d1 = make_uint2(s1[0], s1[1]);
+        *d2 = make_uint2(s2[0], s2[1]);
+    }
+    __syncthreads();
+    // 3. z = relu(h W1^T + b1): wave w -> hidden columns 16w.., both 16-row blocks
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+            const int r = 16 * rb + li, u = 4 * s + q;
+            const int pos = r * NU + (u ^ (r & 15));
+            acc[rb] = pgx3::mfma_x3(As[0][pos], As[1][pos], As[2][pos], w0[s], w1[s], w2[s], acc[rb]);
+        }
+    }
+    __syncthreads();  // every wave is done with the split images before Zs overwrites them
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float z = acc[rb][i] + b1v;
+            Zs[(16 * rb + 4 * q + i) * ZLD + 16 * wave + li] = z > 0.f ? z : 0.f;
+        }
+    __syncthreads();
+    // 4. logits = z W2^T + b2: wave w -> rows 16 (w & 1).., classes 16 (w >> 1)..
+    {
+        const int rb = wave & 1;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 x = ld4(&Zs[(16 * rb + li) * ZLD + 4 * q + 16 * m]);
+            a = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, w2f[m].x, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, w2f[m].y, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, w2f[m].z, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, w2f[m].w, a, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ls[(16 * rb + 4 * q + i) * LLD + c2] = a[i] + b2v;
+    }
+    __syncthreads();
+    // 5. log_softmax (max-shifted, as torch): 8 threads per row
+    {
+        const int r = tid >> 3, part = tid & 7;
+        const int64_t m = m0 + r;
+        float mx = -INFINITY;
+        for (int c = part; c < p.C; c += 8) mx = fmaxf(mx, Ls[r * LLD + c]);
+        mx = fmaxf(mx, __shfl_xor(mx, 1, 8));
+        mx = fmaxf(mx, __shfl_xor(mx, 2, 8));
+        mx = fmaxf(mx, __shfl_xor(mx, 4, 8));
+        float se = 0.f;
+        for (int c = part; c < p.C; c += 8) se += expf(Ls[r * LLD + c] - mx);
+        se += __shfl_xor(se, 1, 8);
+        se += __shfl_xor(se, 2, 8);
+        se += __shfl_xor(se, 4, 8);
+        const float lse = mx + logf(se);
+        if (m < p.M)
+            for (int c = part; c < p.C; c += 8) p.logp[m * p.ldp + c] = Ls[r * LLD + c] - lse;
+    }
+}
+
 // General shapes: one wave per row, VALU.
 __global__ __launch_bounds__(256) void head_generic_kernel(HeadP p) {
     extern __shared__ float sm[];  // per wave: F + H + C floats
@@ -400,7 +548,11 @@ int head_launch(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, cons
         return (unsigned)((ntiles + per_block - 1) / per_block);
     };
     if (vec && F == 128 && H == 64 && C <= 32 && ldh % 4 == 0 && lde % 4 == 0) {
+#ifdef PG_HEAD_FP32
         hipLaunchKernelGGL(head_f128_kernel, dim3((unsigned)((M + 31) / 32)), dim3(256), 0, s, p);
+#else
+        hipLaunchKernelGGL(head_x3_kernel, dim3((unsigned)((M + 31) / 32)), dim3(256), 0, s, p);
+#endif
     } else if (vec && F <= 128 && H <= 64 && C <= 32) {
         hipLaunchKernelGGL((head_kernel<128, 64, 32>), dim3(grid_of(2)), dim3(256), 0, s, p);
     } else if (vec && F <= 256 && H <= 128 && C <= 64) {

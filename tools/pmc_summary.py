@@ -18,6 +18,8 @@ def classify(k):
         return "dense_x3p_pregated" if "<true" in k else "dense_x3p"
     if "head_f128_kernel" in k:
         return "head_f128"
+    if "head_x3_kernel" in k:
+        return "head_x3"
     if "dense_x3_kernel" in k:  # split-bf16 W-stationary dense kernel: <F_IN, KSEG, pregated>
         return "dense_x3_pregated" if k.rstrip(")").find("true>") >= 0 else "dense_x3"
     for key, short in (("dense_ws_kernel", "dense_ws"), ("spmm_vec_kernel", "spmm_bcast"),

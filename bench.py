@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--bf16", action="store_true", help="bf16 mode (config 5): bf16 features/activations, fp32 sums")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-layers", type=int, default=1)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes that "
+                    "measure roofline.traffic (N=1 only)")
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
     ap.add_argument("--chunks", type=int, default=4, help="N>1: layer-boundary all-gather in this many pieces, "
                     "overlapped with the compute (1 = one exchange after the layer)")
@@ -56,11 +58,53 @@ def parse():
                     "path; the graph fits every GPU's HBM); 'exchange' = node-range rows + RCCL all-gather per layer")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
+    ap.add_argument("--launch-check", action="store_true", help="N>1 plumbing check without a GPU: start the ranks, "
+                    "all-reduce over --dist-backend, print one JSON line, exit")
     return ap.parse_args()
+
+
+def launch_workers(n: int) -> int:
+    """--gpus N without an outside launcher: start N ranks with torch.distributed.run (127.0.0.1, a free port) as
+    CHILD processes and return their exit code. Called before anything touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(args, world: int, rank: int) -> None:
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(args.dist_backend)
+    t = torch.tensor([float(rank), 1.0])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world_size": world, "rank_sum": float(t[0]),
+                          "ranks": int(t[1]), "backend": args.dist_backend}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launch_check:
+        return launch_check(args, world, rank)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -69,11 +113,6 @@ def main():
     pkg = load_package()
     from protgram_directgcn_amd import ops, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     dev_index = 0 if args.one_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -96,19 +135,9 @@ def main():
     torch.cuda.synchronize()
     log(f"[bench] graph B(20,{n}): N={N} E={s.size} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s")
 
-    torch.manual_seed(0)
+    model = bench_model(pkg, N, Fd, L, n).to(dev).eval()
     dims = [Fd] * (L + 1)
     C = 20
-    model = pkg.ProtGramDirectGCN(dims, N, C, n, 0, 512, 0.5, True)
-    with torch.no_grad():  # non-trivial gates/biases (the reference init has C=1, b=0)
-        gen = torch.Generator().manual_seed(11)
-        for name, p in model.named_parameters():
-            leaf = name.split(".")[-1]
-            if leaf.startswith("C_"):
-                p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
-            elif "bias" in leaf:
-                p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
-    model = model.to(dev).eval()
     model.fused_norm = args.fused_norm
     x = torch.randn(N, Fd, generator=torch.Generator().manual_seed(1234)).to(dev)
     if args.bf16:
@@ -160,48 +189,46 @@ def main():
     edges_per_step = 3 * g.nnz * L
     value = edges_per_step * args.steps / elapsed
 
-    # roofline of the dominant kernel (SURVEY §8d B_agg, per launch = this rank's rows)
-    if hp is not None:  # launches alternate over the layers' row prefixes: their mean B_agg
-        el = 2 if args.bf16 else 4
-        launch_bytes = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in hp.graphs) // len(hp.graphs)
-    elif part is None:
-        launch_bytes = g.algorithmic_bytes(Fd, elem=2 if args.bf16 else 4)
-        launch_nnz, launch_rows = g.nnz, N
-    else:
-        launch_nnz, launch_rows = part.local.nnz, part.n_local
-        el = 2 if args.bf16 else 4
-        launch_bytes = 8 * (launch_rows + 1) + launch_nnz * (16 + el * Fd) + 3 * launch_rows * Fd * el
-    achieved = launch_bytes / (spmm_avg_ms * 1e-3) / 1e9
-    traffic = None
-    tfile = os.path.join(REPO, "profiles", "traffic_r01.json")
-    if os.path.exists(tfile) and world == 1:
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("workload") == f"B(20,{n})/F{Fd}" and tj.get("kernel_bytes_per_launch") and not args.bf16:
-                traffic = tj["kernel_bytes_per_launch"]
-        except (OSError, ValueError):
-            traffic = None
+    # roofline of the dominant kernel, priced on SURVEY 8(d)'s COMPULSORY bytes per launch (rowptr + records once,
+    # each X row once, 3 output rows, gates): the floor of HBM traffic for one propagation launch
+    el = 2 if args.bf16 else 4
     if args.bf16:
         kname = "pg_spmm3_bf16"
     elif args.fused_norm:
         kname = "pg_spmm3_fusednorm_f32"
-    else:  # single-GPU inference gates the aggregates in the propagation's store (same gathers, same B_agg)
+    else:  # inference gates the aggregates in the propagation's store (same gathers, + 20 B of gates per row)
         kname = "pg_spmm3_gated_f32" if ((world == 1 or hp is not None) and ops.PREGATED_INFERENCE) else "pg_spmm3_f32"
+    gated = kname == "pg_spmm3_gated_f32"
+    if hp is not None:  # launches alternate over the layers' row prefixes: their mean
+        launch_graphs = hp.graphs
+    elif part is None:
+        launch_graphs = [g]
+    else:
+        launch_graphs = [part.local]
+    comp = sum(gi.compulsory_bytes(Fd, elem=el, gated=gated) for gi in launch_graphs) // len(launch_graphs)
+    noreuse = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in launch_graphs) // len(launch_graphs)
+    achieved = comp / (spmm_avg_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": launch_bytes, "avg_launch_ms": round(spmm_avg_ms, 4),
-                "launches_timed": len(spmm_ms)}
-    if traffic:  # the PMC-measured HBM bytes over the same launch time: the kernel's actual DRAM bandwidth
-        roofline["traffic_gbs"] = round(traffic / (spmm_avg_ms * 1e-3) / 1e9, 1)
-        roofline["traffic_frac"] = round(roofline["traffic_gbs"] / HBM_PEAK_GBS, 4)
-        roofline["note"] = ("achieved/frac: SURVEY 8(d) no-reuse gather model (every X-row gather counted as HBM); "
-                            "X re-reads are served by L1/L2/MALL, so frac > 1. traffic_*: measured DRAM bytes. "
-                            "Bound in practice: the L2-served row-gather rate (DESIGN.md 4)")
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_model": "compulsory (SURVEY 8d): 8(N+1) + 16 nnz + X once + 3 output rows (+ 20 B/row gates)",
+                "algorithmic_bytes_per_launch": comp, "avg_launch_ms": round(spmm_avg_ms, 4),
+                "launches_timed": len(spmm_ms),
+                "no_reuse_bytes_per_launch": noreuse,
+                "no_reuse_gbs": round(noreuse / (spmm_avg_ms * 1e-3) / 1e9, 1)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(g, model, x, args.cpu_sample_layers, log)
+
+    if rank == 0 and world == 1 and not args.no_pmc:
+        pmc = pmc_traffic(args, log)
+        if pmc is not None:
+            roofline.update(pmc)
+            if roofline.get("traffic"):
+                roofline["traffic_gbs"] = round(roofline["traffic"] / (spmm_avg_ms * 1e-3) / 1e9, 1)
+                roofline["traffic_frac"] = round(roofline["traffic_gbs"] / HBM_PEAK_GBS, 4)
+                roofline["traffic_over_compulsory"] = round(roofline["traffic"] / comp, 3)
 
     extra = {}
     if args.extra and world == 1:
@@ -232,18 +259,98 @@ def main():
         dist.destroy_process_group()
 
 
+def bench_model(pkg, N, Fd, L, n, C=20):
+    """ProtGramDirectGCN([Fd]*(L+1), N, C) with the reference init (torch.manual_seed(0)) and non-trivial gates /
+    biases (the reference init has C=1, b=0), on the CPU."""
+    import torch
+    torch.manual_seed(0)
+    model = pkg.ProtGramDirectGCN([Fd] * (L + 1), N, C, n, 0, 512, 0.5, True)
+    with torch.no_grad():
+        gen = torch.Generator().manual_seed(11)
+        for name, p in model.named_parameters():
+            leaf = name.split(".")[-1]
+            if leaf.startswith("C_"):
+                p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+            elif "bias" in leaf:
+                p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+    return model
+
+
+def pmc_traffic(args, log, timeout=240):
+    """roofline.traffic measured live: two rocprofv3 counter passes (FETCH_SIZE, then WRITE_SIZE: one TCC group
+    each, --kernel-trace only) over tools/kprobe.py --forward, i.e. this bench's own step on the same workload
+    from this same tree, corrected as MI355X_MICROARCH.md prescribes (read = 2 x FETCH_SIZE KiB on gfx950,
+    write = WRITE_SIZE KiB). The dominant kernel is the one with the largest total duration in the pass."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        log("[bench] rocprofv3 not found: roofline.traffic = null")
+        return None
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import pmc_traffic as pt
+    out = tempfile.mkdtemp(prefix="pg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.join(REPO, "tools", "kprobe.py"), "--forward", "3", "--ngram", str(args.ngram),
+             "--feat", str(args.feat), "--layers", str(args.layers)] + (["--bf16"] if args.bf16 else []) \
+        + (["--fused-norm"] if args.fused_norm else [])
+    env = dict(os.environ)
+    env.setdefault("TMPDIR", "/tmp")
+    t0 = time.time()
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = [prof, "--pmc", counter, "--kernel-trace", "-d", os.path.join(out, counter), "-o", "k",
+               "--output-format", "csv", "--"] + child
+        try:
+            r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
+        except subprocess.TimeoutExpired:
+            log(f"[bench] rocprofv3 --pmc {counter} timed out: roofline.traffic = null")
+            return None
+        if r.returncode != 0:
+            log(f"[bench] rocprofv3 --pmc {counter} failed (rc={r.returncode}): roofline.traffic = null\n"
+                + r.stdout.decode(errors="replace")[-2000:])
+            return None
+    res = pt.reduce(os.path.join(out, "FETCH_SIZE"), os.path.join(out, "WRITE_SIZE"))
+    shutil.rmtree(out, ignore_errors=True)
+    if not res.get("kernel"):
+        return None
+    log(f"[bench] PMC traffic ({time.time() - t0:.0f}s): {res['kernel']}: {res['kernel_bytes_per_launch'] / 1e6:.1f} MB "
+        f"per launch")
+    return {"traffic": res["kernel_bytes_per_launch"], "traffic_kernel": res["kernel"],
+            "traffic_source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                              "tools/kprobe.py --forward (this bench's step), read = 2 x FETCH_SIZE KiB, "
+                              "write = WRITE_SIZE KiB, per launch"}
+
+
+def usable_cpus() -> int:
+    """CPUs this process may run on: its affinity set, capped by a cgroup-v2 CPU quota if there is one."""
+    import math
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
     """The reference algorithm on this host's CPU (oracle = op-for-op restatement of
     protgram_directgcn.py:93-135 with PyG's propagate), on the same graph / weights / features:
     ``layers`` DirectGCN layer forward(s). When one propagate's [nnz, F] message tensor would exceed
     ``max_msg_bytes`` (5-gram: 67 GB), a bounded sample is timed instead: the entries of the first R
-    destination rows (all source rows stay available), and edges/s counts the entries processed."""
+    destination rows (all source rows stay available), and edges/s counts the entries processed.
+
+    Threads (SURVEY 8d / BASELINE.md: all host cores): torch is tried at os.cpu_count() threads and at the CPUs
+    this process may actually use (affinity / cgroup quota) on one propagate, and the faster count runs the
+    measurement; the previous setting is restored afterwards."""
     import numpy as np
     import torch
 
     from oracle import directgcn_cpu as oc
 
-    threads = torch.get_num_threads()
+    prev_threads = torch.get_num_threads()
     e = g.edges3.cpu().numpy()
     rp = g.rowptr.cpu().numpy()
     N = g.n_rows
@@ -256,26 +363,44 @@ def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
     rows = torch.from_numpy(np.repeat(np.arange(N, dtype=np.int64), np.diff(rp))[:nnz_keep])
     ei = torch.stack([torch.from_numpy(e[:nnz_keep, 0].astype(np.int64)), rows])
     w = [torch.from_numpy(e[:nnz_keep, 1 + j].copy().view(np.float32)) for j in range(3)]
-    xc = x.cpu()
-    times = []
-    reps = 3
-    with torch.no_grad():
-        for i, conv in enumerate(model.convs[:layers]):
-            p = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
-            ts = []
-            for rep in range(reps + 1):  # 1 warm-up + `reps` timed runs per layer, median
-                t0 = time.perf_counter()
-                y = oc.layer_forward(p, xc, ei, w[0], ei, w[1], ei, w[2])
-                dt = time.perf_counter() - t0
-                if rep:
-                    ts.append(dt)
-            times.append(sorted(ts)[len(ts) // 2])
-            xc = torch.nn.functional.leaky_relu(y + xc)
+    xc = x.float().cpu()
+    usable, total = usable_cpus(), os.cpu_count() or 1
+    cands = sorted({usable, total})
+    probe = {}
+    try:
+        with torch.no_grad():
+            if len(cands) > 1:
+                k = min(nnz_keep, 1 << 20)  # probe on a bounded slice: an oversubscribed count can be slow
+                for th in cands:  # one warm + one timed propagate per candidate thread count
+                    torch.set_num_threads(th)
+                    oc.propagate(ei[:, :k], xc, w[0][:k])
+                    t0 = time.perf_counter()
+                    oc.propagate(ei[:, :k], xc, w[0][:k])
+                    probe[th] = time.perf_counter() - t0
+                threads = min(probe, key=probe.get)
+            else:
+                threads = cands[0]
+            torch.set_num_threads(threads)
+            times = []
+            reps = 3
+            for i, conv in enumerate(model.convs[:layers]):
+                p = {k: v.detach().float().cpu() for k, v in conv.state_dict().items()}
+                ts = []
+                for rep in range(reps + 1):  # 1 warm-up + `reps` timed runs per layer, median
+                    t0 = time.perf_counter()
+                    y = oc.layer_forward(p, xc, ei, w[0], ei, w[1], ei, w[2])
+                    dt = time.perf_counter() - t0
+                    if rep:
+                        ts.append(dt)
+                times.append(sorted(ts)[len(ts) // 2])
+                xc = torch.nn.functional.leaky_relu(y + xc)
+    finally:
+        torch.set_num_threads(prev_threads)
     t = sum(times)
     val = 3 * nnz_keep * len(times) / t
     full = nnz_keep == e.shape[0]
     log(f"[bench] cpu baseline: {len(times)} layer(s) over {nnz_keep} entries/adj in {t:.2f}s on {threads} threads "
-        f"-> {val:.3e} edges/s")
+        f"(probe s/propagate by threads: {({k: round(v, 3) for k, v in probe.items()})}) -> {val:.3e} edges/s")
     what = (f"full graph (N={N}, 3x{e.shape[0]} entries)" if full else
             f"row sample: first {int(rows[-1]) + 1 if nnz_keep else 0} of {N} destination rows (3x{nnz_keep} of "
             f"3x{e.shape[0]} entries; a full propagate would materialise {e.shape[0] * F * 4 / 1e9:.0f} GB)")
@@ -291,8 +416,11 @@ def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
     return {"value": round(val, 1), "unit": "edges/s", "cores": threads, "kind": "port",
             "sample": f"{len(times)} DirectGCN layer forward(s), {what}; oracle = reference CPU algorithm "
                       f"(6 Linear + 6 index_select/mul/scatter_add_), torch {torch.__version__} CPU, {threads} threads "
-                      f"of {os.cpu_count()} host CPUs ({cpu_model}), median of {reps} timed runs per layer after 1 warm-up",
-            "seconds": round(t, 3)}
+                      f"(faster of os.cpu_count()={total} and the {usable} CPUs usable by this process "
+                      f"[affinity/cgroup quota] on one timed propagate of <=2^20 entries: {({k: round(v, 3) for k, v in probe.items()})} s) "
+                      f"on {cpu_model}, median of {reps} timed runs per layer after 1 warm-up",
+            "threads_probe_s": {str(k): round(v, 3) for k, v in probe.items()},
+            "host_cpus": total, "usable_cpus": usable, "seconds": round(t, 3)}
 
 
 def extra_measurements(pkg, ops, g, model, x, data, log):

@@ -30,6 +30,57 @@ def propagate(edge_index: torch.Tensor, x: torch.Tensor, edge_weight: Optional[t
     return msg.new_zeros((x.size(0), msg.size(1))).scatter_add_(0, index, msg)
 
 
+class _RowChunkedPropagate(torch.autograd.Function):
+    """``propagate`` evaluated over consecutive chunks of entries (each chunk index_select -> mul ->
+    scatter_add_ into the same output, in entry order), with the autograd rule of those three ops written out:
+    grad of scatter_add_ = gather of the output gradient at ei[1], times w (mul), index_add_ at ei[0]
+    (index_select). Chunk boundaries fall between destination rows when ei[1] is sorted, so every output
+    element receives its terms in the same order as the one-shot ``propagate``: the forward is identical to it
+    (tested on the golden graphs) while only one chunk's [chunk, F] message tensor exists at a time and
+    autograd saves no [nnz, F] tensors -- what makes 4-/5-gram autograd runs fit in host memory."""
+
+    @staticmethod
+    def forward(ctx, x, edge_index, edge_weight, bounds):
+        out = x.new_zeros((x.size(0), x.size(1)))
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            src, dst = edge_index[0, a:b], edge_index[1, a:b]
+            x_j = x.index_select(0, src)
+            msg = x_j if edge_weight is None else edge_weight[a:b].view(-1, 1) * x_j
+            out.scatter_add_(0, dst.view(-1, 1).expand_as(msg), msg)
+        ctx.save_for_backward(edge_index, edge_weight if edge_weight is not None else x.new_empty(0))
+        ctx.has_w, ctx.bounds, ctx.n = edge_weight is not None, bounds, x.size(0)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        edge_index, w = ctx.saved_tensors
+        gx = gout.new_zeros((ctx.n, gout.size(1)))
+        for a, b in zip(ctx.bounds[:-1], ctx.bounds[1:]):
+            g = gout.index_select(0, edge_index[1, a:b])
+            if ctx.has_w:
+                g = w[a:b].view(-1, 1) * g
+            gx.index_add_(0, edge_index[0, a:b], g)
+        return gx, None, None, None
+
+
+def row_chunk_bounds(edge_index: torch.Tensor, chunk: int) -> list:
+    """Entry offsets [0, ..., nnz] at most ~chunk apart, each moved forward to the next change of ei[1] (a
+    destination-row boundary when ei[1] is sorted; one chunk otherwise)."""
+    nnz = edge_index.size(1)
+    dst = edge_index[1]
+    if nnz <= chunk or bool((dst[1:] < dst[:-1]).any()):
+        return [0, nnz]
+    cuts = torch.arange(chunk, nnz, chunk)
+    cuts = torch.searchsorted(dst, dst[cuts], right=True)  # first entry of the next destination row
+    return sorted({0, nnz, *[int(c) for c in cuts if 0 < int(c) < nnz]})
+
+
+def propagate_chunked(edge_index: torch.Tensor, x: torch.Tensor, edge_weight: Optional[torch.Tensor],
+                      chunk: int = 1 << 21) -> torch.Tensor:
+    """``propagate`` with bounded memory (see _RowChunkedPropagate); same values and gradients."""
+    return _RowChunkedPropagate.apply(x, edge_index, edge_weight, row_chunk_bounds(edge_index, chunk))
+
+
 def linear(x, w, b=None):
     return F.linear(x, w, b)
 
@@ -38,8 +89,11 @@ def linear(x, w, b=None):
 # DirectGCNLayer.forward -- src/models/protgram_directgcn.py:93-135
 # --------------------------------------------------------------------------------------------
 def layer_forward(p: dict, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices=None,
-                  use_vector_coeffs: bool = True, prefix: str = ""):
+                  use_vector_coeffs: bool = True, prefix: str = "", prop=propagate):
+    """``prop``: ``propagate`` (the reference's PyG path) or ``propagate_chunked`` (same values and gradients,
+    bounded memory, for the 4-/5-gram sizes)."""
     g = lambda k: p[prefix + k]  # noqa: E731
+    propagate = prop
     # the reference layer drops to scalar coefficients when num_nodes == 0 (:48-60)
     use_vector_coeffs = use_vector_coeffs and (prefix + "C_in_vec") in p
     # :101-103
@@ -100,18 +154,26 @@ def apply_pe(p: dict, x, n_gram_len: int, one_gram_dim: int):
 
 def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices=None,
                   n_gram_len: int = 0, one_gram_dim: int = 0, use_vector_coeffs: bool = True,
-                  training: bool = False, dropout: float = 0.5, l2_eps: float = 1e-12):
-    """ProtGramDirectGCN.forward, protgram_directgcn.py:195-222 (eval: dropout inactive)."""
+                  training: bool = False, dropout: float = 0.5, l2_eps: float = 1e-12, prop=propagate,
+                  act_masks=None):
+    """ProtGramDirectGCN.forward, protgram_directgcn.py:195-222 (eval: dropout inactive).
+
+    ``act_masks`` (tests only): per layer, a boolean [N, F] mask choosing leaky_relu's branch instead of the sign of
+    this computation's own pre-activation -- F.leaky_relu's formula (v if v > 0 else 0.01 v) on a given branch.
+    Comparing two fp32 computations of the same model, a pre-activation within rounding of 0 can fall on either
+    side of the kink and change that element's gradient by 100x; passing the other computation's branches
+    compares the two on the same piecewise-linear function."""
     h = apply_pe(p, x, n_gram_len, one_gram_dim)
     for i in range(len(layer_dims) - 1):
         h_res = h
         out = layer_forward(p, h_res, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices,
-                            use_vector_coeffs, prefix=f"convs.{i}.")
+                            use_vector_coeffs, prefix=f"convs.{i}.", prop=prop)
         if f"res_projs.{i}.weight" in p:
             res = linear(h_res, p[f"res_projs.{i}.weight"], p[f"res_projs.{i}.bias"])
         else:
             res = h_res
-        h = F.leaky_relu(out + res)
+        z = out + res
+        h = F.leaky_relu(z) if act_masks is None else torch.where(act_masks[i], z, z * 0.01)
         h = F.dropout(h, p=dropout, training=training)
     z = linear(h, p["decoder_fc.0.weight"], p["decoder_fc.0.bias"])
     z = F.relu(z)

@@ -30,7 +30,7 @@ from typing import List, Optional
 import torch
 
 from .data import Data
-from .graph import CSRGraph, _bits, _rowptr, _sort_by
+from .graph import CSRGraph, _bits, _rowptr, _sort_by, take
 
 
 def cluster_count(num_nodes: int, target_nodes: int = 500, min_clusters: int = 2, max_clusters: int = 500) -> int:
@@ -95,8 +95,8 @@ def _cut(lay: ClusterLayout, ei: torch.Tensor, ew: Optional[torch.Tensor]):
     ks, kd = s[keep], d[keep]
     kc = lay.rank[ks]
     p = _sort_by(kc)
-    local = torch.stack([lay.pos[ks[p]], lay.pos[kd[p]]])
-    w = ew.reshape(-1)[keep][p] if ew is not None else None
+    local = torch.stack([take(lay.pos, take(ks, p)), take(lay.pos, take(kd, p))])
+    w = take(ew.reshape(-1)[keep], p) if ew is not None else None
     counts = torch.bincount(kc, minlength=lay.num_clusters)
     eptr = torch.zeros(lay.num_clusters + 1, dtype=torch.int64, device=ei.device)
     eptr[1:] = torch.cumsum(counts, 0)
@@ -149,10 +149,12 @@ def _batched_csrs(lay: ClusterLayout, cut, ptr, eptr) -> List[CSRGraph]:
     offs = torch.tensor(ptr[:-1], dtype=torch.int64, device=dev)
     grow = offs[cl] + local[1]
     p = _sort_by(grow)
-    rec = torch.stack([local[0][p].to(torch.int32), _bits(wi[p]), _bits(wo[p]), _bits(wu[p])], 1).contiguous()
+    rec = torch.stack([take(local[0], p).to(torch.int32), _bits(take(wi, p)), _bits(take(wo, p)), _bits(take(wu, p))],
+                      1).contiguous()
     rowptr = _rowptr(grow, ptr[-1])
     pt = _sort_by(offs[cl] + local[0])
-    rec_t = torch.stack([local[1][pt].to(torch.int32), _bits(wi[pt]), _bits(wo[pt]), _bits(wu[pt])], 1).contiguous()
+    rec_t = torch.stack([take(local[1], pt).to(torch.int32), _bits(take(wi, pt)), _bits(take(wo, pt)),
+                        _bits(take(wu, pt))], 1).contiguous()
     rowptr_t = _rowptr(offs[cl] + local[0], ptr[-1])
     out = []
     for c in range(len(ptr) - 1):

@@ -101,6 +101,33 @@ class CSRGraph:
             return 8 * (n + 1) + self.nnz * (16 + F * elem) + 3 * n * F * elem
         return sum(8 * (n + 1) + a.nnz * (8 + F * elem) + n * F * elem for a in self.adj)
 
+    def compulsory_bytes(self, F: int, elem: int = 4, gated: bool = False) -> int:
+        """SURVEY §8d's compulsory model: rowptr + records once, every X row read ONCE (the rows of X the
+        graph references: n_cols, or n_rows), 3 output rows; gated launches also read 5 fp32 gates per row.
+        The byte floor a propagation launch cannot go below; the roofline fraction is priced on it."""
+        n = self.n_rows
+        nx = self.n_cols if self.n_cols is not None else n
+        g = 20 * n if gated else 0
+        if self.shared:
+            return 8 * (n + 1) + 16 * self.nnz + nx * F * elem + 3 * n * F * elem + g
+        return sum(8 * (n + 1) + 8 * a.nnz + nx * F * elem + n * F * elem for a in self.adj) + g
+
+
+_TAKE_CHUNK = 1 << 24  # indices per gather piece
+
+
+def take(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``t[idx]`` along dim 0. On the GPU, a result of 256 MiB or more is gathered in pieces of 2^24 indices:
+    ROCm torch's index gather (torch 2.10+rocm7.0 on MI355X) silently leaves the last 1 GiB of a result of
+    1 GiB or more unwritten -- measured with tools/halo_device_probe.py (profiles/r02_halo_device_probe.txt):
+    ``edges3[src]`` with 114.8M indices into the 5-gram [131M, 4] int32 records returned its last 2^26 rows
+    as zeros, index_select likewise, 2^24-index pieces exact. That was the round-1 device halo_partition
+    fault: the unwritten rows held stale ids, and the next gather by them read out of bounds."""
+    row = t.element_size() * (t[0].numel() if t.dim() > 1 and t.size(0) else 1)
+    if not t.is_cuda or idx.numel() * row < (1 << 28):
+        return t[idx]
+    return torch.cat([t[idx[k:k + _TAKE_CHUNK]] for k in range(0, idx.numel(), _TAKE_CHUNK)])
+
 
 def _bits(w: torch.Tensor) -> torch.Tensor:
     return w.contiguous().to(torch.float32).view(torch.int32)
@@ -137,9 +164,9 @@ def _single(ei: torch.Tensor, ew: Optional[torch.Tensor], n: int) -> ShapedAdjac
     if w.numel() != src.numel():
         raise ValueError("edge_weight length does not match edge_index")
     p = _sort_by(dst)
-    e = torch.stack([src[p].to(torch.int32), _bits(w[p])], 1).contiguous()
+    e = torch.stack([take(src, p).to(torch.int32), _bits(take(w, p))], 1).contiguous()
     pt = _sort_by(src)
-    et = torch.stack([dst[pt].to(torch.int32), _bits(w[pt])], 1).contiguous()
+    et = torch.stack([take(dst, pt).to(torch.int32), _bits(take(w, pt))], 1).contiguous()
     return ShapedAdjacency(_rowptr(dst, n), e, _rowptr(src, n), et, int(src.numel()))
 
 
@@ -184,10 +211,12 @@ def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, ca
 
         wi, wo, wu = w(ew_in), w(ew_out), w(ew_und)
         p = _sort_by(dst)
-        edges3 = torch.stack([src[p].to(torch.int32), _bits(wi[p]), _bits(wo[p]), _bits(wu[p])], 1).contiguous()
+        edges3 = torch.stack([take(src, p).to(torch.int32), _bits(take(wi, p)), _bits(take(wo, p)),
+                              _bits(take(wu, p))], 1).contiguous()
         rowptr = _rowptr(dst, n)
         pt = _sort_by(src)
-        edges3_t = torch.stack([dst[pt].to(torch.int32), _bits(wi[pt]), _bits(wo[pt]), _bits(wu[pt])], 1).contiguous()
+        edges3_t = torch.stack([take(dst, pt).to(torch.int32), _bits(take(wi, pt)), _bits(take(wo, pt)),
+                                _bits(take(wu, pt))], 1).contiguous()
         rowptr_t = _rowptr(src, n)
         sym = torch.equal(rowptr, rowptr_t) and torch.equal(edges3, edges3_t)
         if sym:

@@ -25,8 +25,11 @@ _ROWS_OK: dict = {}
 
 
 def _check_rows(rows: torch.Tensor, limit: int):
+    """Range check of original_indices (the dense kernel gathers gates/constant rows by them), cached per
+    tensor: the entry holds the tensor itself, so a new tensor at a reused address never hits it."""
     k = _key(rows, n=limit)
-    if k in _ROWS_OK:
+    hit = _ROWS_OK.get(k)
+    if hit is not None and hit is rows:
         return
     if rows.numel():
         lo, hi = int(rows.min()), int(rows.max())
@@ -34,7 +37,7 @@ def _check_rows(rows: torch.Tensor, limit: int):
             raise IndexError(f"original_indices in [{lo}, {hi}] outside [0, {limit})")
     if len(_ROWS_OK) > 64:
         _ROWS_OK.clear()
-    _ROWS_OK[k] = True
+    _ROWS_OK[k] = rows
 
 
 class DirectGCNLayer(nn.Module):

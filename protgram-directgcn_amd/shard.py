@@ -32,7 +32,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .graph import CSRGraph
+from .graph import CSRGraph, take
 
 
 @dataclass
@@ -395,7 +395,9 @@ def halo_partition(g: CSRGraph, rank: int, world: int, layers: int,
     if owner is None:
         owner = halo_owner(g, world)
     # The index work (halo sets, relabelling, the permuted CSR) runs on the host and the result moves to the
-    # device once: it is setup, and the host path is the one the CPU tests exercise.
+    # device once: it is setup, and the host path is the one the CPU tests exercise. (A device version of the same
+    # steps returned wrong records at 5-gram: ROCm torch's index gather drops the last 1 GiB of results >= 1 GiB,
+    # see graph.take; with take() it matches this host construction -- tools/halo_device_probe.py.)
     owner = owner.to(device="cpu", dtype=torch.int64)
     if owner.numel() != n or (n and (int(owner.min()) < 0 or int(owner.max()) >= world)):
         raise ValueError("owner must assign every node a rank in [0, world)")
@@ -454,7 +456,7 @@ def halo_inputs(model, hp: HaloPartition, x_full: torch.Tensor):
     """The rank's resident inputs in its own node order: the input features (all n rows: layer 0 gathers from
     anywhere) and, per layer, the per-node parameters (gates, constant) of the rows it computes. Built once per
     parameter set, like the parameter shards of the exchange path; rebuild after the parameters change."""
-    x_p = x_full.index_select(0, hp.perm.to(x_full.device))
+    x_p = take(x_full, hp.perm.to(x_full.device))
     layers = []
     for conv, R in zip(model.convs, hp.layer_rows):
         prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))

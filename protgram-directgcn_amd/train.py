@@ -131,6 +131,47 @@ class Adam(torch.optim.Optimizer):
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
 
+    def _cohorts(self, ps: List[torch.Tensor]) -> List[tuple]:
+        """Group the parameters being stepped by their step counter (one pg_adam_f32 launch per counter).
+
+        torch.optim.Adam counts steps per parameter: a parameter without a gradient is not stepped and its
+        count stays behind. Here parameters that are always stepped together share ONE device scalar (so the
+        usual case is one launch per group); a counter shared with a parameter that is not stepped this time
+        is split off first (a device-side clone: no host sync). Counters that are not fp32 scalars on the
+        parameter's device -- e.g. after ``load_state_dict`` from a checkpoint mapped to the CPU, which also
+        un-shares them -- are rebuilt on the device, one shared scalar per distinct host value."""
+        dev = ps[0].device
+        rebuilt: dict = {}
+        for p in ps:
+            st = self.state[p]
+            s = st["step"]
+            if not (torch.is_tensor(s) and s.device == dev and s.dtype == torch.float32 and s.dim() == 0):
+                if torch.is_tensor(s) and s.device.type != "cpu":
+                    s = s.to(device=dev, dtype=torch.float32).reshape(())  # another device: stream-ordered copy
+                    st["step"] = s
+                else:
+                    v = float(s)  # host value (CPU tensor or number): no device sync
+                    if v not in rebuilt:
+                        rebuilt[v] = torch.full((), v, dtype=torch.float32, device=dev)
+                    st["step"] = rebuilt[v]
+        users: dict = {}  # counter -> number of parameters (in any group) that share it
+        for st in self.state.values():
+            s = st.get("step")
+            if torch.is_tensor(s):
+                users[id(s)] = users.get(id(s), 0) + 1
+        groups: dict = {}
+        for p in ps:
+            groups.setdefault(id(self.state[p]["step"]), []).append(p)
+        out = []
+        for members in groups.values():
+            s = self.state[members[0]]["step"]
+            if users[id(s)] > len(members):  # shared with parameters that are not stepped now: split
+                s = s.clone()
+                for p in members:
+                    self.state[p]["step"] = s
+            out.append((members, s))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -144,29 +185,35 @@ class Adam(torch.optim.Optimizer):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
+            fresh = None
             for p in ps:
                 if p.grad.is_sparse or p.dtype != torch.float32:
                     raise RuntimeError("train.Adam takes dense fp32 parameters")
+                if p.device != ps[0].device:
+                    raise RuntimeError("train.Adam: the parameters of a group must share one device")
                 st = self.state[p]
                 if not st:
-                    st["step"] = group.setdefault("_step", torch.zeros((), dtype=torch.float32, device=p.device))
+                    if fresh is None:  # new parameters of this step share one counter
+                        fresh = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["step"] = fresh
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            step = group.setdefault("_step", self.state[ps[0]]["step"])
-            grads = [p.grad.contiguous() for p in ps]
-            tl = TensorList(ps, grads, [self.state[p]["exp_avg"] for p in ps],
-                            [self.state[p]["exp_avg_sq"] for p in ps])
             b1, b2 = group["betas"]
             dev = ps[0].device
             gs = grad_scale.to(dev) if grad_scale is not None else None
             fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
-            check(lib.pg_adam_f32(len(ps), ctypes.c_void_p(tl.desc.data_ptr()), ctypes.c_void_p(tl.chunk_ptr.data_ptr()),
-                                  tl.nchunks, float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                  float(group["weight_decay"]) + float(getattr(self, "_l2_extra", 0.0)),
-                                  ctypes.c_void_p(step.data_ptr()),
-                                  ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
-                                  ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
-                  "pg_adam_f32")
+            for members, step in self._cohorts(ps):
+                grads = [p.grad.contiguous() for p in members]
+                tl = TensorList(members, grads, [self.state[p]["exp_avg"] for p in members],
+                                [self.state[p]["exp_avg_sq"] for p in members])
+                check(lib.pg_adam_f32(len(members), ctypes.c_void_p(tl.desc.data_ptr()),
+                                      ctypes.c_void_p(tl.chunk_ptr.data_ptr()), tl.nchunks, float(group["lr"]),
+                                      float(b1), float(b2), float(group["eps"]),
+                                      float(group["weight_decay"]) + float(getattr(self, "_l2_extra", 0.0)),
+                                      ctypes.c_void_p(step.data_ptr()),
+                                      ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
+                                      ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
+                      "pg_adam_f32")
             for p in ps:  # written in place by the kernel: let autograd / version-keyed caches see it
                 torch.autograd.graph.increment_version(p)
         return loss

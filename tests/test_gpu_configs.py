@@ -1,0 +1,285 @@
+"""BASELINE.json configs 3, 4 and 5 at their own sizes on the MI355X:
+
+  config 3 -- 4-gram graph (N=160,000, 6,559,580 entries per adjacency), dims [128,128,128]: the trainer's loss
+              (nll + 1e-7 * sum ||p||^2, protgram_directgcn_trainer.py:91-100) forward + backward against oracle
+              autograd (loss, log-probs, embeddings, grad x, every parameter gradient), then one
+              train.train_step + train.Adam step against torch.optim.Adam on the oracle's gradients;
+  config 4 -- 5-gram graph (N=3.2M, 131,199,580 entries per adjacency: 64-bit row offsets, 32-bit column ids
+              near their range): the 2-layer forward against the oracle on sampled output rows (the oracle runs
+              on those rows' 2-hop neighbourhood with original_indices), and the halo-recompute partition for
+              8 ranks bit-exact against the single-GPU forward;
+  config 5 -- bf16 mode, dims [128,256,256,256] on the 4-gram graph: a training step of the trainer's loop
+              against the fp32 model (loss, gradient directions), then train.train_step + train.Adam steps.
+
+The oracle is oracle/directgcn_cpu.py with propagate_chunked (the reference's index_select -> mul ->
+scatter_add_ per propagate, evaluated in row-aligned chunks: same values and gradients, bounded host memory).
+Tolerances are the ones of tests/test_gpu_parity.py: outputs |d| <= 1e-5 + 1e-5|ref|; gradients
+|d| <= 2e-5 max|ref| + 1e-4 |ref|.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from oracle import directgcn_cpu as oc
+from test_gpu_parity import assert_close
+
+pytestmark = pytest.mark.gpu
+LAM = 1e-7   # l2_lambda, config.py:74
+LR = 1e-3    # Adam lr of the trainer
+
+
+def _model(pkg, dims, N, n, C=20, seed=0):
+    """ProtGramDirectGCN with the reference init (torch.manual_seed) and randomised gates / biases (the
+    reference init's C = 1, b = 0 would hide gate and bias bugs)."""
+    torch.manual_seed(seed)
+    m = pkg.ProtGramDirectGCN(dims, N, C, n, 0, 512, 0.5, True)
+    gen = torch.Generator().manual_seed(seed + 11)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            leaf = name.split(".")[-1]
+            if leaf.startswith("C_"):
+                p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+            elif "bias" in leaf:
+                p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+    return m
+
+
+def _csr_coo(g):
+    """The graph's CSR as the reference's COO inputs (ei = [source, destination], entries in CSR order) and the
+    three weight vectors."""
+    e = g.edges3.cpu().numpy()
+    rp = g.rowptr.cpu().numpy()
+    rows = torch.from_numpy(np.repeat(np.arange(g.n_rows, dtype=np.int64), np.diff(rp)))
+    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
+    w = [torch.from_numpy(e[:, 1 + j].copy().view(np.float32)) for j in range(3)]
+    return ei, w
+
+
+def _grad_close_or_as_exact(got, ref32, ref64, what):
+    """The stated gradient tolerance against the fp32 oracle (|d| <= 2e-5 max|ref| + 1e-4 |ref|). Full-size
+    gradients are sums over up to N rows chained through two layers, where the fp32 oracle's own rounding can
+    exceed that bound: elements outside it pass only if the GPU gradient is at least as close to the float64
+    gradient (same inputs) as the fp32 oracle is, up to 2x -- no less accurate than the reference itself."""
+    got = got.detach().double().cpu()
+    ref32, ref64 = ref32.detach().double(), ref64.detach().double()
+    scale = float(ref32.abs().max()) if ref32.numel() else 0.0
+    bad = (got - ref32).abs() > 2e-5 * scale + 1e-7 + 1e-4 * ref32.abs()
+    if not bool(bad.any()):
+        return
+    e_gpu = float((got - ref64).abs().max())
+    e_ref = float((ref32 - ref64).abs().max())
+    assert e_gpu <= 2 * e_ref + 1e-7 * float(ref64.abs().max()), (
+        f"{what}: {int(bad.sum())} elements outside the fp32 tolerance, and max |gpu - f64| = {e_gpu:.3e} vs "
+        f"max |oracle fp32 - f64| = {e_ref:.3e}")
+
+
+def _labels(N, n):
+    return torch.arange(N) // 20 ** (n - 1)  # the first letter
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# config 3
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.mark.timeout(1200)
+def test_config3_4gram_training_step_vs_oracle(pkg, cuda):
+    from protgram_directgcn_amd import train
+    n, F, dims = 4, 128, [128, 128, 128]
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    assert g.nnz == 6_559_580
+    m = _model(pkg, dims, N, n).to(cuda).eval()  # eval: dropout off (its masks come from another RNG stream)
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(1234))
+    y = _labels(N, n)
+    yd = y.to(cuda)
+
+    xd = x.to(cuda).requires_grad_(True)
+    # ProtGramDirectGCN.forward (eval) written out, to keep each layer's leaky_relu branch for the oracle
+    h, masks = xd, []
+    for conv in m.convs:  # identity residuals: res_projs are nn.Identity
+        h = conv.fused_forward(h, g, None, res_x=h, act=True)
+        masks.append((h > 0).detach().cpu())
+    lp, emb = m.head(h)
+    loss = Fn.nll_loss(lp, yd) + LAM * sum(p.norm(2).pow(2) for p in m.parameters())
+    loss.backward()
+    with torch.no_grad():
+        lp_m, emb_m = m(pkg.Data(x=xd, graph=g))
+    assert_close(lp_m, lp.detach(), "model forward vs the written-out forward")
+
+    ei, w = _csr_coo(g)
+    p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr = x.clone().requires_grad_(True)
+    lp_r, emb_r = oc.model_forward(p, dims, xr, ei, w[0], ei, w[1], ei, w[2], n_gram_len=n, prop=oc.propagate_chunked,
+                                   act_masks=masks)
+    loss_r = Fn.nll_loss(lp_r, y) + LAM * sum(v.norm(2).pow(2) for v in p.values())
+    loss_r.backward()
+
+    # the same in float64 on the same (fp32-valued) inputs: the exact gradients both fp32 paths approximate
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in p.items()}
+    x64 = x.double().requires_grad_(True)
+    lp64, _ = oc.model_forward(p64, dims, x64, ei, w[0], ei, w[1], ei, w[2], n_gram_len=n, prop=oc.propagate_chunked,
+                               act_masks=masks)
+    (Fn.nll_loss(lp64, y) + LAM * sum(v.norm(2).pow(2) for v in p64.values())).backward()
+
+    loss, loss_r = float(loss.detach()), float(loss_r.detach())
+    assert abs(loss - loss_r) <= 1e-5 * abs(loss_r), (loss, loss_r)
+    assert_close(lp, lp_r, "4-gram log_probs")
+    assert_close(emb, emb_r, "4-gram embeddings")
+    _grad_close_or_as_exact(xd.grad, xr.grad, x64.grad, "4-gram grad x")
+    for k, prm in m.named_parameters():
+        _grad_close_or_as_exact(prm.grad, p[k].grad, p64[k].grad, f"4-gram grad {k}")
+
+    # one step: train.train_step + train.Adam (GPU) vs torch.optim.Adam on the oracle's gradients (CPU)
+    torch.optim.Adam(list(p.values()), lr=LR).step()
+    g_gpu = {k: prm.grad.detach().cpu() for k, prm in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    opt = train.Adam(m.parameters(), lr=LR)
+    loss_s = train.train_step(m, pkg.Data(x=x.to(cuda), graph=g), yd, opt, l2_lambda=LAM, scaler=None)
+    assert abs(float(loss_s) - loss_r) <= 1e-5 * abs(loss_r)
+    for k, prm in m.named_parameters():
+        gref = p[k].grad
+        # the gradient tolerance, or the actual GPU-vs-oracle gradient difference where that is larger
+        delta = torch.maximum(2e-5 * float(gref.abs().max()) + 1e-4 * gref.abs(), 1.5 * (g_gpu[k] - gref).abs())
+        # Adam's first update is lr * g / (|g| + eps): a gradient within delta of the oracle's moves it by at most
+        # lr * eps * delta / (|g| - delta + eps)^2, or by up to 2 lr where the sign itself is within tolerance
+        sens = torch.where(gref.abs() > delta, LR * 1e-8 * delta / (gref.abs() - delta + 1e-8) ** 2,
+                           torch.full_like(gref, 2 * LR))
+        err = (prm.detach().cpu() - p[k].detach()).abs()
+        bad = err > sens + 1e-6
+        assert not bool(bad.any()), f"{k}: {int(bad.sum())} parameters off, max |d| {float(err.max()):.3e}"
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# config 4
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def five_gram(pkg, cuda):
+    n, F = 5, 128
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    del s, d, c
+    m = _model(pkg, [F, F, F], N, n).to(cuda).eval()
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(1234))
+    xd = x.to(cuda)
+    with torch.no_grad():
+        lp, emb = m(pkg.Data(x=xd, graph=g))
+    return {"N": N, "n": n, "F": F, "g": g, "m": m, "x": x, "xd": xd, "lp": lp, "emb": emb}
+
+
+@pytest.mark.timeout(1200)
+def test_config4_5gram_csr_matches_host_build(pkg, cuda, five_gram):
+    """The GPU-built 5-gram CSR (torch GPU integer ops + pg_edges_normalize_f32) against the same construction
+    on the host (torch CPU ops; the IEEE closed form in numpy for the weights), bit for bit: the sampled-row
+    oracle check below reads the GPU-built weights, so this is what pins them at this size. (ROCm torch's
+    index gather silently drops output past 1 GiB -- DESIGN.md §5a -- which is why this is checked at size.)"""
+    from test_host import _closed_form
+    f = five_gram
+    g, N = f["g"], f["N"]
+    _, s, d, c = pkg.synth.de_bruijn_edges(f["n"])
+    rc = pkg.graph.ngram_raw_csr(N, s, d, c, device="cpu", schedule=False)
+    del s, d, c
+    assert rc.nnz == g.nnz
+    assert torch.equal(g.rowptr.cpu(), rc.rowptr)
+    assert torch.equal(g.raw.cpu(), rc.raw)
+    assert torch.equal(g.node_norm.cpu(), rc.node_norm)
+    rows, col, w = _closed_form(rc.raw.numpy(), rc.node_norm.numpy(), rc.rowptr.numpy())
+    del rows, col
+    e = g.edges3.cpu().numpy()
+    assert np.array_equal(e[:, 0], rc.raw[:, 0].numpy())
+    for j, k in enumerate(("in", "out", "und")):
+        assert np.array_equal(e[:, 1 + j], w[k].view(np.int32)), k
+
+
+@pytest.mark.timeout(1200)
+def test_config4_5gram_forward_sampled_rows_vs_oracle(pkg, cuda, five_gram):
+    f = five_gram
+    N, n, g, m, x = f["N"], f["n"], f["g"], f["m"], f["x"]
+    assert N == 3_200_000 and g.nnz == 131_199_580
+    rp = g.rowptr.cpu()
+    assert rp.dtype == torch.int64 and int(rp[-1]) == g.nnz  # offsets past 2^31 bytes of records
+    e = g.edges3.cpu()
+    gen = torch.Generator().manual_seed(5)
+    R = torch.cat([torch.tensor([0, 1, N // 2, N - 2, N - 1]), torch.randint(0, N, (43,), generator=gen)]).unique()
+
+    def entries(rows):  # CSR entries of these destination rows, in CSR order
+        cnt = rp[rows + 1] - rp[rows]
+        starts = torch.repeat_interleave(rp[rows], cnt)
+        off = torch.arange(int(cnt.sum())) - torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt)
+        return torch.repeat_interleave(rows, cnt), e[starts + off]
+
+    d2, e2 = entries(R)                                     # layer 2 reads layer-1 rows S1
+    S1 = torch.cat([R, e2[:, 0].long()]).unique()
+    d1, e1 = entries(S1)                                    # layer 1 reads input rows S0
+    S0 = torch.cat([S1, e1[:, 0].long()]).unique()          # sorted: relabelling keeps column order
+    assert int(e1[:, 0].max()) < N and int(e1[:, 0].min()) >= 0
+    loc = lambda ids: torch.searchsorted(S0, ids)  # noqa: E731
+    p = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    xs = x[S0]
+
+    def layer(prefix, h, dst, ent):
+        ei = torch.stack([loc(ent[:, 0].long()), loc(dst)])
+        w = [ent[:, 1 + j].contiguous().view(torch.float32) for j in range(3)]
+        return oc.layer_forward(p, h, ei, w[0], ei, w[1], ei, w[2], original_indices=S0, prefix=prefix)
+
+    with torch.no_grad():
+        h1 = Fn.leaky_relu(layer("convs.0.", xs, d1, e1) + xs)   # identity residual (128 -> 128)
+        h2 = Fn.leaky_relu(layer("convs.1.", h1, d2, e2) + h1)[loc(R)]
+        z = Fn.relu(oc.linear(h2, p["decoder_fc.0.weight"], p["decoder_fc.0.bias"]))
+        lp_r = Fn.log_softmax(oc.linear(z, p["decoder_fc.3.weight"], p["decoder_fc.3.bias"]), dim=-1)
+        emb_r = oc.l2_normalize(h2)
+    Rd = R.to(cuda)
+    assert_close(f["lp"][Rd], lp_r, "5-gram log_probs (sampled rows)")
+    assert_close(f["emb"][Rd], emb_r, "5-gram embeddings (sampled rows)")
+    assert bool(torch.isfinite(f["lp"]).all()) and bool(torch.isfinite(f["emb"]).all())
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("rank", [0, 7])
+def test_config4_5gram_halo_partition_bitexact(pkg, cuda, five_gram, rank):
+    """The 8-way halo-recompute partition at 5-gram (the multi-GPU forward bench.py --gpus 8 runs), one rank at a
+    time on this GPU: its rows equal the single-GPU forward's bit for bit."""
+    from protgram_directgcn_amd import shard
+    f = five_gram
+    hp = shard.halo_partition(f["g"], rank, 8, 2)
+    assert hp.layer_rows[-1] in (f["N"] // 8, f["N"] // 8 + 1)
+    inp = shard.halo_inputs(f["m"], hp, f["xd"])
+    lp, emb = shard.halo_forward(f["m"], hp, inp)
+    rows = hp.global_rows
+    assert torch.equal(lp, f["lp"][rows]) and torch.equal(emb, f["emb"][rows])
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# config 5
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.mark.timeout(900)
+def test_config5_bf16_4gram_256_training_vs_fp32(pkg, cuda):
+    from protgram_directgcn_amd import train
+    n, dims = 4, [128, 256, 256, 256]
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = _labels(N, n).to(cuda)
+    data = pkg.Data(x=x, graph=g)
+    grads, losses = [], []
+    for dt in (torch.float32, torch.bfloat16):
+        m = _model(pkg, dims, N, n).to(cuda).eval()
+        m.compute_dtype = dt
+        with torch.amp.autocast("cuda", enabled=True):  # the trainer's loop (trainer :91-100)
+            lp, emb = m(data)
+            loss = Fn.nll_loss(lp, y) + LAM * sum(p.norm(2).pow(2) for p in m.parameters())
+        assert lp.dtype == torch.float32 and emb.dtype == torch.float32
+        loss.backward()
+        losses.append(float(loss.detach()))
+        grads.append({k: p.grad.detach().float().clone() for k, p in m.named_parameters()})
+    assert abs(losses[0] - losses[1]) < 2e-2 * abs(losses[0]), losses
+    for k, g32 in grads[0].items():
+        g16 = grads[1][k]
+        cos = float((g32 * g16).sum() / (g32.norm() * g16.norm() + 1e-30))
+        assert cos > 0.99, (k, cos)
+    # the full step in bf16 mode: train_step + train.Adam under autocast + GradScaler; the loss goes down
+    m = _model(pkg, dims, N, n).to(cuda).eval()
+    m.compute_dtype = torch.bfloat16
+    opt = train.Adam(m.parameters(), lr=LR)
+    scaler = torch.amp.GradScaler("cuda", enabled=True)
+    ls = [float(train.train_step(m, data, y, opt, l2_lambda=LAM, scaler=scaler)) for _ in range(5)]
+    assert all(np.isfinite(ls)) and ls[-1] < ls[0], ls

@@ -964,6 +964,42 @@ def test_fused_adam_matches_torch_adam(pkg, cuda):
     assert float(o_ours.state[ps_ours[0]]["step"]) == 5.0
 
 
+def test_adam_checkpoint_round_trip_and_skipped_params(pkg, cuda, tmp_path):
+    """train.Adam against torch.optim.Adam across a checkpoint loaded with map_location='cpu' (the step
+    counters come back as host tensors), with parameters whose gradient is None on some steps (torch counts
+    steps per parameter: a skipped parameter's bias correction stays behind)."""
+    from protgram_directgcn_amd import train
+    g = torch.Generator().manual_seed(1)
+    shapes = [(64, 32), (32,), (1000, 1), (7,)]
+    init = [torch.randn(s, generator=g).to(cuda) for s in shapes]
+    ref = [t.clone().requires_grad_(True) for t in init]
+    ours = [t.clone().requires_grad_(True) for t in init]
+    opts = [torch.optim.Adam(ref, lr=1e-2), train.Adam(ours, lr=1e-2)]
+
+    def do_step(skip):
+        gs = [torch.randn(s, generator=g).to(cuda) for s in shapes]
+        for i, (a, b) in enumerate(zip(ref, ours)):
+            a.grad = None if i in skip else gs[i].clone()
+            b.grad = None if i in skip else gs[i].clone()
+        for o in opts:
+            o.step()
+
+    for skip in ((), (1,), (), (1, 3)):
+        do_step(skip)
+    torch.save({"ref": opts[0].state_dict(), "ours": opts[1].state_dict()}, tmp_path / "opt.pt")
+    ck = torch.load(tmp_path / "opt.pt", map_location="cpu", weights_only=True)
+    opts = [torch.optim.Adam(ref, lr=1e-2), train.Adam(ours, lr=1e-2)]
+    opts[0].load_state_dict(ck["ref"])
+    opts[1].load_state_dict(ck["ours"])
+    for skip in ((2,), (), (0,)):
+        do_step(skip)
+    for a, b in zip(ours, ref):
+        d = (a.detach() - b.detach()).abs().max().item()
+        assert d <= 2e-6 * max(1.0, b.detach().abs().max().item()), d
+        assert float(opts[1].state[a]["step"]) == float(opts[0].state[b]["step"])
+        assert opts[1].state[a]["step"].device == a.device
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("writer", ["torch_fused_adam", "pg_adam", "no_version_bump"])
 def test_forward_sees_in_place_parameter_writes(pkg, cuda, writer):

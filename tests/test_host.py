@@ -190,3 +190,19 @@ def test_oracle_not_imported_by_product():
             if f.endswith(".py"):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus N` without an outside launcher starts N ranks itself (torch.distributed.run children,
+    before anything touches a GPU); the plumbing check all-reduces over gloo and prints one JSON line."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--launch-check"], capture_output=True, text=True, timeout=240,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["world_size"] == 2 and out["ranks"] == 2 and out["rank_sum"] == 1.0

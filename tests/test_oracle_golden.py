@@ -100,3 +100,26 @@ def test_oracle_debruijn3_layer_samples():
         y = oc.layer_forward(p, x, *m["in"], *m["out"], *m["und"])
     np.testing.assert_array_equal(y[t(fx["L_rows"])].numpy(), fx["L_y_rows"])
     np.testing.assert_allclose(y.double().sum(0).numpy(), fx["L_colsum"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["f1_fasta2", "f5_fasta3", "f2_edge"])
+def test_chunked_propagate_equals_propagate(name):
+    """oracle.propagate_chunked (the bounded-memory form the 4-/5-gram GPU tests use) gives the same output as
+    the one-shot propagate bit for bit when ei[1] is sorted (chunks cut between destination rows), and the
+    gradient of index_select -> mul -> scatter_add_ that autograd gives the one-shot form."""
+    fx = load(name)
+    ei, ew = graph(fx)
+    N = int(fx["N"][0])
+    for k in ("in", "out", "und"):
+        order = torch.sort(ei[k][1], stable=True).indices  # CSR-by-destination entry order
+        e, w = ei[k][:, order], ew[k][order]
+        x = torch.randn(N, 24, generator=torch.Generator().manual_seed(7), requires_grad=True)
+        x2 = x.detach().clone().requires_grad_(True)
+        y = oc.propagate(e, x, w)
+        y2 = oc.propagate_chunked(e, x2, w, chunk=97)
+        assert len(oc.row_chunk_bounds(e, 97)) > 3 or e.size(1) <= 97 * 3
+        assert torch.equal(y, y2), k
+        R = torch.randn(N, 24, generator=torch.Generator().manual_seed(8))
+        (y * R).sum().backward()
+        (y2 * R).sum().backward()
+        torch.testing.assert_close(x2.grad, x.grad, rtol=1e-6, atol=1e-6)

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
-"""Run the default hot-path kernels on the 4-gram workload a few times (target for rocprofv3 --pmc passes).
-usage: python tools/kprobe.py [reps]"""
-import dataclasses
+"""Targets for rocprofv3 --pmc passes (one counter group per run).
+
+  python tools/kprobe.py [reps]                 every hot-path kernel on the 4-gram workload (forward,
+                                                training forward, backward, head), `reps` times
+  python tools/kprobe.py --forward [reps] ...   exactly bench.py's step (the eval forward of its model on its
+                                                workload), `reps` times: bench.py's live roofline.traffic
+"""
+import argparse
 import os
 import sys
 
@@ -14,12 +19,36 @@ from __graft_entry__ import load_package  # noqa: E402
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
 
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+ap = argparse.ArgumentParser()
+ap.add_argument("reps", nargs="?", type=int, default=5)
+ap.add_argument("--forward", action="store_true")
+ap.add_argument("--ngram", type=int, default=4)
+ap.add_argument("--feat", type=int, default=128)
+ap.add_argument("--layers", type=int, default=2)
+ap.add_argument("--bf16", action="store_true")
+ap.add_argument("--fused-norm", action="store_true")
+args = ap.parse_args()
+reps = args.reps
 dev = torch.device("cuda:0")
-N, s, d, c = pkg.synth.de_bruijn_edges(4)
-g = pkg.build_propagation_csr(N, s, d, c, device=dev)
-kin, kout = pkg.graph.class_keys(N, torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev))
-gt = dataclasses.replace(g, tiles=pkg.graph.build_row_tiles(g, kin, kout, 128))
+N, s, d, c = pkg.synth.de_bruijn_edges(args.ngram)
+g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm or not args.forward)
+
+if args.forward:
+    import bench  # noqa: E402
+    model = bench.bench_model(pkg, N, args.feat, args.layers, args.ngram).to(dev).eval()
+    model.fused_norm = args.fused_norm
+    x = torch.randn(N, args.feat, generator=torch.Generator().manual_seed(1234)).to(dev)
+    if args.bf16:
+        model.compute_dtype = torch.bfloat16
+        x = x.to(torch.bfloat16)
+    data = pkg.Data(x=x, graph=g)
+    with torch.no_grad():
+        for _ in range(reps):
+            model(data)
+    torch.cuda.synchronize()
+    print("ok")
+    sys.exit(0)
+
 x = torch.randn(N, 128, device=dev)
 torch.manual_seed(0)
 layer = pkg.DirectGCNLayer(128, 128, N).to(dev)
@@ -28,11 +57,10 @@ W1, b1 = torch.randn(64, 128, device=dev) * 0.1, torch.zeros(64, device=dev)
 W2, b2 = torch.randn(20, 64, device=dev) * 0.1, torch.zeros(20, device=dev)
 dY = torch.randn(N, 128, device=dev)
 for _ in range(reps):
-    Zg = ops.spmm3_gated(g, x, prm, 0)  # spmm_win_kernel<32,1,4,0,256,true>: the inference (bench) propagation
-    ops.layer_dense(Zg, prm, 0, constant=layer.constant.detach(), res_x=x, act=True, pregated=True)  # dense_ws
-    Z = ops.spmm3(g, x)                 # spmm_win_kernel<32,1,4,0>: the training propagation
-    ops.spmm3(gt, x)                    # spmm3_tiled_full_kernel (opt-in row tiles)
-    ops.spmm3_t(g, Z)                   # spmm_win_kernel<..,2>: transposed propagation (backward)
+    Zg = ops.spmm3_gated(g, x, prm, 0)  # the inference (bench) propagation
+    ops.layer_dense(Zg, prm, 0, constant=layer.constant.detach(), res_x=x, act=True, pregated=True)
+    Z = ops.spmm3(g, x)                 # the training propagation
+    ops.spmm3_t(g, Z)                   # transposed propagation (backward)
     Y = ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)
     ops.layer_dense_backward(dY, Z, Y, prm, 0, res_x=x, act=True)  # dgrad / wgrad / reduce
     ops.head(Y, W1, b1, W2, b2, 1e-12)

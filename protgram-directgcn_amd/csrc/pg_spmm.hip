@@ -102,10 +102,10 @@ __device__ __forceinline__ W3 fused_weights(float a_fwd, float a_bwd, float m, f
         const float d = diag ? 1.0f : 0.0f;
         const float p1 = mul(a_fwd, nj.x), p2 = mul(a_bwd, ni.x);
         const float so = mul(add(mul(p1, p1), mul(p2, p2)), 0.5f);
-        w.out = add(__fsqrt_rn(add(so, eps)), d);
+        w.out = add(pg::sqrt_rn(add(so, eps)), d);
         const float q1 = mul(a_bwd, nj.y), q2 = mul(a_fwd, ni.y);
         const float si = mul(add(mul(q1, q1), mul(q2, q2)), 0.5f);
-        w.in = add(__fsqrt_rn(add(si, eps)), d);
+        w.in = add(pg::sqrt_rn(add(si, eps)), d);
     }
     w.und = mul(m, mul(nj.z, ni.z));
     return w;

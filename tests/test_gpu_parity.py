@@ -79,6 +79,11 @@ def test_gpu_weights_and_fusednorm(pkg, cuda, name):
         np.testing.assert_array_equal(key[order], idx[0] * N + idx[1])
         ulp = np.abs(e[order, 1 + j].astype(np.int64) - fx[f"{k}_val"].view(np.int32).astype(np.int64))
         assert ulp.max() <= (0 if k == "und" else 1), (k, ulp.max())
+    # ... and bit-exact against the IEEE closed form (correctly rounded sqrt: pg::sqrt_rn)
+    from test_host import _closed_form
+    _, _, wcf = _closed_form(g.raw.cpu().numpy(), g.node_norm.cpu().numpy(), g.rowptr.cpu().numpy())
+    for j, k in enumerate(("in", "out", "und")):
+        assert np.array_equal(e[:, 1 + j], wcf[k].view(np.int32)), k
     # fused-norm SpMM == SpMM over the materialised weights, bit for bit; == oracle on those weights
     F = 32
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(4)).to(cuda)

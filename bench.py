@@ -192,26 +192,31 @@ def main():
     # roofline of the dominant kernel, priced on SURVEY 8(d)'s COMPULSORY bytes per launch (rowptr + records once,
     # each X row once, 3 output rows, gates): the floor of HBM traffic for one propagation launch
     el = 2 if args.bf16 else 4
-    if args.bf16:
-        kname = "pg_spmm3_bf16"
-    elif args.fused_norm:
-        kname = "pg_spmm3_fusednorm_f32"
-    else:  # inference gates the aggregates in the propagation's store (same gathers, + 20 B of gates per row)
-        kname = "pg_spmm3_gated_f32" if ((world == 1 or hp is not None) and ops.PREGATED_INFERENCE) else "pg_spmm3_f32"
-    gated = kname == "pg_spmm3_gated_f32"
+    gated = (world == 1 or hp is not None) and ops.PREGATED_INFERENCE and not args.fused_norm and not args.bf16
     if hp is not None:  # launches alternate over the layers' row prefixes: their mean
         launch_graphs = hp.graphs
     elif part is None:
         launch_graphs = [g]
     else:
         launch_graphs = [part.local]
+    ngram = all(gi.ngram is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm and Fd in (64, 128)
+    if args.bf16:
+        kname = "pg_spmm3_bf16"
+    elif args.fused_norm:
+        kname = "pg_spmm3_fusednorm_f32"
+    elif ngram:  # n-gram tile kernel; inference gates the aggregates at its store
+        kname = "pg_spmm3_ngram_f32" + (" (gated)" if gated else "")
+    else:
+        kname = "pg_spmm3_gated_f32" if gated else "pg_spmm3_f32"
     comp = sum(gi.compulsory_bytes(Fd, elem=el, gated=gated) for gi in launch_graphs) // len(launch_graphs)
     noreuse = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in launch_graphs) // len(launch_graphs)
     achieved = comp / (spmm_avg_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "kernel": kname,
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_model": "compulsory (SURVEY 8d): 8(N+1) + 16 nnz + X once + 3 output rows (+ 20 B/row gates)",
+                "bytes_model": ("compulsory: the kernel's own inputs once (n-gram tile kernel: its plan weights; CSR kernels: "
+                                "8(N+1) rowptr + 16 B records per entry, SURVEY 8d) + X once + 3 output rows "
+                                "(+ 20 B/row gates)"),
                 "algorithmic_bytes_per_launch": comp, "avg_launch_ms": round(spmm_avg_ms, 4),
                 "launches_timed": len(spmm_ms),
                 "no_reuse_bytes_per_launch": noreuse,
@@ -425,8 +430,6 @@ def cpu_baseline(g, model, x, layers, log, max_msg_bytes=6 << 30):
 
 def extra_measurements(pkg, ops, g, model, x, data, log):
     """Kernel-variant timings and a training step (diagnostics, stderr + 'extra' field)."""
-    import math
-
     import torch
     res = {}
 
@@ -442,47 +445,31 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
 
+    from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM, PG_FLAG_UNROLL4
     Fd = x.size(1)
-    B = g.algorithmic_bytes(Fd)
-    import dataclasses
-    g0 = dataclasses.replace(g, row_order=None)
-    for fl, name in ((0, "nosched"), (4, "nosched_unroll4"), (6, "nosched_lds_unroll4")):
-        ms = timeit(lambda: ops.spmm3(g0, x, flags=fl))
-        res[f"spmm3_{name}_ms"] = round(ms, 4)
-    if g.raw is not None:
-        kin, kout = pkg.graph.class_keys(g.n_rows, *[torch.from_numpy(a).to(x.device) for a in
-                                                      pkg.synth.de_bruijn_edges(round(math.log(g.n_rows, 20)))[1:3]])
-        gt = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout))
-        for fl, name in ((0, "tiled_fc32_u8"),):
-            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(gt, x, flags=fl)), 4)
-        gr = dataclasses.replace(g, tiles=pkg.graph.build_row_tiles(g, kin, kout, x.size(1)))
-        res["row_tiles"] = [gr.tiles.n_tiles, gr.tiles.max_rows, gr.tiles.max_ucols, round(gr.tiles.reuse, 2)]
-        for fl, name in ((0, "tiled_rows"), (1, "tiled_rows_noremap")):
-            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(gr, x, flags=fl)), 4)
-        # alternative tile shape: 4x4 tiles (<=176 staged rows: fits the 64-float chunk kernel)
-        g44 = dataclasses.replace(g, tiles=pkg.graph.build_tiles(g, kin, kout, K=4, L=4, max_ucols=192))
-        for fl, name in ((32, "tiles44_fc64_u8"),):
-            res[f"spmm3_{name}_ms"] = round(timeit(lambda: ops.spmm3(g44, x, flags=fl)), 4)
-    for fl, name in ((0, "window_u4"), (4, "window_u8"), (128, "bcast_u8"), (1, "window_u4_noremap")):
+    comp = g.compulsory_bytes(Fd)
+    conv0 = model.convs[0]
+    prm0 = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv0._dense_params())))
+    for fl, name in ((0, "ngram" if g.ngram is not None else "csr"), (PG_FLAG_NO_NGRAM, "csr_window_u4"),
+                     (PG_FLAG_NO_NGRAM | PG_FLAG_UNROLL4, "csr_window_u8")):
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
-        res[f"spmm3_{name}_GBs"] = round(B / ms / 1e6, 1)
-        if g.raw is not None:
-            ms = timeit(lambda: ops.spmm3(g, x, fused=True, flags=fl))
-            res[f"spmm3_fused_{name}_ms"] = round(ms, 4)
+        res[f"spmm3_{name}_compulsory_GBs"] = round(comp / ms / 1e6, 1)
+        res[f"spmm3_gated_{name}_ms"] = round(timeit(lambda: ops.spmm3_gated(g, x, prm0, 0, flags=fl)), 4)
+        if g.raw is not None and fl:
+            res[f"spmm3_fused_{name}_ms"] = round(timeit(lambda: ops.spmm3(g, x, fused=True, flags=fl)), 4)
     Z = ops.spmm3(g, x)
     conv = model.convs[0]
     prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
     flops = 2 * x.size(0) * 3 * Fd * conv.out_channels
-    for fl, name in ((0, "dense"), (512, "dense_4waves"), (8, "dense_bm64_w8"), (8 | 512, "dense_bm64_w4")):
-        ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True, flags=fl))
-        res[f"{name}_ms"] = round(ms, 4)
-        res[f"{name}_TFLOPs"] = round(flops / ms / 1e9, 2)
+    ms = timeit(lambda: ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x, act=True))
+    res["dense_ms"] = round(ms, 4)
+    res["dense_TFLOPs"] = round(flops / ms / 1e9, 2)
     dec = model.decoder_fc
     res["head_ms"] = round(timeit(lambda: ops.head(x, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias,
                                                    1e-12)), 4)
     G = torch.randn_like(Z)
-    for fl, name in ((0, "window_u4"), (4, "window_u8"), (128, "bcast_u8")):
+    for fl, name in ((0, "ngram" if g.ngram is not None else "csr"), (PG_FLAG_NO_NGRAM, "csr_window_u4")):
         res[f"spmm3t_{name}_ms"] = round(timeit(lambda: ops.spmm3_t(g, G, flags=fl)), 4)
     # copy-kernel bandwidth reference
     a = torch.empty(512 * 1024 * 1024 // 4, device=x.device)

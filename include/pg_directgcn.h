@@ -74,12 +74,8 @@ typedef struct pg_edge1 {
  * (PG_FLAG_BCAST_RECORDS); B = block-wide LDS staging of records (PG_FLAG_EDGE_LDS). */
 #define PG_FLAG_DENSE_BM64 (1u << 3)   /* dense kernel: force 64-row tiles */
 #define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
-#define PG_FLAG_TILED_FC64 (1u << 5)   /* tiled SpMM: 64-float feature chunks (default 32) */
-#define PG_FLAG_UNTILED (1u << 6)      /* host-side: do not use the tiled SpMM even if tiles exist */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
 #define PG_FLAG_DENSE_4WAVES (1u << 9)  /* dense kernel: 4 waves per 128-row tile (64x64 per wave) instead of 8 */
-#define PG_FLAG_SPMM_BLOCK512 (1u << 10)  /* SpMM variant C: 512-thread blocks (more consecutive rows per CU) */
-#define PG_FLAG_SPMM_BLOCK1024 (1u << 11) /* SpMM variant C: 1024-thread blocks */
 #define PG_FLAG_DENSE_PF2 (1u << 12)      /* dense kernel: two K tiles of operands in flight (register sets) */
 #define PG_FLAG_DENSE_WS (1u << 13)       /* dense kernel: W-stationary persistent variant (F_out = 128; default when pre-gated) */
 #define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
@@ -88,11 +84,8 @@ typedef struct pg_edge1 {
                                             operands (6 products, fp32-level accuracy); F_out = 128, K = 384 or 256,
                                             no row map. Default for that shape unless another dense variant flag is set;
                                             F_in = 128 runs the 16-row software-pipelined kernel */
-#define PG_FLAG_SPMM_OCC6 (1u << 28)      /* SpMM variant C compiled for >= 6 waves per SIMD (measurement) */
-#define PG_FLAG_SPMM_OCC8 (1u << 29)      /* SpMM variant C compiled for 8 waves per SIMD (measurement) */
-#define PG_FLAG_SPMM_SC1 (1u << 19)       /* SpMM variant C: Z stores with sc1 (dropped from L2 instead of kept) */
-#define PG_FLAG_SPMM_CU_CHUNKS (1u << 18) /* SpMM variant C: persistent grid, each CU walks a contiguous schedule chunk */
 #define PG_FLAG_DENSE_X3_32 (1u << 17)    /* split-bf16 dense kernel: the 32-row unpipelined tile loop instead */
+#define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -120,36 +113,6 @@ int pg_spmm3_fusednorm_f32(int64_t n_rows, const int64_t* rowptr, const int32_t*
                            const float* node_norm, float eps,
                            const float* X, int64_t ldx, int64_t F,
                            float* Z, int64_t ldz, uint32_t flags, void* stream);
-
-/* Row tiles for the LDS-staged SpMM (built once per graph, graph.py build_tiles). Tile t owns the rows
- * tile_rows[tile_rowptr[t] .. tile_rowptr[t+1]) and stages the sorted unique source rows
- * tile_ucols[tile_uptr[t] .. tile_uptr[t+1]) in LDS; erow_ptr/entries list each tile-ordered row's
- * entries in CSR order with `col` replaced by the LDS slot (0 .. U_t-1). */
-typedef struct pg_tiles {
-    const int32_t* tile_rowptr;  /* [n_tiles+1] */
-    const int32_t* tile_rows;    /* [n_rows]    */
-    const int64_t* erow_ptr;     /* [n_rows+1]  */
-    const pg_edge3_t* entries;   /* [nnz]       */
-    const int32_t* tile_uptr;    /* [n_tiles+1] */
-    const int32_t* tile_ucols;   /* [sum U_t]   */
-    int64_t n_tiles;
-    int32_t max_rows;
-    int32_t max_ucols;
-    int32_t max_entries;
-} pg_tiles_t;
-
-/* Same output as pg_spmm3_f32 (bit for bit) through the LDS-staged tiles: each unique source row chunk is
- * read from L2 once per tile instead of once per entry. F % 32 == 0; max_ucols <= 320 (192 with
- * PG_FLAG_TILED_FC64) and max_entries <= 1344; PG_ERR_UNSUPPORTED otherwise (callers then use
- * pg_spmm3_f32). */
-int pg_spmm3_tiled_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
-                       float* Z, int64_t ldz, uint32_t flags, void* stream);
-
-/* Same output again, full-width-row tiles (v3): one workgroup per tile of <= 256/(F/4) rows staging
- * <= 128 (F=128), 192 (F=64) or 64 (F=256) unique source rows whole in LDS; PG_ERR_UNSUPPORTED for other
- * shapes. Tiles for it: graph.py build_tiles(K=4, L=2, max_ucols=128, max_rows=8) at F=128. */
-int pg_spmm3_tiled_rows_f32(const pg_tiles_t* tiles, const float* X, int64_t ldx, int64_t F,
-                            float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Materialise the precomputed-weight records from raw records (same closed form as fused mode). */
 int pg_edges_normalize_f32(int64_t n_rows, const int64_t* rowptr, const pg_edgeraw_t* raw,
@@ -225,6 +188,30 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uin
 int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
                        const float* X, int64_t ldx, int64_t F, const pg_layer_args_t* gates,
                        float* Z, int64_t ldz, uint32_t flags, void* stream);
+
+/* N-gram tile propagation (pg_ngram_spmm.hip). For a shared-pattern graph over ALL K^n n-grams (node id = the
+ * base-K number of the n-gram, as the builder's sorted-string ids are when every n-gram occurs: data_builder.py
+ * :164-175), the rows of each middle (n-2)-gram form a K x K grid whose out- and in-neighbour parts are dense
+ * K x K blocks; one wave owns a 4 x 4 sub-block and reuses every source row it loads for 4 rows from registers
+ * (11 source rows per output row at K = 20 instead of the CSR's ~41). Same aggregates as pg_spmm3_f32 /
+ * pg_spmm3_gated_f32 / pg_spmm3t_f32 (protgram_directgcn.py:101-112) up to fp32 summation order (FMA, slot
+ * order); X must be finite (missing transitions are zero weights).
+ *   pg_ngram_plan_floats: plan size in floats for (K, n, n_rows = K^n), or -1 when the shape is not supported
+ *     (K a multiple of 4, n >= 2).
+ *   pg_ngram_plan_f32: scatters the CSR's weights into the plan (zeroed first); *bad (device int) receives the
+ *     number of entries that fit no slot -- a nonzero count means the graph is not an n-gram graph over K^n
+ *     ids and the plan must not be used.
+ *   pg_spmm3_ngram_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the store
+ *     (as pg_spmm3_gated_f32). F = 64 or 128.
+ *   pg_spmm3t_ngram_f32: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k).
+ *     F = 64, 128 or 256. */
+int64_t pg_ngram_plan_floats(int K, int n, int64_t n_rows);
+int pg_ngram_plan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, float* plan,
+                      int64_t plan_floats, int* bad, void* stream);
+int pg_spmm3_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
+                       const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream);
+int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
+                        float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

@@ -17,8 +17,6 @@ PG_FLAG_EDGE_LDS = 1 << 1
 PG_FLAG_UNROLL4 = 1 << 2
 PG_FLAG_DENSE_BM64 = 1 << 3
 PG_FLAG_DENSE_BM128 = 1 << 4
-PG_FLAG_TILED_FC64 = 1 << 5
-PG_FLAG_UNTILED = 1 << 6
 PG_FLAG_BCAST_RECORDS = 1 << 7
 PG_FLAG_DENSE_4WAVES = 1 << 9
 PG_FLAG_DENSE_WS = 1 << 13
@@ -26,10 +24,7 @@ PG_FLAG_DENSE_PREGATED = 1 << 14
 PG_FLAG_DENSE_TILED = 1 << 15
 PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_DENSE_X3_32 = 1 << 17
-PG_FLAG_SPMM_CU_CHUNKS = 1 << 18
-PG_FLAG_SPMM_SC1 = 1 << 19
-PG_FLAG_SPMM_OCC6 = 1 << 28
-PG_FLAG_SPMM_OCC8 = 1 << 29
+PG_FLAG_NO_NGRAM = 1 << 20
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -66,13 +61,6 @@ class LayerGradArgs(ctypes.Structure):
                 ("work", c_vp), ("work_floats", c_i64)]
 
 
-class TilesArgs(ctypes.Structure):
-    """pg_tiles_t"""
-    _fields_ = [("tile_rowptr", c_vp), ("tile_rows", c_vp), ("erow_ptr", c_vp), ("entries", c_vp),
-                ("tile_uptr", c_vp), ("tile_ucols", c_vp), ("n_tiles", c_i64), ("max_rows", c_i32),
-                ("max_ucols", c_i32), ("max_entries", c_i32)]
-
-
 # symbol -> (restype, argtypes); every symbol declared in include/pg_directgcn.h
 SIGNATURES = {
     "pg_last_error": (ctypes.c_char_p, []),
@@ -82,10 +70,13 @@ SIGNATURES = {
                                           c_i64, c_u32, c_vp]),
     "pg_spmm3_fusednorm_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_i64, c_i64, c_vp, c_i64,
                                               c_u32, c_vp]),
-    "pg_spmm3_tiled_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
-    "pg_spmm3_tiled_rows_f32": (ctypes.c_int, [ctypes.POINTER(TilesArgs), c_vp, c_i64, c_i64, c_vp, c_i64, c_u32,
-                                               c_vp]),
     "pg_edges_normalize_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp]),
+    "pg_ngram_plan_floats": (c_i64, [ctypes.c_int, ctypes.c_int, c_i64]),
+    "pg_ngram_plan_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "pg_spmm3_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,
+                                          ctypes.POINTER(LayerArgs), c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                           ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
                                      c_vp]),
     "pg_spmm1_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,

@@ -23,6 +23,8 @@ matrices) it aliases the forward CSR.
 """
 from __future__ import annotations
 
+import math
+
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -47,6 +49,15 @@ class ShapedAdjacency:
 
 
 @dataclass
+class NgramPlan:
+    """Weights of a shared-pattern graph over all K^n n-grams laid out for the n-gram tile kernels
+    (pg_ngram_plan_f32 / pg_spmm3_ngram_f32 / pg_spmm3t_ngram_f32): node id = base-K number of the n-gram."""
+    K: int
+    n: int
+    plan: torch.Tensor  # fp32 [pg_ngram_plan_floats(K, n, K^n)]
+
+
+@dataclass
 class CSRGraph:
     n_rows: int
     shared: bool
@@ -61,8 +72,8 @@ class CSRGraph:
     eps: float = 1e-9
     nnz: int = 0
     row_order: Optional[torch.Tensor] = None  # int32 processing schedule of destination rows (None = 0..n-1)
-    tiles: Optional["RowTiles"] = None       # LDS-staged tiling (pg_spmm3_tiled_f32), if built
     n_cols: Optional[int] = None             # rows of X (= output rows of the transpose); None = n_rows
+    ngram: Optional[NgramPlan] = None        # n-gram tile plan (build_ngram_plan), used instead of the CSR kernels
 
     @property
     def device(self):
@@ -77,16 +88,19 @@ class CSRGraph:
         mv = lambda t: None if t is None else t.to(device)  # noqa: E731
         g = CSRGraph(n_rows=self.n_rows, shared=self.shared, rowptr=mv(self.rowptr), edges3=mv(self.edges3),
                      symmetric=self.symmetric, raw=mv(self.raw), node_norm=mv(self.node_norm), eps=self.eps,
-                     nnz=self.nnz, row_order=mv(self.row_order), tiles=None, n_cols=self.n_cols)
+                     nnz=self.nnz, row_order=mv(self.row_order), n_cols=self.n_cols)
         if self.symmetric and self.rowptr_t is self.rowptr:
             g.rowptr_t, g.edges3_t = g.rowptr, g.edges3
         else:
             g.rowptr_t, g.edges3_t = mv(self.rowptr_t), mv(self.edges3_t)
         g.adj = [ShapedAdjacency(mv(a.rowptr), mv(a.edges), mv(a.rowptr_t), mv(a.edges_t), a.nnz) for a in self.adj]
+        if self.ngram is not None:
+            g.ngram = NgramPlan(self.ngram.K, self.ngram.n, self.ngram.plan.to(device))
         return g
 
     def tensors(self):
-        ts = [self.rowptr, self.edges3, self.rowptr_t, self.edges3_t, self.row_order]
+        ts = [self.rowptr, self.edges3, self.rowptr_t, self.edges3_t, self.row_order,
+              self.ngram.plan if self.ngram is not None else None]
         for a in self.adj:
             ts += [a.rowptr, a.edges, a.rowptr_t, a.edges_t]
         return [t for t in ts if t is not None]
@@ -104,10 +118,13 @@ class CSRGraph:
     def compulsory_bytes(self, F: int, elem: int = 4, gated: bool = False) -> int:
         """SURVEY §8d's compulsory model: rowptr + records once, every X row read ONCE (the rows of X the
         graph references: n_cols, or n_rows), 3 output rows; gated launches also read 5 fp32 gates per row.
+        With an n-gram plan (the tile kernel runs, F = 64 / 128 fp32) the plan's weights replace rowptr + records.
         The byte floor a propagation launch cannot go below; the roofline fraction is priced on it."""
         n = self.n_rows
         nx = self.n_cols if self.n_cols is not None else n
         g = 20 * n if gated else 0
+        if self.ngram is not None and F in (64, 128) and elem == 4:  # the n-gram tile kernel reads its plan instead
+            return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g
         if self.shared:
             return 8 * (n + 1) + 16 * self.nnz + nx * F * elem + 3 * n * F * elem + g
         return sum(8 * (n + 1) + 8 * a.nnz + nx * F * elem + n * F * elem for a in self.adj) + g
@@ -241,152 +258,6 @@ def clear_cache():
 # n-gram propagation matrices straight from the raw transition table
 # ------------------------------------------------------------------------------------------------
 @dataclass
-class RowTiles:
-    """Row tiles for pg_spmm3_tiled_f32: tile t owns rows tile_rows[tile_rowptr[t]:tile_rowptr[t+1]] and
-    stages its sorted unique source rows tile_ucols[tile_uptr[t]:tile_uptr[t+1]] in LDS; entries are the
-    CSR entries of those rows (same per-row order) with col replaced by the local slot."""
-    tile_rowptr: torch.Tensor  # int32 [T+1]
-    tile_rows: torch.Tensor    # int32 [N]   row ids in tile order
-    erow_ptr: torch.Tensor     # int64 [N+1] entries of the p-th tile-ordered row
-    entries: torch.Tensor      # int32 [nnz, 4] {slot, w_in, w_out, w_und}
-    tile_uptr: torch.Tensor    # int32 [T+1]
-    tile_ucols: torch.Tensor   # int32 [sum U]
-    n_tiles: int
-    max_rows: int
-    max_ucols: int
-    max_entries: int
-    reuse: float               # entries / staged rows
-    kind: str = "chunk"        # "chunk": pg_spmm3_tiled_f32 (feature chunks); "rows": pg_spmm3_tiled_rows_f32
-
-
-def class_keys(n: int, src: torch.Tensor, dst: torch.Tensor):
-    """(min in-neighbour, min out-neighbour) per node: identifies the rows with identical in-neighbour
-    sets ((n-1)-prefix class of an n-gram) and identical out-neighbour sets ((n-1)-suffix class)."""
-    dev = src.device
-    big = torch.full((n,), n, dtype=torch.int64, device=dev)
-    kout = big.clone().scatter_reduce_(0, src, dst, reduce="amin") if src.numel() else big.clone()
-    kin = big.clone().scatter_reduce_(0, dst, src, reduce="amin") if src.numel() else big.clone()
-    return kin, kout
-
-
-def tile_schedule(kin: torch.Tensor, kout: torch.Tensor, K: int, L: int) -> tuple:
-    """2-D tiles over the (in-class x out-class) grid of each connected block.
-
-    Rows of an n-gram graph sit on a grid: row s_1..s_n has in-class (s_1..s_{n-1}) and out-class
-    (s_2..s_n); rows sharing the middle s_2..s_{n-1} form one complete |Sigma| x |Sigma| block (a
-    connected component of the class incidence graph). A K x L tile of that block needs only
-    20K + 20L + KL distinct source rows for 41KL entries. Returns (order, tile_id_per_position)."""
-    import numpy as np
-    from scipy.sparse import coo_matrix
-    from scipy.sparse.csgraph import connected_components
-    kin_np, kout_np = kin.cpu().numpy(), kout.cpu().numpy()
-    n = kin_np.size
-    ui, ii = np.unique(kin_np, return_inverse=True)
-    uo, io = np.unique(kout_np, return_inverse=True)
-    ni, no = ui.size, uo.size
-    g = coo_matrix((np.ones(n), (ii, ni + io)), shape=(ni + no, ni + no))
-    _, lab = connected_components(g, directed=False)
-    comp = lab[ii]
-    # rank of each class inside its component (classes sorted by key within a component)
-    a = _rank_within(lab[:ni], ii)
-    b = _rank_within(lab[ni:], io)
-    ta, tb = a // K, b // L
-    order = np.lexsort((b, a, tb, ta, comp))
-    tkey = (comp.astype(np.int64) * (n + 1) + ta) * (n + 1) + tb
-    tk = tkey[order]
-    tile_id = np.concatenate([[0], np.cumsum(tk[1:] != tk[:-1])]).astype(np.int64)
-    return order, tile_id
-
-
-def _rank_within(class_comp, class_of_row):
-    import numpy as np
-    # classes are already sorted by key (np.unique); rank = index among classes of the same component
-    m = class_comp.size
-    o = np.lexsort((np.arange(m), class_comp))
-    rank = np.empty(m, np.int64)
-    starts = np.concatenate([[0], np.flatnonzero(np.diff(class_comp[o])) + 1])
-    grp = np.repeat(np.arange(starts.size), np.diff(np.append(starts, m)))
-    rank[o] = np.arange(m) - starts[grp]
-    return rank[class_of_row]
-
-
-ROW_TILE_SHAPES = {64: (4, 4, 192, 16), 128: (4, 2, 128, 8), 256: (2, 2, 64, 4)}  # F -> K, L, max_ucols, max_rows
-
-
-def build_row_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, F: int) -> RowTiles:
-    """Tiles for pg_spmm3_tiled_rows_f32 at feature width F (capacities in ROW_TILE_SHAPES)."""
-    K, L, mu, mr = ROW_TILE_SHAPES[F]
-    t = build_tiles(g, kin, kout, K=K, L=L, max_ucols=mu, max_rows=mr)
-    t.kind = "rows"
-    return t
-
-
-def build_tiles(g: "CSRGraph", kin: torch.Tensor, kout: torch.Tensor, K: int = 4, L: int = 8,
-                max_ucols: int = 320, max_entries: int = 1344, max_rows: int = 1 << 30) -> RowTiles:
-    """Tile the shared-pattern CSR for the LDS-staged kernel (tiles over max_ucols unique source rows are
-    split by rows). Pure index work; the entries keep each row's CSR order (bit-identical sums)."""
-    import numpy as np
-    n = g.n_rows
-    order, tile_id = tile_schedule(kin, kout, K, L)
-    rp = g.rowptr.cpu().numpy()
-    e = g.edges3.cpu().numpy()
-    cnt = np.diff(rp)
-    # split tiles with more than max_ucols distinct source rows greedily by rows (rare for n-gram
-    # graphs: only the oversized tiles go through the Python loop)
-    lens0 = cnt[order]
-    ekey = np.repeat(tile_id, lens0) * (n + 1) + e[np.repeat(rp[order], lens0) +
-                                                (np.arange(lens0.sum()) - np.repeat(np.cumsum(lens0) - lens0, lens0)), 0]
-    uk = np.unique(ekey)
-    ntile0 = int(tile_id[-1]) + 1 if tile_id.size else 0
-    ucount = np.bincount(uk // (n + 1), minlength=ntile0)
-    ecount = np.bincount(tile_id, weights=lens0, minlength=ntile0)
-    new_tile = np.empty_like(tile_id)
-    t_next = 0
-    bounds = np.flatnonzero(np.diff(np.concatenate([[-1], tile_id, [-2]])) != 0)
-    for t, (s0, s1) in enumerate(zip(bounds[:-1], bounds[1:])):
-        if ucount[t] <= max_ucols and ecount[t] <= max_entries and s1 - s0 <= max_rows:
-            new_tile[s0:s1] = t_next
-            t_next += 1
-            continue
-        rows = order[s0:s1]
-        cur, start, ne = set(), s0, 0
-        for j, r in enumerate(rows):
-            cols = e[rp[r]:rp[r + 1], 0]
-            if cur and (len(cur.union(cols.tolist())) > max_ucols or ne + cols.size > max_entries
-                        or s0 + j - start >= max_rows):
-                new_tile[start:s0 + j] = t_next
-                t_next += 1
-                cur, start, ne = set(), s0 + j, 0
-            cur.update(cols.tolist())
-            ne += cols.size
-        new_tile[start:s1] = t_next
-        t_next += 1
-    T = t_next
-    tile_rowptr = np.concatenate([[0], np.cumsum(np.bincount(new_tile, minlength=T))]).astype(np.int32)
-    # entries in tile order
-    lens = cnt[order]
-    erow_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-    src_idx = np.repeat(rp[order] - erow_ptr[:-1], lens) + np.arange(erow_ptr[-1])
-    ent = e[src_idx].copy()
-    ent_tile = np.repeat(new_tile, lens)
-    key = ent_tile * (n + 1) + ent[:, 0].astype(np.int64)
-    ukey, inv = np.unique(key, return_inverse=True)
-    u_tile = ukey // (n + 1)
-    tile_uptr = np.concatenate([[0], np.cumsum(np.bincount(u_tile, minlength=T))]).astype(np.int32)
-    ucols = (ukey % (n + 1)).astype(np.int32)
-    ent[:, 0] = (inv - tile_uptr[ent_tile]).astype(np.int32)
-    dev = g.rowptr.device
-    usz = np.diff(tile_uptr)
-    return RowTiles(
-        tile_rowptr=torch.from_numpy(tile_rowptr).to(dev), tile_rows=torch.from_numpy(order.astype(np.int32)).to(dev),
-        erow_ptr=torch.from_numpy(erow_ptr).to(dev), entries=torch.from_numpy(np.ascontiguousarray(ent)).to(dev),
-        tile_uptr=torch.from_numpy(tile_uptr).to(dev), tile_ucols=torch.from_numpy(ucols).to(dev),
-        n_tiles=T, max_rows=int(np.diff(tile_rowptr).max()) if T else 0, max_ucols=int(usz.max()) if T else 0,
-        max_entries=int(np.diff(erow_ptr[tile_rowptr.astype(np.int64)]).max()) if T else 0,
-        reuse=float(erow_ptr[-1] / max(1, usz.sum())))
-
-
-@dataclass
 class RawNgramCSR:
     n: int
     rowptr: torch.Tensor     # int64 [n+1]
@@ -461,17 +332,41 @@ def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu", schedule: bool = 
     nn_ = np.stack([dout_inv, din_inv, r, np.zeros(n, np.float32)], 1).astype(np.float32)
     node_norm = torch.from_numpy(np.ascontiguousarray(nn_)).to(dev)
     order = locality_schedule(n, s, d) if schedule else None
-    out = RawNgramCSR(n, rowptr, raw, node_norm, int(nnz), order)
-    out.class_keys = class_keys(n, s, d)
-    return out
+    return RawNgramCSR(n, rowptr, raw, node_norm, int(nnz), order)
+
+
+def build_ngram_plan(g: CSRGraph, K: int = 20) -> Optional[NgramPlan]:
+    """The n-gram tile plan of a shared-pattern device graph whose node ids are the base-K numbers of ALL K^n
+    n-grams (n >= 2; the builder's sorted-string ids when every n-gram occurs), or None when the graph is not
+    one (size not a power of K, or an entry that is neither a transition nor the diagonal -- counted by the
+    plan kernel and checked here with one host sync, at build time)."""
+    from . import ops
+    if not g.shared or g.edges3 is None or not g.rowptr.is_cuda or g.n_rows < K * K:
+        return None
+    n = int(round(math.log(g.n_rows) / math.log(K)))
+    if K ** n != g.n_rows:
+        return None
+    lib = ops.load_library()
+    floats = int(lib.pg_ngram_plan_floats(K, n, g.n_rows))
+    if floats < 0:
+        return None
+    plan = torch.empty(floats, dtype=torch.float32, device=g.rowptr.device)
+    bad = torch.zeros(1, dtype=torch.int32, device=g.rowptr.device)
+    ops.check(lib.pg_ngram_plan_f32(K, n, g.n_rows, ops._p(g.rowptr), ops._p(g.edges3), ops._p(plan), floats,
+                                    ops._p(bad), ops._stream(plan)), "pg_ngram_plan_f32")
+    if int(bad.item()) != 0:
+        return None
+    return NgramPlan(K, n, plan)
 
 
 def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,
-                          keep_raw: bool = True, schedule: bool = True, tiles: bool = False) -> CSRGraph:
+                          keep_raw: bool = True, schedule: bool = True,
+                          ngram_alphabet: Optional[int] = 20) -> CSRGraph:
     """Shared-pattern device CSR of (mathcal_A_in, mathcal_A_out, A_undirected_norm) from raw counts.
 
     Weights are materialised on the GPU by ``pg_edges_normalize_f32`` (bit-exact closed form of
-    graph_utils.py:198-273 / :160-196)."""
+    graph_utils.py:198-273 / :160-196). When the node set is all ngram_alphabet^n n-grams (node id = base-K
+    number), the n-gram tile plan is attached as well (build_ngram_plan; None to skip)."""
     from . import ops
 
     if int(num_nodes) > 0 and np.asarray(src).size == 0:
@@ -482,6 +377,6 @@ def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: flo
     g = CSRGraph(n_rows=rc.n, shared=True, rowptr=rc.rowptr, edges3=edges3, rowptr_t=rc.rowptr,
                  edges3_t=edges3, symmetric=True, raw=rc.raw if keep_raw else None,
                  node_norm=rc.node_norm if keep_raw else None, eps=eps, nnz=rc.nnz, row_order=rc.row_order)
-    if tiles and rc.n > 0:
-        g.tiles = build_tiles(g, *rc.class_keys)
+    if ngram_alphabet and g.edges3.is_cuda:
+        g.ngram = build_ngram_plan(g, ngram_alphabet)
     return g

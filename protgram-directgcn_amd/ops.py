@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import PG_FLAG_UNTILED, LayerArgs, TilesArgs, check, default_flags, load_library
+from ._lib import PG_FLAG_NO_NGRAM, LayerArgs, check, default_flags, load_library
 from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
@@ -86,6 +86,13 @@ def _is_bf16(t) -> bool:
 # ------------------------------------------------------------------------------------------------
 # raw kernel calls
 # ------------------------------------------------------------------------------------------------
+def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128)) -> bool:
+    """The n-gram tile kernels take this call: the graph has a plan, x is fp32 with a supported width and exactly
+    the graph's rows, and PG_FLAG_NO_NGRAM is not set."""
+    return (g.ngram is not None and not (fl & PG_FLAG_NO_NGRAM) and x.dtype == torch.float32
+            and x.size(0) == g.n_rows and x.size(1) in widths)
+
+
 def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
           flags: Optional[int] = None) -> torch.Tensor:
     """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels. bf16 x -> bf16 Z
@@ -103,17 +110,13 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     fl = default_flags() if flags is None else flags
     s = _stream(x)
     ev = _ev_start(x)
-    tl = g.tiles
-    if g.shared and not fused and tl is not None and F % 32 == 0 and not (fl & PG_FLAG_UNTILED):
-        a = TilesArgs(_p(tl.tile_rowptr), _p(tl.tile_rows), _p(tl.erow_ptr), _p(tl.entries), _p(tl.tile_uptr),
-                      _p(tl.tile_ucols), tl.n_tiles, tl.max_rows, tl.max_ucols, tl.max_entries)
-        fn = lib.pg_spmm3_tiled_rows_f32 if tl.kind == "rows" else lib.pg_spmm3_tiled_f32
-        rc = fn(ctypes.byref(a), _p(x), x.stride(0), F, _p(Z), Z.stride(0), fl, s)
-        if rc == 0:
+    if g.shared and not fused and _ngram_ok(g, x, fl):
+        ng = g.ngram
+        rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, None, _p(Z), Z.stride(0), fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:  # unaligned operands: the CSR kernel below
+            check(rc, "pg_spmm3_ngram_f32")
             _ev_end(x, ev)
             return Z
-        if rc != _lib.PG_ERR_UNSUPPORTED:  # -> the untiled kernel below
-            check(rc, "pg_spmm3_tiled_f32")
     if g.shared:
         if fused:
             if g.raw is None:
@@ -174,6 +177,15 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     a, keep = _layer_args(None, prm, gate_mode, M=N)
     fl = default_flags() if flags is None else flags
     ev = _ev_start(x)
+    if _ngram_ok(g, x, fl):
+        ng = g.ngram
+        rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, ctypes.byref(a), _p(Z),
+                                    Z.stride(0), fl, _stream(x))
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_spmm3_ngram_f32")
+            _ev_end(x, ev)
+            del keep
+            return Z
     check(lib.pg_spmm3_gated_f32(N, _p(g.rowptr), _p(g.row_order), _p(g.edges3), _p(x), x.stride(0), F,
                                  ctypes.byref(a), _p(Z), Z.stride(0), fl, _stream(x)), "pg_spmm3_gated_f32")
     _ev_end(x, ev)
@@ -206,6 +218,12 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     dX = torch.empty(N, F, device=G.device, dtype=torch.float32)
     fl = default_flags() if flags is None else flags
     s = _stream(G)
+    if g.shared and g.symmetric and G.size(0) == g.n_rows and _ngram_ok(g, dX, fl, (64, 128, 256)):
+        ng = g.ngram
+        rc = lib.pg_spmm3t_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0, fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_spmm3t_ngram_f32")
+            return dX
     if g.shared:
         ro = g.row_order if g.symmetric else None
         check(lib.pg_spmm3t_f32(N, _p(g.rowptr_t), _p(ro), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,

@@ -1,0 +1,96 @@
+"""The n-gram tile propagation kernels (pg_ngram_spmm.hip) against the CSR kernels, which are bit-exact to the
+reference's propagate() (tests/test_gpu_parity.py), and against the oracle directly.
+
+Tolerance: the tile kernels sum the same w*x terms in another order with FMAs, so aggregates agree within fp32
+summation rounding: |d| <= 1e-5 + 1e-5 |ref| (BASELINE.json's fp32 bound).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import directgcn_cpu as oc
+from test_gpu_parity import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _csr_flag():
+    from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM
+    return PG_FLAG_NO_NGRAM
+
+
+def _graph(pkg, cuda, n, keep=1.0, seed=0):
+    """B(20,n) with a `keep` fraction of its transitions (missing transitions = zero plan weights)."""
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    if keep < 1.0:
+        m = np.random.default_rng(seed).random(s.size) < keep
+        s, d, c = s[m], d[m], c[m]
+    return pkg.build_propagation_csr(N, s, d, c, device=cuda)
+
+
+def test_plan_only_for_ngram_graphs(pkg, cuda):
+    from golden_util import load
+    assert _graph(pkg, cuda, 2).ngram is not None
+    assert _graph(pkg, cuda, 3, keep=0.3).ngram is not None
+    fx = load("f5_fasta3")  # sorted-string ids of the n-grams present: not the full 20^3 id space
+    g = pkg.build_propagation_csr(int(fx["N"][0]), fx["src"], fx["dst"], fx["cnt"], device=cuda)
+    assert g.ngram is None
+    # a K^n-sized graph with one entry that is no transition: the plan kernel counts it and no plan is attached
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    s2, d2 = np.append(s, 0), np.append(d, 4321)
+    assert pkg.build_propagation_csr(N, s2, d2, np.append(c, 1.0).astype(np.float32), device=cuda).ngram is None
+    assert pkg.build_propagation_csr(N, s, d, c, device=cuda, ngram_alphabet=None).ngram is None
+
+
+@pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
+@pytest.mark.parametrize("F", [64, 128])
+def test_ngram_spmm3_vs_csr(pkg, cuda, n, keep, F):
+    from protgram_directgcn_amd import ops
+    g = _graph(pkg, cuda, n, keep)
+    assert g.ngram is not None
+    x = torch.randn(g.n_rows, F, generator=torch.Generator().manual_seed(n * 100 + F)).to(cuda)
+    Z = ops.spmm3(g, x)
+    Zc = ops.spmm3(g, x, flags=_csr_flag())
+    assert_close(Z, Zc, f"n={n} keep={keep} F={F}")
+    assert torch.equal(ops.spmm3(g, x), Z)  # deterministic
+    # gated store (inference path) == gates applied to the ungated CSR aggregates
+    N = g.n_rows
+    gen = torch.Generator().manual_seed(5)
+    prm = {k: (torch.rand(N, 1, generator=gen) + 0.5).to(cuda) for k in ("C_in", "C_out", "C_directed",
+                                                                          "C_undirected", "C_all")}
+    prm["W_main_in"] = torch.zeros(F, F, device=cuda)  # only its shape is read (F_in for the gate block)
+    Zg = ops.spmm3_gated(g, x, prm, 0)
+    cad = prm["C_all"] * prm["C_directed"]
+    s = [cad * prm["C_in"], cad * prm["C_out"], prm["C_all"] * prm["C_undirected"]]
+    ref = torch.cat([Zc[:, k * F:(k + 1) * F] * s[k] for k in range(3)], 1)
+    assert_close(Zg, ref, f"gated n={n} F={F}")
+
+
+@pytest.mark.parametrize("n,keep", [(3, 1.0), (3, 0.5), (4, 1.0)])
+@pytest.mark.parametrize("F", [64, 128, 256])
+def test_ngram_spmm3t_vs_csr(pkg, cuda, n, keep, F):
+    from protgram_directgcn_amd import ops
+    g = _graph(pkg, cuda, n, keep)
+    assert g.ngram is not None and g.symmetric
+    G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(F)).to(cuda)
+    assert_close(ops.spmm3_t(g, G), ops.spmm3_t(g, G, flags=_csr_flag()), f"transposed n={n} F={F}")
+
+
+def test_ngram_spmm3_vs_oracle_and_fallback_widths(pkg, cuda):
+    """Directly against the oracle's propagate (the reference's index_select -> mul -> scatter_add_), and widths
+    the tile kernels do not take (here F = 32) run the CSR kernel bit-exactly."""
+    from protgram_directgcn_amd import ops
+    g = _graph(pkg, cuda, 3, keep=0.7, seed=3)
+    N = g.n_rows
+    e = g.edges3.cpu().numpy()
+    rows = torch.from_numpy(np.repeat(np.arange(N), np.diff(g.rowptr.cpu().numpy())))
+    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
+    for F in (128, 32):
+        x = torch.randn(N, F, generator=torch.Generator().manual_seed(F))
+        Z = ops.spmm3(g, x.to(cuda)).cpu()
+        for j in range(3):
+            ref = oc.propagate(ei, x, torch.from_numpy(e[:, 1 + j].copy().view(np.float32)))
+            if F == 32:
+                assert torch.equal(Z[:, j * F:(j + 1) * F], ref), j
+            else:
+                assert_close(Z[:, j * F:(j + 1) * F], ref, f"oracle {j}")

@@ -88,7 +88,7 @@ def test_gpu_weights_and_fusednorm(pkg, cuda, name):
     F = 32
     x = torch.randn(N, F, generator=torch.Generator().manual_seed(4)).to(cuda)
     for fl in FLAG_VARIANTS:
-        Z0 = ops.spmm3(g, x, flags=fl)
+        Z0 = ops.spmm3(g, x, flags=fl | _lib_csr())
         Z1 = ops.spmm3(g, x, fused=True, flags=fl)
         assert torch.equal(Z0, Z1), fl
     src_idx = torch.from_numpy(e[:, 0].astype(np.int64))
@@ -117,11 +117,12 @@ def test_spmm3_transpose_matches_autograd(pkg, cuda, name, F):
 
 
 def test_schedule_does_not_change_results(pkg, cuda):
+    """The CSR kernels' locality schedule changes no bit (n-gram plan off: it has no schedule)."""
     import dataclasses
     from protgram_directgcn_amd import ops
     N, s, d, c = pkg.synth.de_bruijn_edges(3)
-    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
-    assert g.row_order is not None
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda, ngram_alphabet=None)
+    assert g.row_order is not None and g.ngram is None
     g0 = dataclasses.replace(g, row_order=None)
     x = torch.randn(N, 64, device=cuda)
     for fl in FLAG_VARIANTS:
@@ -238,9 +239,10 @@ def test_debruijn3_layer_samples(pkg, cuda):
     x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
     g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
     with torch.no_grad():
-        y = layer.fused_forward(x, g)
-        y_f = layer.fused_forward(x, g, fused_norm=True)
-    assert torch.equal(y, y_f)
+        y = layer.fused_forward(x, g)  # n-gram tile propagation (g.ngram)
+        y_f = layer.fused_forward(x, g, fused_norm=True)  # CSR kernel with in-kernel weights
+    assert g.ngram is not None
+    assert_close(y, y_f, "n-gram tile vs fused-norm CSR layer")
     assert_close(y[t(fx["L_rows"]).to(cuda)], fx["L_y_rows"], "3-gram sampled rows")
     np.testing.assert_allclose(y.double().sum(0).cpu().numpy(), fx["L_colsum"], rtol=1e-5, atol=1e-3)
 
@@ -279,9 +281,13 @@ def test_full_size_4gram_layer_vs_oracle(pkg, cuda, n, F):
     with torch.no_grad():
         y_ref = oc.layer_forward(p, x, ei, w[0], ei, w[1], ei, w[2])
     assert_close(y, y_ref, "4-gram layer")
-    Z = ops.spmm3(g, xd)
+    Z = ops.spmm3(g, xd, flags=_lib_csr())  # the CSR kernel: bit-exact
+    Zn = ops.spmm3(g, xd)  # the n-gram tile kernel (g.ngram): within fp32 summation-order rounding
+    assert g.ngram is not None
     for j in range(3):
-        assert torch.equal(Z[:, j * F:(j + 1) * F].cpu(), oc.propagate(ei, x, w[j])), j
+        ref = oc.propagate(ei, x, w[j])
+        assert torch.equal(Z[:, j * F:(j + 1) * F].cpu(), ref), j
+        assert_close(Zn[:, j * F:(j + 1) * F], ref, f"n-gram tile propagation {j}")
 
 
 @pytest.mark.parametrize("F,H,C", [(128, 64, 20), (128, 64, 32), (128, 64, 1), (32, 16, 5), (256, 128, 50), (16, 8, 400),
@@ -318,44 +324,6 @@ def test_model_inference_path_vs_reference(pkg, cuda, name):
         lp, emb = m(data)
     assert_close(lp, fx["M_logp"], f"{name} log_probs (no_grad)")
     assert_close(emb, fx["M_emb"], f"{name} embeddings (no_grad)")
-
-
-@pytest.mark.parametrize("graph_kind", ["debruijn3", "fasta3", "random"])
-@pytest.mark.parametrize("F", [32, 64, 128, 256])
-def test_tiled_spmm_bitexact(pkg, cuda, graph_kind, F):
-    """pg_spmm3_tiled_f32 == pg_spmm3_f32 == oracle propagate, bit for bit, all variants."""
-    from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_TILED_FC64, PG_FLAG_UNROLL4, PG_FLAG_UNTILED
-    if graph_kind == "debruijn3":
-        N, s, d, c = pkg.synth.de_bruijn_edges(3)
-        max_u = 320
-    elif graph_kind == "fasta3":
-        fx = load("f5_fasta3")
-        N, s, d, c = int(fx["N"][0]), fx["src"], fx["dst"], fx["cnt"]
-        max_u = 320
-    else:
-        rng = np.random.default_rng(7)
-        N = 2000
-        k = np.unique(rng.integers(0, N, 30000) * N + rng.integers(0, N, 30000))
-        s, d, c = k // N, k % N, rng.integers(1, 9, k.size).astype(np.float32)
-        max_u = 96  # forces the row-split path of the tiler
-    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
-    rc = pkg.graph.ngram_raw_csr(N, s, d, c, device=cuda)
-    g.tiles = pkg.graph.build_tiles(g, *rc.class_keys, max_ucols=max_u)
-    x = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda)
-    ref = ops.spmm3(g, x, flags=PG_FLAG_UNTILED)
-    for fl in (0, PG_FLAG_UNROLL4, PG_FLAG_TILED_FC64, PG_FLAG_TILED_FC64 | PG_FLAG_UNROLL4, 1):
-        assert torch.equal(ops.spmm3(g, x, flags=fl), ref), fl
-    e = g.edges3.cpu().numpy()
-    rows = torch.from_numpy(np.repeat(np.arange(N), np.diff(g.rowptr.cpu().numpy())))
-    ei = torch.stack([torch.from_numpy(e[:, 0].astype(np.int64)), rows])
-    w = torch.from_numpy(e[:, 1].copy().view(np.float32))
-    assert torch.equal(ref[:, :F].cpu(), oc.propagate(ei, x.cpu(), w))
-    if F in pkg.graph.ROW_TILE_SHAPES:  # v3 full-row tiles
-        g.tiles = pkg.graph.build_row_tiles(g, *rc.class_keys, F)
-        assert g.tiles.max_rows <= pkg.graph.ROW_TILE_SHAPES[F][3]
-        for fl in (0, 1):
-            assert torch.equal(ops.spmm3(g, x, flags=fl), ref), ("rows", fl)
 
 
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
@@ -608,7 +576,7 @@ def test_spmm3_bf16_exact(pkg, cuda, F):
         x = torch.randn(g.n_rows, F, generator=torch.Generator().manual_seed(F)).to(cuda).to(torch.bfloat16)
         Z = ops.spmm3(g, x)
         assert Z.dtype == torch.bfloat16
-        ref32 = ops.spmm3(g, x.float(), flags=_lib_untiled())
+        ref32 = ops.spmm3(g, x.float(), flags=_lib_csr())
         _assert_bf16_round(Z, ref32, (name, F))
         G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(F + 1)).to(cuda).to(torch.bfloat16)
         dX = ops.spmm3_t(g, G)
@@ -628,9 +596,9 @@ def _assert_bf16_round(got, ref32, what):
     assert same > 0.99, (what, same)
 
 
-def _lib_untiled():
-    from protgram_directgcn_amd._lib import PG_FLAG_UNTILED
-    return PG_FLAG_UNTILED
+def _lib_csr():
+    from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM
+    return PG_FLAG_NO_NGRAM
 
 
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
@@ -908,9 +876,13 @@ def test_train_step_adam_folded_l2_matches_reference_loop(pkg, cuda, amp):
                 losses.append(float(loss))
         runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-5)
-    for k, v in runs[0][1].items():  # Adam normalises each step to ~lr: compare on that scale
-        err = float((runs[1][1][k] - v).abs().max())
-        assert err <= 5e-5, (k, err)
+    for k, v in runs[0][1].items():
+        # Adam normalises each step to ~lr * sign(g): compare on that scale. An element whose gradient is within fp32
+        # noise of zero (the data term and 2*lambda*p cancelling) can step the other way in one of the two summation
+        # orders, by at most 2 lr per step; such elements must be rare
+        err = (runs[1][1][k] - v).abs()
+        assert float(err.max()) <= 3 * 2 * 1e-3 + 1e-6, (k, float(err.max()))
+        assert int((err > 5e-5).sum()) <= max(1, err.numel() // 10000), (k, int((err > 5e-5).sum()))
 
 
 def test_multi_tensor_helpers(pkg, cuda):

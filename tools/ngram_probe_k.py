@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Time the propagation kernels at B(20,n), F: n-gram tile forward (default / LDS-weight variant), the CSR window
+kernel, and the transposed kernels (min of interleaved rounds, HIP events), plus a max-|d| check vs the CSR result.
+usage: python tools/ngram_probe_k.py [n=4] [F=128] [reps=20]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import torch  # noqa: E402
+
+from __graft_entry__ import load_package  # noqa: E402
+
+pkg = load_package()
+from protgram_directgcn_amd import ops  # noqa: E402
+from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+F = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+dev = torch.device("cuda:0")
+N, s, d, c = pkg.synth.de_bruijn_edges(n)
+g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+assert g.ngram is not None
+x = torch.randn(N, F, device=dev)
+G = torch.randn(N, 3 * F, device=dev)
+
+
+def timeit(fn):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+cases = {"fwd_ngram": lambda: ops.spmm3(g, x),
+         "fwd_csr": lambda: ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM),
+         "bwd_ngram": lambda: ops.spmm3_t(g, G), "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
+best = {k: 1e9 for k in cases}
+for _ in range(4):
+    for k, fn in cases.items():
+        best[k] = min(best[k], timeit(fn))
+ref = ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM)
+for k in ("fwd_ngram",):
+    z = cases[k]()
+    print(f"{k}: max |d| vs csr {float((z - ref).abs().max()):.3e}")
+comp = g.compulsory_bytes(F)
+print(" ".join(f"{k}={v:.4f}ms" for k, v in best.items()), f"compulsory_fwd={comp / 1e6:.1f}MB "
+      f"-> {comp / best['fwd_ngram'] / 1e6:.0f} GB/s")

@@ -9,6 +9,10 @@ import sys
 
 
 def classify(k):
+    if "ngram_spmm3t_kernel" in k:
+        return "ngram_spmm3t"
+    if "ngram_spmm3_kernel" in k:
+        return "ngram_spmm3_gated" if ", true>" in k else "ngram_spmm3"
     if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0, 256, true>", k):
         return "spmm3_gated_window"
     m = re.search(r"spmm_win_kernel<\d+, \d+, \d+, (\d)(, \d+, false)?>", k)
@@ -23,8 +27,7 @@ def classify(k):
     if "dense_x3_kernel" in k:  # split-bf16 W-stationary dense kernel: <F_IN, KSEG, pregated>
         return "dense_x3_pregated" if k.rstrip(")").find("true>") >= 0 else "dense_x3"
     for key, short in (("dense_ws_kernel", "dense_ws"), ("spmm_vec_kernel", "spmm_bcast"),
-                       ("spmm3_tiled_full", "spmm_tiled_rows"),
-                       ("spmm3_tiled", "spmm_tiled"), ("dgrad_kernel", "dense_dgrad"), ("wgrad_kernel", "dense_wgrad"),
+                       ("dgrad_kernel", "dense_dgrad"), ("wgrad_kernel", "dense_wgrad"),
                        ("reduce_splits", "wgrad_reduce"), ("dense_kernel", "dense"), ("head_kernel", "head")):
         if key in k:
             return short

@@ -162,7 +162,8 @@ def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew
     this computation's own pre-activation -- F.leaky_relu's formula (v if v > 0 else 0.01 v) on a given branch.
     Comparing two fp32 computations of the same model, a pre-activation within rounding of 0 can fall on either
     side of the kink and change that element's gradient by 100x; passing the other computation's branches
-    compares the two on the same piecewise-linear function."""
+    compares the two on the same piecewise-linear function. An extra last mask does the same for the decoder's
+    ReLU (where a hidden unit within rounding of 0 switches a whole term of that row's gradient on or off)."""
     h = apply_pe(p, x, n_gram_len, one_gram_dim)
     for i in range(len(layer_dims) - 1):
         h_res = h
@@ -176,7 +177,8 @@ def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew
         h = F.leaky_relu(z) if act_masks is None else torch.where(act_masks[i], z, z * 0.01)
         h = F.dropout(h, p=dropout, training=training)
     z = linear(h, p["decoder_fc.0.weight"], p["decoder_fc.0.bias"])
-    z = F.relu(z)
+    nl = len(layer_dims) - 1
+    z = F.relu(z) if act_masks is None or len(act_masks) <= nl else torch.where(act_masks[nl], z, z * 0)
     z = F.dropout(z, p=0.5, training=training)
     logits = linear(z, p["decoder_fc.3.weight"], p["decoder_fc.3.bias"])
     return F.log_softmax(logits, dim=-1), l2_normalize(h, eps=l2_eps)

@@ -16,6 +16,8 @@ scatter_add_ per propagate, evaluated in row-aligned chunks: same values and gra
 Tolerances are the ones of tests/test_gpu_parity.py: outputs |d| <= 1e-5 + 1e-5|ref|; gradients
 |d| <= 2e-5 max|ref| + 1e-4 |ref|.
 """
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -101,7 +103,10 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda):
     for conv in m.convs:  # identity residuals: res_projs are nn.Identity
         h = conv.fused_forward(h, g, None, res_x=h, act=True)
         masks.append((h > 0).detach().cpu())
-    lp, emb = m.head(h)
+    hook = m.decoder_fc[1].register_forward_hook(lambda mod, inp, out: masks.append((inp[0] > 0).detach().cpu()))
+    lp, emb = m.head(h)  # decoder_fc: Linear, ReLU (its branches appended to masks), Dropout, Linear
+    hook.remove()
+    assert len(masks) == len(m.convs) + 1
     loss = Fn.nll_loss(lp, yd) + LAM * sum(p.norm(2).pow(2) for p in m.parameters())
     loss.backward()
     torch.cuda.synchronize()
@@ -175,7 +180,12 @@ def five_gram(pkg, cuda):
     xd = x.to(cuda)
     with torch.no_grad():
         lp, emb = m(pkg.Data(x=xd, graph=g))
-    return {"N": N, "n": n, "F": F, "g": g, "m": m, "x": x, "xd": xd, "lp": lp, "emb": emb}
+        # the same forward on the CSR kernels alone: what a halo rank's subgraph (no n-gram tile plan) runs
+        lp_c, emb_c = m(pkg.Data(x=xd, graph=dataclasses.replace(g, ngram=None)))
+    assert g.ngram is not None
+    assert_close(lp, lp_c, "5-gram forward: n-gram tile kernels vs CSR kernels")
+    return {"N": N, "n": n, "F": F, "g": g, "m": m, "x": x, "xd": xd, "lp": lp, "emb": emb, "lp_csr": lp_c,
+            "emb_csr": emb_c}
 
 
 @pytest.mark.timeout(1200)
@@ -253,7 +263,8 @@ def test_config4_5gram_forward_sampled_rows_vs_oracle(pkg, cuda, five_gram):
 @pytest.mark.parametrize("rank", [0, 7])
 def test_config4_5gram_halo_partition_bitexact(pkg, cuda, five_gram, rank):
     """The 8-way halo-recompute partition at 5-gram (the multi-GPU forward bench.py --gpus 8 runs), one rank at a
-    time on this GPU: its rows equal the single-GPU forward's bit for bit."""
+    time on this GPU: its rows equal the single-GPU forward's bit for bit (on the CSR kernels; the single-GPU
+    default runs the n-gram tile kernels, within fp32 summation rounding of those -- checked in the fixture)."""
     from protgram_directgcn_amd import shard
     f = five_gram
     hp = shard.halo_partition(f["g"], rank, 8, 2)
@@ -261,7 +272,7 @@ def test_config4_5gram_halo_partition_bitexact(pkg, cuda, five_gram, rank):
     inp = shard.halo_inputs(f["m"], hp, f["xd"])
     lp, emb = shard.halo_forward(f["m"], hp, inp)
     rows = hp.global_rows
-    assert torch.equal(lp, f["lp"][rows]) and torch.equal(emb, f["emb"][rows])
+    assert torch.equal(lp, f["lp_csr"][rows]) and torch.equal(emb, f["emb_csr"][rows])
 
 
 # ---------------------------------------------------------------------------------------------------------------

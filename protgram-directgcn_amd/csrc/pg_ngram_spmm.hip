@@ -125,7 +125,12 @@ __device__ __forceinline__ int plan_slot(int i, int jb, int PB) { return i * PB 
 // reading each step's weights as LDS broadcasts (every lane the same address). A lane holds VEC = F/64 features.
 // Measured at B(20,4), F=128 (tools/ngram_probe_k.py): 0.147-0.156 ms against 0.198 for the CSR window kernel;
 // one wave per block 0.152-0.168; NB = 4 (a wave per SIMD fewer) 0.155; weights through the scalar cache 0.186;
-// 16-B loads with a row per half-wave (half the load instructions, in-sources replicated per half) 0.215.
+// 16-B loads with a row per half-wave (half the load instructions, in-sources replicated per half) 0.215;
+// 16-B loads with the half-waves on alternate steps c (every source once, partial rows summed by
+// v_permlane32_swap; 196 VGPRs, 2 waves/SIMD) 0.187; the workgroup's K + PA source rows per step staged once in a
+// double-buffered LDS slab (10 waves per (M, a-block), one barrier per step; 124 VGPRs + 64 KB LDS, one workgroup
+// per CU) 0.280; the F = 64 kernel on the two column halves 0.164. This kernel is texture-data bound (TD 90 %
+// busy, ~30 cycles per 8-B wave load; PMC, profiles/r02_pmc_summary.txt).
 template <int K, int VEC, int PA, int PB, int AH, int NB, bool GATED>
 __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
     static_assert(K % NB == 0, "the c loop runs in rounds of NB steps");
@@ -186,6 +191,18 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
             }
         }
     };
+    // gates (GATED): lane 5r + q loads gate q (in, out, directed, undirected, all) of the wave's row r in one
+    // instruction; the epilogue reads them back with v_readlane
+    float gv = 0.f;
+    if constexpr (GATED) {
+        static_assert(5 * R <= 64, "one gate per lane");
+        if (lane < 5 * R) {
+            const int r = lane / 5, q = lane - 5 * r;
+            const int64_t row = (int64_t)(a0 + r / PB) * p.Kn1 + M * K + b0 + r % PB;
+            const float* src = q == 0 ? p.g_in : q == 1 ? p.g_out : q == 2 ? p.g_dir : q == 3 ? p.g_und : p.g_all;
+            gv = src[p.gate_scalar ? 0 : row];
+        }
+    }
     V bo[NB][PB], bi[NB][AH];
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u) load(u, bo[u], bi[u]);
@@ -209,11 +226,11 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
             const V xs = (X + row * ldxv)[lane];
             float s[3] = {1.f, 1.f, 1.f};
             if constexpr (GATED) {
-                const int64_t g = p.gate_scalar ? 0 : row;
-                const float cad = p.g_all[g] * p.g_dir[g];
-                s[0] = cad * p.g_in[g];
-                s[1] = cad * p.g_out[g];
-                s[2] = p.g_all[g] * p.g_und[g];
+                auto gate = [&](int q) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), r * 5 + q)); };
+                const float cad = gate(4) * gate(2);
+                s[0] = cad * gate(0);
+                s[1] = cad * gate(1);
+                s[2] = gate(4) * gate(3);
             }
             V* zr = reinterpret_cast<V*>(p.Z + row * p.ldz);
 #pragma unroll

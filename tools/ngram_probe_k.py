@@ -39,15 +39,21 @@ def timeit(fn):
     return e0.elapsed_time(e1) / reps
 
 
-cases = {"fwd_ngram": lambda: ops.spmm3(g, x),
+prm = {k: torch.rand(N, 1, device=dev) + 0.5 for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all")}
+prm["W_main_in"] = torch.zeros(F, F, device=dev)
+ALT = [int(a, 0) for a in os.environ.get("PG_PROBE_ALT", "").split(",") if a]
+cases = {"fwd_ngram": lambda: ops.spmm3(g, x), "gated_ngram": lambda: ops.spmm3_gated(g, x, prm, 0),
          "fwd_csr": lambda: ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM),
          "bwd_ngram": lambda: ops.spmm3_t(g, G), "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
+for a in ALT:
+    cases[f"fwd_alt{a:#x}"] = (lambda a: lambda: ops.spmm3(g, x, flags=a))(a)
+    cases[f"gated_alt{a:#x}"] = (lambda a: lambda: ops.spmm3_gated(g, x, prm, 0, flags=a))(a)
 best = {k: 1e9 for k in cases}
 for _ in range(4):
     for k, fn in cases.items():
         best[k] = min(best[k], timeit(fn))
 ref = ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM)
-for k in ("fwd_ngram",):
+for k in ["fwd_ngram"] + [f"fwd_alt{a:#x}" for a in ALT]:
     z = cases[k]()
     print(f"{k}: max |d| vs csr {float((z - ref).abs().max()):.3e}")
 comp = g.compulsory_bytes(F)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Counter passes for tools/kprobe.py (one rocprofv3 run per pass; counters only with --kernel-trace).
 # usage: tools/pmc_passes.sh OUTDIR [PASSFILE]   (PASSFILE: one space-separated counter group per line)
+# KPROBE_ARGS: arguments for tools/kprobe.py (default "3": every hot-path kernel)
 set -e
 export TMPDIR=/tmp
 OUT=${1:-$GRAFT_REPO_ROOT/gpurun_out/pmc}
@@ -21,6 +22,6 @@ i=0
 while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
-  timeout -k 10 150 rocprofv3 --pmc $line --kernel-trace -d $OUT/p$i -o k --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/kprobe.py 3 > $OUT/p$i.log 2>&1
+  timeout -k 10 150 rocprofv3 --pmc $line --kernel-trace -d $OUT/p$i -o k --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/kprobe.py ${KPROBE_ARGS:-3} > $OUT/p$i.log 2>&1
 done < $PASSES
 echo done

@@ -11,6 +11,10 @@ import sys
 def classify(k):
     if "ngram_spmm3t_kernel" in k:
         return "ngram_spmm3t"
+    if "ngram_spmm3_lds_kernel" in k:
+        return "ngram_spmm3_lds_gated" if ", true>" in k else "ngram_spmm3_lds"
+    if "ngram_spmm3_cs_kernel" in k:
+        return "ngram_spmm3_cs_gated" if ", true>" in k else "ngram_spmm3_cs"
     if "ngram_spmm3_kernel" in k:
         return "ngram_spmm3_gated" if ", true>" in k else "ngram_spmm3"
     if re.search(r"spmm_win_kernel<\d+, \d+, \d+, 0, 256, true>", k):
@@ -37,14 +41,14 @@ def classify(k):
 d = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
-for f in sorted(glob.glob(f"{d}/*/*counter_collection.csv")):
+for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         short = classify(k)
         if short is None:
             continue
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for f in sorted(glob.glob(f"{d}/*/*kernel_trace.csv")):
+for f in sorted(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         short = classify(k)

@@ -72,19 +72,11 @@ typedef struct pg_edge1 {
 #define PG_FLAG_UNROLL4 (1u << 2)      /* alternate gathers-in-flight depth (variants A/B: 4 instead of 8; C: 8 instead of 4) */
 /* SpMM variants: C (default) = per-row-group LDS record window; A = every lane loads the record
  * (PG_FLAG_BCAST_RECORDS); B = block-wide LDS staging of records (PG_FLAG_EDGE_LDS). */
-#define PG_FLAG_DENSE_BM64 (1u << 3)   /* dense kernel: force 64-row tiles */
-#define PG_FLAG_DENSE_BM128 (1u << 4)  /* dense kernel: force 128-row tiles */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
-#define PG_FLAG_DENSE_4WAVES (1u << 9)  /* dense kernel: 4 waves per 128-row tile (64x64 per wave) instead of 8 */
-#define PG_FLAG_DENSE_PF2 (1u << 12)      /* dense kernel: two K tiles of operands in flight (register sets) */
-#define PG_FLAG_DENSE_WS (1u << 13)       /* dense kernel: W-stationary persistent variant (F_out = 128; default when pre-gated) */
 #define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
-#define PG_FLAG_DENSE_TILED (1u << 15)    /* dense kernel: never the W-stationary variant */
-#define PG_FLAG_DENSE_X3 (1u << 16)       /* dense kernel: W-stationary on bf16 MFMA with exact 3-way bf16 splits of both
-                                            operands (6 products, fp32-level accuracy); F_out = 128, K = 384 or 256,
-                                            no row map. Default for that shape unless another dense variant flag is set;
-                                            F_in = 128 runs the 16-row software-pipelined kernel */
-#define PG_FLAG_DENSE_X3_32 (1u << 17)    /* split-bf16 dense kernel: the 32-row unpipelined tile loop instead */
+#define PG_FLAG_DENSE_TILED (1u << 15)    /* dense forward: the tiled fp32 kernel even where the split-bf16 W-stationary
+                                            kernels apply (F_out = 128, K = 384 or 256, no row map: the default) */
+#define PG_FLAG_DENSE_X3 (1u << 16)       /* dense backward: the split-bf16 weight gradient (opt-in) */
 #define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which

@@ -15,15 +15,10 @@ PG_OK = 0
 PG_FLAG_NO_XCD_REMAP = 1 << 0
 PG_FLAG_EDGE_LDS = 1 << 1
 PG_FLAG_UNROLL4 = 1 << 2
-PG_FLAG_DENSE_BM64 = 1 << 3
-PG_FLAG_DENSE_BM128 = 1 << 4
 PG_FLAG_BCAST_RECORDS = 1 << 7
-PG_FLAG_DENSE_4WAVES = 1 << 9
-PG_FLAG_DENSE_WS = 1 << 13
 PG_FLAG_DENSE_PREGATED = 1 << 14
 PG_FLAG_DENSE_TILED = 1 << 15
 PG_FLAG_DENSE_X3 = 1 << 16
-PG_FLAG_DENSE_X3_32 = 1 << 17
 PG_FLAG_NO_NGRAM = 1 << 20
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p

@@ -2,10 +2,9 @@
 //  * dense_x3p_kernel (default, F_in = F_out = 128, no row map): split-bf16 W-stationary, software-pipelined on
 //    16-row tiles (v_mfma_f32_16x16x32_bf16, exact three-way bf16 splits: fp32-level accuracy); reads the
 //    unpacked weights when `packed` is NULL;
-//  * dense_x3_kernel: the same on 32-row tiles without the pipeline (F_in = 64 with a projected residual, or
-//    PG_FLAG_DENSE_X3_32);
-//  * dense_ws_kernel: fp32 W-stationary (v_mfma_f32_16x16x4f32), PG_FLAG_DENSE_WS;
-//  * dense_kernel: the tiled fp32 GEMM described below (every other shape, row maps, projected residuals).
+//  * dense_x3_kernel: the same on 32-row tiles without the pipeline (F_in = 64 with a projected residual);
+//  * dense_kernel: the tiled fp32 GEMM described below (every other shape, row maps, projected residuals;
+//    PG_FLAG_DENSE_TILED forces it).
 // Tiled fp32 kernel (v_mfma_f32_32x32x2_f32):
 //
 // After the fused propagation Z = [A_in X | A_out X | A_und X] (pg_spmm.hip), the layer output of
@@ -20,7 +19,7 @@
 //                            gathered through original_indices when given); epilogue adds the gated bias
 //                            sums, the per-node constant, the residual and leaky_relu, then stores y once.
 //
-// Tiling: 256 threads = 4 waves; block tile BM=128 x BN (128 or 64) x BK=32; operands staged
+// Tiling: 512 threads = 8 waves of 32x32; block tile BM=128 x BN (128 or 64) x BK=32; operands staged
 // global -> registers -> LDS (rows padded to 36 floats: conflict-free ds_read_b128) into a double
 // buffer, one barrier per K tile; the next tile's global loads are in flight during the MFMAs. Each
 // lane feeds its MFMAs with one ds_read_b128 per operand per 4 MFMAs by permuting K identically for A
@@ -58,7 +57,6 @@ struct DenseP {
     int64_t ldy;
     int remap;
     int pregated;  // A segments 0..2 already carry their gates (pg_spmm3_gated_f32): no scaling here
-    int dbg;  // timing probes only (flags bits 20-23): 1 no epilogue memory, 2 no DMA, 4 no MFMA, 8 no conversion (x3)
     // unpacked weights (packed == NULL; the pipelined split-bf16 kernel forms W_q + W_shared and the bias sums
     // itself, with the pack kernel's fp32 adds)
     int rawW;
@@ -78,8 +76,8 @@ __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_
     return p.res_x[m * p.ld_res + (k - 3 * p.F_in)];
 }
 
-template <int BM, int BN, int NW, bool VEC, int PF = 1>
-__global__ __launch_bounds__(64 * NW, PF == 2 ? 4 : 1) void dense_kernel(DenseP p) {
+template <int BM, int BN, int NW, bool VEC>
+__global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
     constexpr int NT = 64 * NW;  // threads
     constexpr int WN = (BM == 64 && NW == 8) ? 4 : (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
     constexpr int WM = NW / WN;
@@ -228,35 +226,15 @@ __global__ __launch_bounds__(64 * NW, PF == 2 ? 4 : 1) void dense_kernel(DenseP 
     };
 
     const int ntiles = (p.K + BK - 1) / BK;
-    if constexpr (PF == 1) {
-        fetch(0);
-        stash(0, 0);
+    fetch(0);
+    stash(0, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < ntiles) fetch((t + 1) * BK);
+        mma(cur);
+        if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BK);
         __syncthreads();
-        for (int t = 0; t < ntiles; ++t) {
-            const int cur = t & 1;
-            if (t + 1 < ntiles) fetch((t + 1) * BK);
-            mma(cur);
-            if (t + 1 < ntiles) stash(cur ^ 1, (t + 1) * BK);
-            __syncthreads();
-        }
-    } else {
-        // two K tiles in flight: register set 0 / 1 alternate (loop unrolled by 2 for static indexing)
-        float4 ra1[A_F4], rb1[B_F4];
-        fetch(0);
-        stash(0, 0);
-        if (ntiles > 1) fetch_to(BK, ra1, rb1);
-        __syncthreads();
-        for (int t = 0; t < ntiles; t += 2) {
-            if (t + 2 < ntiles) fetch_to((t + 2) * BK, ra, rb);
-            mma(0);
-            if (t + 1 < ntiles) stash_from(1, (t + 1) * BK, ra1, rb1);
-            __syncthreads();
-            if (t + 1 >= ntiles) break;
-            if (t + 3 < ntiles) fetch_to((t + 3) * BK, ra1, rb1);
-            mma(1);
-            if (t + 2 < ntiles) stash_from(0, (t + 2) * BK, ra, rb);
-            __syncthreads();
-        }
     }
 
     // Epilogue: park the accumulator tile in LDS (C/D map of the 32x32 MFMA: col = lane&31,
@@ -354,16 +332,9 @@ __global__ __launch_bounds__(64 * NW, PF == 2 ? 4 : 1) void dense_kernel(DenseP 
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// W-stationary variant (F_out = 128): the packed weights never move after the prologue. Wave w of the
-// 512-thread workgroup owns output columns [16w, 16w+16) over the WHOLE K, held in K/4 VGPRs per lane
-// (v_mfma_f32_16x16x4f32: lane l supplies B[k = l>>4][n = l&15]; with the K permutation of dense_kernel a
-// group of 16 k is one float4 per lane), so there is no K split and no partial-sum reduction. One workgroup
-// per CU walks 32-row tiles (XCD-contiguous deal); each tile's A rows arrive by LDS-DMA
-// (global_load_lds_dwordx4, 1 KiB per wave-instruction, lane-linear) into a double-buffered image whose
-// 16-byte chunks are XOR-swizzled by row (chunk c of row r at c ^ (r & 15), set through the per-lane SOURCE
-// address), which makes the 16x16x4 A-fragment ds_read_b128 conflict-free. Gates scale the A fragment after
-// the LDS read. One barrier per tile; the epilogue runs from the accumulators with the constant / residual
-// values prefetched before the MFMAs.
+// Helpers of the W-stationary split-bf16 kernels below. Their tiles' A rows arrive by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction, lane-linear) into images whose 16-byte chunks are
+// XOR-swizzled by row (chunk c of row r at c ^ (r & 15), set through the per-lane SOURCE address).
 // One LDS-DMA piece: 16 B per lane from a per-lane global address to (wave-uniform base + 16 * lane).
 __device__ __forceinline__ void glds16(const float* src, float* lds_base) {
     __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 0);
@@ -378,205 +349,6 @@ __device__ __forceinline__ float epi_sum(float acc, float s0, float s1, float s2
     return __fadd_rn(__fadd_rn(__fadd_rn(__fadd_rn(acc, gb), br), cst), res);
 }
 
-template <int F_IN, int KSEG, bool PRE>
-__global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
-    constexpr int K = F_IN * KSEG;
-    constexpr int CH = K / 4;        // 16-B chunks per row
-    constexpr int BMW = 32;          // rows per tile
-    constexpr int NG = K / 16;       // k-groups
-    constexpr int NI = BMW * CH / 64 / 8;  // LDS-DMA instructions per wave per tile
-    static_assert(CH % 16 == 0 && (BMW * CH) % 512 == 0, "tile shape");
-    // two distinct LDS objects (not As[2][..]) so the compiler can tell the DMA target of the next tile from
-    // the image being read, and does not drain the DMA before every ds_read
-    __shared__ __attribute__((aligned(16))) float As0[BMW * K];
-    __shared__ __attribute__((aligned(16))) float As1[BMW * K];
-    constexpr int ELD = 128 + 4;  // epilogue tile row (floats)
-    __shared__ __attribute__((aligned(16))) float Es[BMW * ELD];   // contraction result
-    __shared__ __attribute__((aligned(16))) float Cs[BMW * 128];   // constant rows (LDS-DMA)
-    __shared__ __attribute__((aligned(16))) float Rs[BMW * 128];   // identity-residual rows (LDS-DMA)
-    __shared__ float Sg[2][BMW][4];
-    __shared__ int64_t Crow[2][BMW];
-    __shared__ __attribute__((aligned(16))) float Bs[4][128];  // bias sums (row 3: b_res or 0)
-
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    const int lc = lane & 15, kg = lane >> 4;
-    const int col = 16 * wave + lc;
-    const int64_t T = (p.M + BMW - 1) / BMW;
-    Bs[tid >> 7][tid & 127] = (tid >> 7) < 3 || p.proj_res ? p.bsum[(tid >> 7) * p.F_out + (tid & 127)] : 0.f;
-    const int nb = gridDim.x, b = blockIdx.x;
-    int64_t ntl, lo, step;
-    if ((nb & 7) == 0 && nb >= 8) {  // XCD x takes a contiguous range of tiles
-        const int x = b & 7, i = b >> 3, bpx = nb >> 3;
-        const int64_t xlo = T * x / 8, xhi = T * (x + 1) / 8;
-        ntl = (xhi - xlo - i + bpx - 1) / bpx;
-        lo = xlo + i;
-        step = bpx;
-    } else {
-        ntl = (T - b + nb - 1) / nb;
-        lo = b;
-        step = nb;
-    }
-    if (ntl < 0) ntl = 0;
-
-    float4 wr[NG];
-    {
-        const float* src = p.Bp + (int64_t)col * K + 4 * kg;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) wr[g] = ld4(src + 16 * g);
-    }
-    // epilogue role: thread owns columns [4ej, 4ej+4) of rows er and er + 16
-    const int ej = tid & 31, er = tid >> 5;
-    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
-    const bool id_res = p.res_x && !p.proj_res;
-
-    // gates of tile row tid (< BMW), protgram_directgcn.py:116-133: raw loads now, products later
-    struct GateRaw {
-        float ci, co, cd, cu, ca;
-        int64_t cr;
-    };
-    auto gate_load = [&](int64_t tile) {
-        GateRaw g{0.f, 0.f, 0.f, 0.f, 0.f, -1};
-        const int64_t m = tile * BMW + tid;
-        if (m < p.M) {
-            g.cr = p.rows ? p.rows[m] : m;
-            const int64_t r = (p.gate_mode == PG_GATES_SCALAR) ? 0 : g.cr;
-            g.ci = p.C_in[r];
-            g.co = p.C_out[r];
-            g.cd = p.C_dir[r];
-            g.cu = p.C_und[r];
-            g.ca = p.C_all[r];
-        }
-        return g;
-    };
-    auto gate_store = [&](const GateRaw& g, int sbuf) {
-        const float cad = g.ca * g.cd;
-        Sg[sbuf][tid][0] = cad * g.ci;
-        Sg[sbuf][tid][1] = cad * g.co;
-        Sg[sbuf][tid][2] = g.ca * g.cu;
-        Sg[sbuf][tid][3] = 1.f;
-        Crow[sbuf][tid] = g.cr;
-    };
-    auto issue_A = [&](int64_t tile, float* Ad) {
-        const int64_t m0 = tile * BMW;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int idx = (wave * NI + i) * 64 + lane;  // lane-linear chunk of the tile image
-            const int r = idx / CH, pos = idx % CH;
-            const int c = pos ^ (r & 15);
-            const int k = 4 * c;
-            const int64_t m = min(m0 + r, p.M - 1);
-            const float* src = k < 3 * F_IN ? p.Z + m * p.ldz + k : p.res_x + m * p.ld_res + (k - 3 * F_IN);
-            if (!(p.dbg & 2)) glds16(src, Ad + (wave * NI + i) * 256);
-        }
-    };
-    // constant / residual rows of the current tile: 32 rows x 512 B each = 16 pieces of 1 KiB, 2 per wave
-    auto issue_CR = [&](int64_t tile, int sbuf) {
-        const int64_t m0 = tile * BMW;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int piece = wave * 2 + i;           // rows 2*piece, 2*piece + 1
-            const int r = 2 * piece + (lane >> 5);
-            const int64_t cr = Crow[sbuf][r];
-            const int64_t m = min(m0 + r, p.M - 1);
-            if (has_const) glds16(p.constant + (cr >= 0 ? cr : 0) * p.ld_const + 4 * (lane & 31), Cs + piece * 256);
-            if (id_res) glds16(p.res_x + m * p.ld_res + 4 * (lane & 31), Rs + piece * 256);
-        }
-    };
-
-    auto tile_body = [&](int64_t kt, const float* Ab, float* An, int buf) {
-        const int64_t m0 = (lo + kt * step) * BMW;
-        asm volatile("" ::: "memory");  // LDS-DMA wrote Ab (and the previous epilogue's Cs / Rs are consumed)
-        __syncthreads();                // (vmcnt(0): this tile's A rows have landed in every wave)
-        issue_CR(lo + kt * step, buf);  // lands during the MFMAs, read after the second barrier
-        const bool more = kt + 1 < ntl;
-        GateRaw gr{};
-        if (more && tid < BMW) gr = gate_load(lo + (kt + 1) * step);  // consumed after the MFMAs
-        if (more) issue_A(lo + (kt + 1) * step, An);
-        float sa[2][3];  // gates of this lane's A rows (row lc of each 16-row subtile)
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) sa[sb][q] = Sg[buf][16 * sb + lc][q];
-        // chunk (4g + kg) of row 16sb + lc sits at chunk 16(g>>2) + ((4(g&3) + kg) ^ lc): four per-lane base
-        // offsets, the rest is a compile-time ds_read immediate
-        const float* Ar = Ab + lc * K;
-        int aoff[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) aoff[j] = 4 * ((4 * j + kg) ^ lc);
-        auto ldA = [&](int g, int sb) { return ld4(Ar + aoff[g & 3] + (16 * sb * K + 64 * (g >> 2))); };
-        f32x4 acc[2];
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb) acc[sb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (!(p.dbg & 4)) {
-            float4 a0 = ldA(0, 0), a1 = ldA(0, 1);
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                float4 n0 = a0, n1 = a1;
-                if (g + 1 < NG) {  // one group of fragments ahead; the sched_barrier below stops the scheduler
-                    n0 = ldA(g + 1, 0);  // from hoisting every read of the tile
-                    n1 = ldA(g + 1, 1);
-                }
-                const int q = (16 * g) / F_IN;  // K segment of this group (F_IN % 16 == 0)
-                if (!PRE && q < 3) {  // gate the aggregates; the projected-residual segment is not gated
-                    a0 = scale4(a0, sa[0][q]);
-                    a1 = scale4(a1, sa[1][q]);
-                }
-                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, wr[g].x, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, wr[g].x, acc[1], 0, 0, 0);
-                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, wr[g].y, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, wr[g].y, acc[1], 0, 0, 0);
-                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, wr[g].z, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, wr[g].z, acc[1], 0, 0, 0);
-                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, wr[g].w, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, wr[g].w, acc[1], 0, 0, 0);
-                a0 = n0;
-                a1 = n1;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        // C/D map of 16x16: rows 4*kg + i, column lc
-#pragma unroll
-        for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Es[(16 * sb + 4 * kg + i) * ELD + col] = acc[sb][i];
-        if (more && tid < BMW) gate_store(gr, buf ^ 1);
-        asm volatile("" ::: "memory");  // LDS-DMA wrote Cs / Rs
-        __syncthreads();
-        // epilogue, row-major float4 sweep: y = acc + sum_q s_q b_q + b_res + constant + residual
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int rl = er + 16 * h;
-            if (Crow[buf][rl] < 0 || (p.dbg & 1)) continue;
-            const float4 v = ld4(&Es[rl * ELD + 4 * ej]);
-            const float4 cv = has_const ? ld4(&Cs[rl * 128 + 4 * ej]) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 rv = id_res ? ld4(&Rs[rl * 128 + 4 * ej]) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 b0 = ld4(&Bs[0][4 * ej]), b1 = ld4(&Bs[1][4 * ej]), b2 = ld4(&Bs[2][4 * ej]),
-                         br = ld4(&Bs[3][4 * ej]);
-            const float s0 = Sg[buf][rl][0], s1 = Sg[buf][rl][1], s2 = Sg[buf][rl][2];
-            const float o[4] = {v.x, v.y, v.z, v.w}, C4[4] = {cv.x, cv.y, cv.z, cv.w}, R4[4] = {rv.x, rv.y, rv.z, rv.w};
-            const float B0[4] = {b0.x, b0.y, b0.z, b0.w}, B1[4] = {b1.x, b1.y, b1.z, b1.w},
-                        B2[4] = {b2.x, b2.y, b2.z, b2.w}, BR[4] = {br.x, br.y, br.z, br.w};
-            float y[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
-                y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
-            }
-            *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
-        }
-    };
-
-    if (ntl > 0) {
-        if (tid < BMW) gate_store(gate_load(lo), 0);
-        issue_A(lo, As0);
-    }
-    for (int64_t kt = 0; kt < ntl; kt += 2) {
-        tile_body(kt, As0, As1, 0);
-        if (kt + 1 < ntl) tile_body(kt + 1, As1, As0, 1);
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------------
 // Split-bf16 W-stationary variant (PG_FLAG_DENSE_X3): fp32 accuracy on the bf16 matrix cores.
 // Every fp32 operand value v is split EXACTLY into three bf16 values v = v0 + v1 + v2 (round-to-nearest-even
@@ -587,10 +359,10 @@ __global__ __launch_bounds__(512) void dense_ws_kernel(DenseP p) {
 // size of one fp32 rounding. Six bf16 MFMAs cost 6 x 16 cycles per 16x16x32 step against 8 x 32 cycles for the
 // same step on v_mfma_f32_16x16x4_f32: 2.67x fewer matrix-core cycles.
 // Tile flow (32 rows, one 512-thread workgroup per CU, wave w owns output columns [16w, 16w+16) with its
-// three W splits in VGPRs): fp32 rows arrive by LDS-DMA in the swizzled image of dense_ws_kernel -> every
+// three W splits in VGPRs): fp32 rows arrive by LDS-DMA in the swizzled image described above -> every
 // thread converts 3 of the tile's 1536 16-byte A units into the three bf16 images (gated here when the
 // operand is not pre-gated) -> the next tile's DMA is issued -> 12 MFMA steps -> accumulators parked in LDS
-// (aliasing the consumed bf16 images) -> the same epilogue as dense_ws_kernel.
+// (aliasing the consumed bf16 images) -> the epilogue (epi_sum).
 // bf2 / split8 / mfma_bf: pg_split3.h (shared with the split-bf16 weight gradient of pg_dense_bwd.hip)
 using pgx3::bf2;
 using pgx3::mfma_bf;
@@ -679,7 +451,7 @@ __device__ __forceinline__ void glds4(const float* src, float* lds_base) {
 // 8-lane ds_write_b128 group of the split pass hits 16 distinct 16-B bank slots.
 __device__ __forceinline__ int a_unit(int s, int r, int g) { return 128 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
 
-template <int F_IN, int KSEG, bool PRE, bool STAMP = false>
+template <int F_IN, int KSEG, bool PRE>
 __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
     constexpr int K = F_IN * KSEG;
     constexpr int CH = K / 4;     // fp32 16-B chunks per row
@@ -689,6 +461,7 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
     constexpr int NI = BMW * CH / 64 / 8;  // A-row LDS-DMA instructions per wave per tile
     constexpr int NG = 3;                  // gate-input LDS-DMA instructions per tile (wave 0)
     constexpr int NCR = 4;                 // constant + residual LDS-DMA instructions per wave per tile
+    (void)NCR;
     constexpr int NCV = (BMW * NU + 511) / 512;  // units converted per thread per tile
     static_assert(CH % 16 == 0 && NU % 16 == 0 && (BMW * CH) % 512 == 0 && BMW * 128 / 4 == 1024, "tile shape");
     __shared__ __attribute__((aligned(16))) float Af[BMW * K];          // fp32 rows (LDS-DMA target)
@@ -759,7 +532,7 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             const int rr = min(r, rmax);
             const float* src = (KSEG == 3 || k < 3 * F_IN) ? zb + (rr * (int)p.ldz + k)
                                                           : xb + (rr * (int)p.ld_res + (k - 3 * F_IN));
-            if (!(p.dbg & 2)) glds16(src, Ad + (wave * NI + i) * 256);
+            glds16(src, Ad + (wave * NI + i) * 256);
         }
     };
     // gate inputs of the tile's rows (wave 0 only): piece i, lanes 0-31 / 32-63 fetch C_x for x = 2i / 2i + 1
@@ -811,7 +584,6 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
     auto convert = [&](const float* Af, int gb) {
 #pragma unroll
         for (int i = 0; i < NCV; ++i) {
-            if (p.dbg & 8) break;
             const int j = tid + 512 * i;
             if (BMW * NU % 512 != 0 && j >= BMW * NU) break;
             const int r = j & (BMW - 1), u = j / BMW;
@@ -849,19 +621,6 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
         issue_A(tile_of(0), Af);
     }
     bool prev_full = false;  // the previous epilogue issued exactly 2 Y stores per thread
-    // timing probe (STAMP instance, flags bit 27): per-phase s_memtime cycle sums of wave 0, written to Y row b
-    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
-    auto stamp = [&](int i) {
-        if constexpr (STAMP) {
-            uint64_t t;
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (i >= 0) tsum[i] += t - tprev;
-            tprev = t;
-        }
-    };
-    stamp(-1);
     for (int64_t kt = 0; kt < ntl; ++kt) {
         const int buf = (int)(kt & 1);
         const int64_t m0 = (lo + kt * step) * BMW;
@@ -870,12 +629,10 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
         if (prev_full) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();  // every wave's pieces have landed; the previous epilogue is done with Es / Cs / Rs
-        stamp(0);
-        if (!(p.dbg & 32)) issue_CR(tile_of(kt));  // Cs / Rs are free: their DMA overlaps the split pass
-        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(kt + 1), buf ^ 1);  // Gi[buf ^ 1]: tile kt-1 is done
+        issue_CR(tile_of(kt));  // Cs / Rs are free: their DMA overlaps the split pass
+        if (wave == 0) issue_G(tile_of(kt + 1), buf ^ 1);  // Gi[buf ^ 1]: tile kt-1 is done
         convert(Af, buf);
         lds_barrier();  // bf16 images ready; Af is free
-        stamp(1);
         issue_A(tile_of(kt + 1), Af);
         f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
         // operands of k step s for row blocks 0 / 1 sit at one per-lane address + s * 2 KB (+ 1 KB for block 1):
@@ -891,10 +648,9 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             o[4] = ab0[BMW * NU + 64 + 128 * s];
             o[5] = ab2[64 + 128 * s];
         };
-        if (!(p.dbg & 4)) ld_ops(0, op[0]);
+        ld_ops(0, op[0]);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            if (p.dbg & 4) break;
             if (s + 1 < NS) ld_ops(s + 1, op[(s + 1) & 1]);
             const uint4 a00 = op[s & 1][0], a01 = op[s & 1][1], a02 = op[s & 1][2];
             const uint4 a10 = op[s & 1][3], a11 = op[s & 1][4], a12 = op[s & 1][5];
@@ -912,21 +668,18 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             acc[1] = mfma_bf(a10, w0[s], acc[1]);
             __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting later steps' reads (VGPRs)
         }
-        stamp(2);
         lds_barrier();  // every wave is done reading the bf16 images: Es may overwrite them
 #pragma unroll
         for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
             for (int i = 0; i < 4; ++i) lds_stf(&Es[(16 * sb + 4 * kg + i) * ELD + col], acc[sb][i]);
-        stamp(3);
         if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_W0) : "memory");  // CR(kt)
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT_WN) : "memory");
         lds_barrier();
-        stamp(4);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int rl = er + 16 * h;
-            if (m0 + rl >= p.M || (p.dbg & 64)) continue;
+            if (m0 + rl >= p.M) continue;
             float4 v, cv, rv, bb[4];
             lds_ld4x2(&Cs[rl * 128 + 4 * ej], &Rs[rl * 128 + 4 * ej], cv, rv);
             lds_ld4x4(&Es[rl * ELD + 4 * ej], &Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], bb);
@@ -947,15 +700,11 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
                 const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                 y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
             }
-            if (!(p.dbg & 1)) *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
+            *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
         }
-        prev_full = m0 + BMW <= p.M && !(p.dbg & (1 | 64));
-        stamp(5);
+        prev_full = m0 + BMW <= p.M;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tile's DMA must land before the LDS is freed
-    if constexpr (STAMP) {
-        if (tid < 6 && (int64_t)b < p.M) p.Y[(int64_t)b * p.ldy + tid] = (float)tsum[tid];
-    }
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -970,7 +719,7 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
 // LDS: Af 2 x 24 KB, As 2 x 36 KB, Cs/Rs 16 KB, Es 8.3 KB, gate inputs 4 x 512 B, bias sums 2 KB.
 __device__ __forceinline__ int a_unit16(int s, int r, int g) { return 64 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
 
-template <bool PRE, bool STAMP = false>
+template <bool PRE>
 __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     constexpr int F_IN = 128, K = 384;
     constexpr int CH = K / 4;    // fp32 16-B chunks per row
@@ -980,6 +729,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     constexpr int NI = BM * CH / 64 / 8;  // A-row LDS-DMA pieces per wave per tile (3)
     constexpr int NG = 2;                 // gate-input pieces per tile (wave 0)
     constexpr int NCR = 2;                // constant + residual pieces per wave per tile
+    (void)NCR;
     constexpr int ELD = 128 + 4;
     static_assert(BM * CH % 512 == 0 && NI == 3, "tile shape");
     __shared__ __attribute__((aligned(16))) float Af0[BM * K];  // separate objects: the compiler tells the DMA
@@ -1059,7 +809,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
             const int r = idx / CH, pos = idx - r * CH;
             const int k = 4 * (pos ^ r);
             const int rr = min(r, rmax);
-            if (!(p.dbg & 2)) glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
+            glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
         }
     };
     // gate inputs of a tile (wave 0): piece 0 = C_in | C_out | C_dir | C_und (16 lanes each), piece 1 = C_all
@@ -1100,7 +850,6 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     // fp32 tile -> three bf16 images; thread j converts units j and j + 512 (row j & 15, unit j >> 4): waves 0-3
     // two units, waves 4-7 one; all of a thread's fp32 reads in one LDS round trip
     auto split_tile = [&](const float* Af, int ab, int gslot) {
-        if (p.dbg & 8) return;
         const int r = tid & 15;
         const bool two = tid + 512 < BM * NU;  // wave-uniform
         const int u0 = tid >> 4, u1 = u0 + 32;
@@ -1138,7 +887,6 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         const uint4* a2 = &As[ab][2][a_unit16(0, lc, kg)];
         uint4 op[2][3];
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (p.dbg & 4) return;
         op[0][0] = a0[0];
         op[0][1] = a1[0];
         op[0][2] = a2[0];
@@ -1159,17 +907,6 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
-    auto stamp = [&](int i) {
-        if constexpr (STAMP) {
-            uint64_t t;
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (i >= 0) tsum[i] += t - tprev;
-            tprev = t;
-        }
-    };
 
     // prologue: A(0), G(0) and A(1), G(1) in flight; split(0) once A(0) has landed
     if (ntl > 0) {
@@ -1185,44 +922,36 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     // bias sums of this thread's epilogue columns (Bs was published by the prologue barrier)
     float4 bq[4];
     if (ntl > 0) lds_ld4x4(&Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], &Bs[3][4 * ej], bq);
-    stamp(-1);
     bool y_pending = false;  // the previous epilogue left exactly one Y store per thread in flight
     for (int64_t i = 0; i <= ntl && ntl > 0; ++i) {
         const int ab = (int)(i & 1);
         if (y_pending) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // A(i+1), G(i+1) have landed
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();  // B1: A(i+1) and split(i) visible; epilogue(i-2) done with Es / Cs / Rs; As[ab ^ 1] free
-        stamp(0);
         if (i >= 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) lds_stf(&Es[(4 * kg + e) * ELD + col], acc[e]);
         }
-        if (!(p.dbg & 32)) issue_CR(tile_of(i - 1));
+        issue_CR(tile_of(i - 1));
         issue_A(tile_of(i + 2), ab ? Af1 : Af0);  // Af[(i + 2) & 1] = Af[ab]: split(i) is done with it
-        if (wave == 0 && !(p.dbg & 16)) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
-        stamp(1);
+        if (wave == 0) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
         const bool do_mfma = i < ntl, do_split = i + 1 < ntl;
         if (mfma_first) {
             if (do_mfma) mfma_tile(ab);
-            stamp(2);
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
-            stamp(3);
         } else {
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
-            stamp(3);
             if (do_mfma) mfma_tile(ab);
-            stamp(2);
         }
         // CR(i-1) has landed: younger are A(i+2) (+ G(i+2) on wave 0)
         if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + NG) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
         lds_barrier();  // B2: Es and Cs / Rs visible
-        stamp(4);
         y_pending = false;
         if (i >= 1) {
             const int64_t m0 = tile_of(i - 1) * BM;
             const int gs = (int)((i - 1) & 3);
-            if (m0 + er < p.M && !(p.dbg & 64)) {
+            if (m0 + er < p.M) {
                 float4 cv, rv, ov;
                 float c[5];
                 lds_epi<BM * 4>(&Cs[er * 128 + 4 * ej], &Rs[er * 128 + 4 * ej], &Es[er * ELD + 4 * ej], &Gi[gs][0][er],
@@ -1241,18 +970,14 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                     const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                     y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
                 }
-                if (!(p.dbg & 1)) {
+                {
                     *reinterpret_cast<float4*>(p.Y + (m0 + er) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
                     y_pending = true;
                 }
             }
         }
-        stamp(5);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles' DMA must land before the LDS is freed
-    if constexpr (STAMP) {
-        if (tid < 6 && (int64_t)b < p.M) p.Y[(int64_t)b * p.ldy + tid] = (float)tsum[tid];
-    }
 }
 
 __global__ __launch_bounds__(256) void pack_kernel(int F_in, int F_out, int K, const float* W0, const float* W1,
@@ -1365,7 +1090,6 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.Y = a->Y;
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
-    p.dbg = (int)((flags >> 20) & 255);
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.vec_out = (a->F_out % 4 == 0) && (a->ldy % 4 == 0) && pg::aligned16(a->Y) &&
                 (!a->constant || (a->ld_const % 4 == 0 && pg::aligned16(a->constant))) &&
@@ -1374,110 +1098,52 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     if (a->res_x) vec = vec && pg::aligned16(a->res_x) && (a->ld_res % 4 == 0);
     const bool wide = a->F_out > 64;
     const int64_t BN = wide ? 128 : 64;
-    // BM=64 row tiles double the grid (fewer idle CUs in the last wave of blocks); BM=128 halves the
-    // B-tile re-reads. PG_FLAG_DENSE_BM64 / PG_FLAG_DENSE_BM128 force one; default picks by grid size.
-    const int64_t nb128 = ((a->M + 127) / 128) * ((a->F_out + BN - 1) / BN);
-    bool bm64 = false;
-    (void)nb128;
-    if (flags & PG_FLAG_DENSE_BM64) bm64 = true;
-    if (flags & PG_FLAG_DENSE_BM128) bm64 = false;
-    const int64_t BMv = bm64 ? 64 : 128;
-    const int64_t nb = ((a->M + BMv - 1) / BMv) * ((a->F_out + BN - 1) / BN);
+    const int64_t nb = ((a->M + 127) / 128) * ((a->F_out + BN - 1) / BN);
     hipStream_t s = (hipStream_t)stream;
-#define PG_LAUNCH(BMx, BNx, NWx)                                                                                \
-    do {                                                                                                           \
-        if (vec && pf2) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true, 2>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
-        else if (vec) hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, true>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p); \
-        else hipLaunchKernelGGL((dense_kernel<BMx, BNx, NWx, false>), dim3((unsigned)nb), dim3(64 * NWx), 0, s, p);    \
-    } while (0)
-    const bool w8 = !(flags & PG_FLAG_DENSE_4WAVES);
-    const bool pf2 = (flags & PG_FLAG_DENSE_PF2) != 0;
-    // W-stationary kernel: the default for pre-gated operands (measured 0.161 vs 0.176 ms for the tiled kernel at
-    // B(20,4), F=128); PG_FLAG_DENSE_WS forces it, PG_FLAG_DENSE_TILED forbids it
-    const bool want_ws = (flags & PG_FLAG_DENSE_WS) || (p.pregated && !(flags & PG_FLAG_DENSE_TILED));
+    // split-bf16 W-stationary kernels (fp32-accurate, bf16 matrix cores): K = 384 (F_in 128: the pipelined 16-row
+    // kernel) or 256 (F_in 64 with the projected residual: the 32-row kernel). The default wherever their shape
+    // applies (B(20,4), F=128: 0.127-0.134 ms; the tiled fp32 kernel 0.188, an fp32 W-stationary kernel 0.162, the
+    // 32-row split kernel at F_in 128 0.140 -- both removed; max |err| vs float64 1.4e-5 against 1.8e-5 for fp32
+    // MFMA); PG_FLAG_DENSE_TILED selects the tiled kernel below instead.
     const bool ws_shape_ok = a->F_out == 128 && vec && p.vec_out &&
                              (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)));
-    // split-bf16 W-stationary kernel (fp32-accurate, bf16 matrix cores): K = 384 (F_in 128) or 256 (F_in 64 with
-    // the projected residual). The default wherever its shape applies (B(20,4), F=128: 0.140 ms ungated and 0.145
-    // pre-gated, against 0.188 tiled and 0.162 fp32 W-stationary; max |err| vs float64 1.4e-5 against 1.8e-5 for
-    // the fp32 MFMA kernels); any explicit tiling / W-stationary flag selects that kernel instead.
-    const uint32_t other_variant = PG_FLAG_DENSE_TILED | PG_FLAG_DENSE_WS | PG_FLAG_DENSE_BM64 | PG_FLAG_DENSE_BM128 |
-                                   PG_FLAG_DENSE_4WAVES | PG_FLAG_DENSE_PF2;
-    const bool want_x3 = (flags & PG_FLAG_DENSE_X3) || !(flags & other_variant);
-    if (want_x3 && !(flags & PG_FLAG_DENSE_TILED) && ws_shape_ok && a->ldz < (1 << 24) &&
-        a->rows == nullptr &&
+    if (!(flags & PG_FLAG_DENSE_TILED) && ws_shape_ok && a->ldz < (1 << 24) && a->rows == nullptr &&
         (!a->res_x || a->ld_res < (1 << 24)) &&
         ((a->F_in == 128 && !a->W_res) || (a->F_in == 64 && a->W_res))) {
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        const int64_t T = (a->M + 31) / 32;
-        const unsigned g = (unsigned)(T < ncu ? T : ncu);
-#define PG_X3(FI, KS)                                                                                     \
-    do {                                                                                                  \
-        if (p.pregated) hipLaunchKernelGGL((dense_x3_kernel<FI, KS, true>), dim3(g), dim3(512), 0, s, p); \
-        else hipLaunchKernelGGL((dense_x3_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
-    } while (0)
-        const bool pipelined = a->F_in == 128 && !(flags & PG_FLAG_DENSE_X3_32);
-        if (p.rawW && !(pipelined && pg::aligned16(a->W_main_in) && pg::aligned16(a->W_main_out) &&
-                        pg::aligned16(a->W_undirected) && pg::aligned16(a->W_shared)))
-            return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
-                                                     "split-bf16 kernel (F_in = F_out = 128, no row map)");
-        if (pipelined) {  // 16-row software-pipelined kernel
+        if (a->F_in == 128) {  // 16-row software-pipelined kernel
+            if (p.rawW && !(pg::aligned16(a->W_main_in) && pg::aligned16(a->W_main_out) &&
+                            pg::aligned16(a->W_undirected) && pg::aligned16(a->W_shared)))
+                return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights must be 16-B aligned");
             const int64_t T16 = (a->M + 15) / 16;
             const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
-            const bool st = (p.dbg & 128) != 0;  // timing probe: phase cycle sums in Y rows 0..grid-1
-            if (p.pregated) {
-                if (st) hipLaunchKernelGGL((dense_x3p_kernel<true, true>), dim3(g16), dim3(512), 0, s, p);
-                else hipLaunchKernelGGL((dense_x3p_kernel<true>), dim3(g16), dim3(512), 0, s, p);
-            } else {
-                if (st) hipLaunchKernelGGL((dense_x3p_kernel<false, true>), dim3(g16), dim3(512), 0, s, p);
-                else hipLaunchKernelGGL((dense_x3p_kernel<false>), dim3(g16), dim3(512), 0, s, p);
-            }
-        } else if (p.dbg & 128) {
-            if (a->F_in == 128 && p.pregated) hipLaunchKernelGGL((dense_x3_kernel<128, 3, true, true>), dim3(g), dim3(512), 0, s, p);
-            else if (a->F_in == 128) hipLaunchKernelGGL((dense_x3_kernel<128, 3, false, true>), dim3(g), dim3(512), 0, s, p);
-        } else if (a->F_in == 128) PG_X3(128, 3);
-        else PG_X3(64, 4);
-#undef PG_X3
+            if (p.pregated) hipLaunchKernelGGL((dense_x3p_kernel<true>), dim3(g16), dim3(512), 0, s, p);
+            else hipLaunchKernelGGL((dense_x3p_kernel<false>), dim3(g16), dim3(512), 0, s, p);
+        } else {
+            if (p.rawW)
+                return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
+                                                         "split-bf16 kernel (F_in = F_out = 128, no row map)");
+            const int64_t T = (a->M + 31) / 32;
+            const unsigned g = (unsigned)(T < ncu ? T : ncu);
+            if (p.pregated) hipLaunchKernelGGL((dense_x3_kernel<64, 4, true>), dim3(g), dim3(512), 0, s, p);
+            else hipLaunchKernelGGL((dense_x3_kernel<64, 4, false>), dim3(g), dim3(512), 0, s, p);
+        }
         return pg::check_launch("pg_directgcn_dense_f32");
     }
     if (p.rawW)
         return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
                                                  "split-bf16 kernel (F_in = F_out = 128, no row map)");
-    if (want_ws && a->F_out == 128 && vec && p.vec_out && (a->F_in == 64 || (a->F_in == 128 && !a->W_res)) &&
-        (!a->res_x || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)))) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-        const int64_t T = (a->M + 31) / 32;
-        const unsigned g = (unsigned)(T < ncu ? T : ncu);
-#define PG_WS(FI, KS)                                                                                     \
-    do {                                                                                                  \
-        if (p.pregated) hipLaunchKernelGGL((dense_ws_kernel<FI, KS, true>), dim3(g), dim3(512), 0, s, p); \
-        else hipLaunchKernelGGL((dense_ws_kernel<FI, KS, false>), dim3(g), dim3(512), 0, s, p);          \
-    } while (0)
-        if (a->F_in == 128) PG_WS(128, 3);
-        else if (!p.proj_res) PG_WS(64, 3);
-        else PG_WS(64, 4);
-#undef PG_WS
-        return pg::check_launch("pg_directgcn_dense_f32");
-    }
-    if (bm64 && w8 && wide) {
-        PG_LAUNCH(64, 128, 8);  // 8 waves of 32x32 (measured 0.186 ms vs 0.177 for the default at B(20,4))
-    } else if (bm64) {
-        if (wide) PG_LAUNCH(64, 128, 4);
-        else PG_LAUNCH(64, 64, 4);
-    } else if (w8) {
-        if (wide) PG_LAUNCH(128, 128, 8);
-        else PG_LAUNCH(128, 64, 8);
+    // tiled fp32 kernel: 128-row tiles, 8 waves of 32x32 (BM = 64 and 4-wave tilings measured slower, removed)
+    if (vec) {
+        if (wide) hipLaunchKernelGGL((dense_kernel<128, 128, 8, true>), dim3((unsigned)nb), dim3(512), 0, s, p);
+        else hipLaunchKernelGGL((dense_kernel<128, 64, 8, true>), dim3((unsigned)nb), dim3(512), 0, s, p);
     } else {
-        if (wide) PG_LAUNCH(128, 128, 4);
-        else PG_LAUNCH(128, 64, 4);
+        if (wide) hipLaunchKernelGGL((dense_kernel<128, 128, 8, false>), dim3((unsigned)nb), dim3(512), 0, s, p);
+        else hipLaunchKernelGGL((dense_kernel<128, 64, 8, false>), dim3((unsigned)nb), dim3(512), 0, s, p);
     }
-#undef PG_LAUNCH
     return pg::check_launch("pg_directgcn_dense_f32");
 }
 

@@ -30,7 +30,7 @@ def classify(k):
         return "head_x3"
     if "dense_x3_kernel" in k:  # split-bf16 W-stationary dense kernel: <F_IN, KSEG, pregated>
         return "dense_x3_pregated" if k.rstrip(")").find("true>") >= 0 else "dense_x3"
-    for key, short in (("dense_ws_kernel", "dense_ws"), ("spmm_vec_kernel", "spmm_bcast"),
+    for key, short in (("spmm_vec_kernel", "spmm_bcast"),
                        ("dgrad_kernel", "dense_dgrad"), ("wgrad_kernel", "dense_wgrad"),
                        ("reduce_splits", "wgrad_reduce"), ("dense_kernel", "dense"), ("head_kernel", "head")):
         if key in k:

@@ -1,11 +1,58 @@
 """n-gram producer (ngram.py): host-side semantics of the reference's builder on CPU; the GPU key kernel and
 sorts against the Python restatement (synth.fasta_edges, which made the golden fixtures) and the fixtures'
-own raw transition tables."""
+own raw transition tables. p1_fasta (tools/golden/make_producer_golden.py) pins both to the reference's own
+FASTA reader and builder functions (data_utils.py:182-212, data_builder.py:29-54) run on a committed FASTA text."""
 import numpy as np
 import pytest
 import torch
 
 from golden_util import load
+
+
+# ----------------------------------------------------------------------------------------------------------
+# p1_fasta: outputs of the reference's DataLoader.parse_sequences and data_builder helpers (n = 1..4)
+# ----------------------------------------------------------------------------------------------------------
+def _p1():
+    return load("p1_fasta")
+
+
+def _p1_path(tmp_path):
+    f = tmp_path / "p1.fasta"
+    f.write_bytes(_p1()["fasta"].tobytes())
+    return str(f)
+
+
+def test_p1_read_fasta_and_preprocess_match_reference(pkg, tmp_path):
+    from protgram_directgcn_amd import ngram
+    fx = _p1()
+    got = list(ngram.read_fasta(_p1_path(tmp_path)))
+    assert [g[0] for g in got] == fx["ids"].tolist()
+    assert [g[1] for g in got] == fx["seqs"].tolist()
+    assert ngram.preprocess([g[1] for g in got]) == fx["pre"].tolist()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
+def test_p1_restatement_matches_reference_builder(pkg, n):
+    """synth.fasta_edges (which made the f1/f5 FASTA fixtures and is the CPU check of the GPU producer) against the
+    reference builder's own n-gram map and aggregated transition table."""
+    fx = _p1()
+    N, s, d, c, ordered = pkg.synth.fasta_edges(n, fx["pre"].tolist())
+    assert ordered == fx[f"n{n}_ngrams"].tolist() and N == len(ordered)
+    assert np.array_equal(s, fx[f"n{n}_src"]) and np.array_equal(d, fx[f"n{n}_dst"])
+    assert np.array_equal(c, fx[f"n{n}_w"].astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
+def test_p1_gpu_producer_matches_reference_builder(pkg, cuda, tmp_path, n):
+    from protgram_directgcn_amd import ngram
+    fx = _p1()
+    seqs = [g[1] for g in ngram.read_fasta(_p1_path(tmp_path))]
+    got = ngram.ngram_transitions(seqs, n, device=cuda, pad=True)
+    assert got.node_strings() == fx[f"n{n}_ngrams"].tolist()
+    assert np.array_equal(got.src.cpu().numpy(), fx[f"n{n}_src"])
+    assert np.array_equal(got.dst.cpu().numpy(), fx[f"n{n}_dst"])
+    assert np.array_equal(got.cnt.cpu().numpy(), fx[f"n{n}_w"].astype(np.float32))
 
 
 def test_read_fasta_follows_parse_sequences(pkg, tmp_path):

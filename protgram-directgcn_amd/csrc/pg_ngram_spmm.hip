@@ -129,8 +129,11 @@ __device__ __forceinline__ int plan_slot(int i, int jb, int PB) { return i * PB 
 // 16-B loads with the half-waves on alternate steps c (every source once, partial rows summed by
 // v_permlane32_swap; 196 VGPRs, 2 waves/SIMD) 0.187; the workgroup's K + PA source rows per step staged once in a
 // double-buffered LDS slab (10 waves per (M, a-block), one barrier per step; 124 VGPRs + 64 KB LDS, one workgroup
-// per CU) 0.280; the F = 64 kernel on the two column halves 0.164. This kernel is texture-data bound (TD 90 %
-// busy, ~30 cycles per 8-B wave load; PMC, profiles/r02_pmc_summary.txt).
+// per CU) 0.280; the same slab filled by LDS-DMA (global_load_lds_dwordx4) in a ring of 3 or 4 steps ahead (90
+// VGPRs, two workgroups per CU) 0.185, and 0.126 against 0.063 at F = 64, i.e. a per-step cost that does not
+// shrink with the bytes; 4 x 5 plan blocks with the two blocks of a workgroup sharing their in-sources through a
+// register-staged LDS slab 0.274 (this kernel on 4 x 5 blocks: 0.170). This kernel is texture-data bound (TD
+// 90 % busy, ~30 cycles per 8-B wave load; PMC, profiles/r02_pmc_summary.txt).
 template <int K, int VEC, int PA, int PB, int AH, int NB, bool GATED>
 __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
     static_assert(K % NB == 0, "the c loop runs in rounds of NB steps");

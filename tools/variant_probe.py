@@ -37,15 +37,16 @@ def timeit(fn, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM as CSR  # noqa: E402
+
 variants = {
-    "f32_u4": lambda: ops.spmm3(g, x32, flags=0),
-    "f32_b512": lambda: ops.spmm3(g, x32, flags=1024),
-    "f32_b1024": lambda: ops.spmm3(g, x32, flags=2048),
-    "f32_b1024_u8": lambda: ops.spmm3(g, x32, flags=2048 | 4),
-    "f32t_b1024": lambda: ops.spmm3_t(g, G32, flags=2048),
+    "f32": lambda: ops.spmm3(g, x32, flags=0),            # n-gram tile kernel on B(20,n)
+    "f32_csr": lambda: ops.spmm3(g, x32, flags=CSR),
+    "f32_csr_u8": lambda: ops.spmm3(g, x32, flags=CSR | 4),
+    "f32t": lambda: ops.spmm3_t(g, G32, flags=0),
+    "f32t_csr": lambda: ops.spmm3_t(g, G32, flags=CSR),
     "bf16_u4": lambda: ops.spmm3(g, x16, flags=0),
     "bf16_u8": lambda: ops.spmm3(g, x16, flags=4),
-    "f32t_u4": lambda: ops.spmm3_t(g, G32, flags=0),
     "bf16t_u4": lambda: ops.spmm3_t(g, G16, flags=0),
     "bf16t_u8": lambda: ops.spmm3_t(g, G16, flags=4),
 }

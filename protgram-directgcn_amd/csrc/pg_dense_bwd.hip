@@ -1120,6 +1120,112 @@ SplitPlan split_rows(int64_t M, int64_t tiles) {
     return sp;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Any-shape path (F_in / F_out not multiples of 4, unaligned or odd leading dimensions): the same outputs as
+// dgrad_kernel + wgrad_kernel from plain per-element loops. Sums run in another order (within fp32 rounding of
+// the vector path); these shapes are off the model's hot path.
+// ------------------------------------------------------------------------------------------------
+constexpr int GEN_MAX_FOUT = 8192;  // dpre row staged in LDS
+
+// one 256-thread block per row (grid-stride): dpre, gates, dZ / dres, and ds_q into dsp tile 0
+__global__ __launch_bounds__(256) void dgrad_generic_kernel(DgradP p) {
+    __shared__ float dp[GEN_MAX_FOUT];
+    __shared__ float red[3][256];
+    const int tid = threadIdx.x;
+    for (int64_t m = blockIdx.x; m < p.M; m += gridDim.x) {
+        float ci, co, cd, cu, ca;
+        gate_values(p.g, m, ci, co, cd, cu, ca);
+        const float cad = ca * cd;
+        const float s[3] = {cad * ci, cad * co, ca * cu};
+        if (tid == 0) {
+            p.gates[m * 4 + 0] = s[0];
+            p.gates[m * 4 + 1] = s[1];
+            p.gates[m * 4 + 2] = s[2];
+            p.gates[m * 4 + 3] = 1.f;
+        }
+        float ds[3] = {0.f, 0.f, 0.f};
+        for (int o = tid; o < p.F_out; o += 256) {
+            float d = p.dY[m * p.lddy + o];
+            if (p.act) d = p.Y[m * p.ldy + o] > 0.f ? d : d * p.slope;
+            dp[o] = d;
+            p.dpre[m * p.ldp + o] = d;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) ds[q] += d * p.bsum[q * p.F_out + o];
+        }
+        __syncthreads();
+        for (int j = tid; j < p.N; j += 256) {
+            const float* bt = p.BT + (int64_t)j * p.F_out;
+            float G = 0.f;
+            for (int o = 0; o < p.F_out; ++o) G += dp[o] * bt[o];
+            const int seg = j / p.F_in;
+            if (seg < 3) {
+                ds[seg] += G * p.Z[m * p.ldz + j];
+                if (p.dZ) p.dZ[m * p.lddz + j] = s[seg] * G;
+            } else {
+                p.dres[m * p.lddres + (j - 3 * p.F_in)] = G;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) red[q][tid] = ds[q];
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (tid < w)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) red[q][tid] += red[q][tid + w];
+            __syncthreads();
+        }
+        if (tid < 3) p.dsp[(int64_t)tid * p.M + m] = red[tid][0];
+        __syncthreads();  // dp / red are reused by the next row
+    }
+}
+
+// partial [split][F_out * K + 4 F_out]: dB[o][j] = sum_m s_seg(j)[m] dpre[m][o] A[m][j] (A = Z, or res_x in
+// segment 3 with s = 1), dbsum[q][o] = sum_m s_q[m] dpre[m][o] (q = 3: the projected residual's bias, else 0)
+struct WgradGenP {
+    int64_t M;
+    int F_in, F_out, K, proj;
+    const float *dpre, *Z, *R, *gates;
+    int64_t ldp, ldz, ldr;
+    int64_t rows_per_split, part_stride;
+    float* part;
+};
+
+__global__ __launch_bounds__(256) void wgrad_generic_kernel(WgradGenP w) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = (int64_t)w.F_out * (w.K + 4);
+    if (idx >= n) return;
+    const int64_t m0 = (int64_t)blockIdx.y * w.rows_per_split;
+    const int64_t m1 = m0 + w.rows_per_split < w.M ? m0 + w.rows_per_split : w.M;
+    float acc = 0.f;
+    int64_t out;
+    if (idx < (int64_t)w.F_out * w.K) {  // dB[o][j], j fastest
+        const int o = (int)(idx / w.K), j = (int)(idx % w.K);
+        const int seg = j / w.F_in;
+        for (int64_t m = m0; m < m1; ++m) {
+            const float a = seg < 3 ? w.Z[m * w.ldz + j] : w.R[m * w.ldr + (j - 3 * w.F_in)];
+            const float sv = seg < 3 ? w.gates[m * 4 + seg] : 1.f;
+            acc += sv * w.dpre[m * w.ldp + o] * a;
+        }
+        out = idx;
+    } else {
+        const int64_t t = idx - (int64_t)w.F_out * w.K;
+        const int q = (int)(t / w.F_out), o = (int)(t % w.F_out);
+        if (q < 3 || w.proj)
+            for (int64_t m = m0; m < m1; ++m) acc += (q < 3 ? w.gates[m * 4 + q] : 1.f) * w.dpre[m * w.ldp + o];
+        out = (int64_t)w.F_out * w.K + (int64_t)q * w.F_out + o;
+    }
+    w.part[(int64_t)blockIdx.y * w.part_stride + out] = acc;
+}
+
+__global__ __launch_bounds__(256) void reduce_generic_kernel(int64_t n, int splits, int64_t stride, const float* part,
+                                                             float* out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float acc = 0.f;
+    for (int k = 0; k < splits; ++k) acc += part[(int64_t)k * stride + i];
+    out[i] = acc;
+}
+
 int64_t up4(int64_t v) { return (v + 3) / 4 * 4; }
 
 // the split-bf16 weight gradient (wgrad_x3_kernel, opt-in: PG_FLAG_DENSE_X3) takes the model's shape
@@ -1172,12 +1278,10 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
                      pg::aligned16(a->Z) && pg::aligned16(g->dY) && pg::aligned16(g->dpre) && (!g->dZ || (pg::aligned16(g->dZ) && g->lddz % 4 == 0)) &&
                      pg::aligned16(g->gates) && pg::aligned16(g->dW) && pg::aligned16(g->work) &&
                      pg::aligned16(packed) && (!a->act || pg::aligned16(a->Y));
-    if (!vec)
-        return pg::set_error(PG_ERR_UNSUPPORTED,
-                             "pg_directgcn_dense_bwd_f32: needs F_in, F_out and leading dims multiple of 4 and "
-                             "16-B aligned buffers");
     PG_REQUIRE(a->ldz >= 3 * a->F_in && (!g->dZ || g->lddz >= 3 * a->F_in) && g->lddy >= a->F_out && g->ldp >= a->F_out,
                "leading dimensions too small");
+    PG_REQUIRE(vec || a->F_out <= GEN_MAX_FOUT, "F_out %lld > %d on the any-shape path", (long long)a->F_out,
+               GEN_MAX_FOUT);
     hipStream_t s = (hipStream_t)stream;
     const int K = pl.K;
     const int F_in = (int)a->F_in, F_out = (int)a->F_out;
@@ -1196,6 +1300,58 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed, BT);
     }
     Gates gt{a->gate_mode, a->C_in, a->C_out, a->C_directed, a->C_undirected, a->C_all, a->rows};
+    if (!vec) {  // any shape: per-element kernels (same outputs, sums in another order)
+        DgradP p{};
+        p.M = a->M;
+        p.F_in = F_in;
+        p.F_out = F_out;
+        p.N = K;
+        p.dY = g->dY;
+        p.lddy = g->lddy;
+        p.Y = a->Y;
+        p.ldy = a->ldy;
+        p.act = a->act;
+        p.slope = a->slope;
+        p.BT = BT;
+        p.bsum = packed + (int64_t)F_out * K;
+        p.Z = a->Z;
+        p.ldz = a->ldz;
+        p.g = gt;
+        p.dpre = g->dpre;
+        p.ldp = g->ldp;
+        p.dZ = g->dZ;
+        p.lddz = g->lddz;
+        p.dres = g->dres;
+        p.lddres = g->lddres;
+        p.gates = g->gates;
+        p.dsp = dsp;
+        const unsigned nb = (unsigned)std::min<int64_t>(a->M, 8192);
+        hipLaunchKernelGGL(dgrad_generic_kernel, dim3(nb), dim3(256), 0, s, p);
+        const int gb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);
+        hipLaunchKernelGGL(gate_grad_kernel, dim3(gb), dim3(256), 0, s, a->M, 1, (const float*)dsp, gt, g->dgate);
+        WgradGenP w{};
+        w.M = a->M;
+        w.F_in = F_in;
+        w.F_out = F_out;
+        w.K = K;
+        w.proj = proj ? 1 : 0;
+        w.dpre = g->dpre;
+        w.ldp = g->ldp;
+        w.Z = a->Z;
+        w.ldz = a->ldz;
+        w.R = a->res_x;
+        w.ldr = a->ld_res;
+        w.gates = g->gates;
+        w.rows_per_split = pl.rows_per_split;
+        w.part_stride = pl.part_stride;
+        w.part = part;
+        const int64_t n = (int64_t)F_out * (K + 4);
+        hipLaunchKernelGGL(wgrad_generic_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)pl.splits), dim3(256), 0, s,
+                           w);
+        hipLaunchKernelGGL(reduce_generic_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, pl.splits,
+                           pl.part_stride, (const float*)part, g->dW);
+        return pg::check_launch("pg_directgcn_dense_bwd_f32");
+    }
     {
         DgradP p{};
         p.M = a->M;

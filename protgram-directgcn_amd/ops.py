@@ -410,8 +410,8 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
                          act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
                          need_dZ: bool = True):
-    """pg_directgcn_dense_bwd_f32. Returns None when the shape is not supported by the HIP kernels
-    (F_in / F_out not multiples of 4), else a dict with
+    """pg_directgcn_dense_bwd_f32 (any shape; bf16 operands: pg_directgcn_dense_bwd_bf16, None when F_in / F_out
+    are not multiples of 8 -- the caller then runs the fp32 kernels on widened copies). Returns a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
       dgate [5, M] (per-row grads of c_in, c_out, c_directed, c_undirected, c_all),
       dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out]."""
@@ -420,7 +420,7 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     M, F_in = Z.size(0), Z.size(1) // 3
     F_out = prm["W_main_in"].size(0)
     bf = _is_bf16(Z)
-    if (F_in % 8 or F_out % 8) if bf else (F_in % 4 or F_out % 4):
+    if bf and (F_in % 8 or F_out % 8):
         return None
     if bf:
         packed, p16 = pack_weights_bf16(prm, W_res, b_res)
@@ -570,47 +570,6 @@ _DENSE_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in
                "C_in", "C_out", "C_directed", "C_undirected", "C_all")
 
 
-def _dense_backward_torch(dY, Z, Y, prm, gate_mode, rows, res_x, W_res, act, slope):
-    """The dense backward as torch GPU ops (shapes the HIP kernels do not take: F_in or F_out % 4 != 0).
-    Same outputs as layer_dense_backward."""
-    M, F_in = Z.size(0), Z.size(1) // 3
-    dpre = dY * torch.where(Y > 0, 1.0, slope) if act else dY
-
-    def gate(name):
-        v = prm[name]
-        if gate_mode == 1:
-            return v.reshape(1, 1).expand(M, 1)
-        return (v[rows] if rows is not None else v[:M]).reshape(M, 1)
-
-    ci, co, cd, cu, ca = (gate(k) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"))
-    cad = ca * cd
-    s = [cad * ci, cad * co, ca * cu]
-    Wp = [prm["W_main_in"] + prm["W_shared"], prm["W_main_out"] + prm["W_shared"],
-          prm["W_undirected"] + prm["W_shared"]]
-    bp = [prm["b_main_in"] + prm["b_dir_shared_in"], prm["b_main_out"] + prm["b_dir_shared_out"],
-          prm["b_undirected"] + prm["b_undirected_shared"]]
-    dZ = torch.empty_like(Z)
-    ds, dB, db = [], [], []
-    for k in range(3):
-        Zk = Z[:, k * F_in:(k + 1) * F_in]
-        Gk = dpre @ Wp[k]
-        dZ[:, k * F_in:(k + 1) * F_in] = s[k] * Gk
-        ds.append((Gk * Zk).sum(1, keepdim=True) + dpre @ bp[k].reshape(-1, 1))
-        sd = s[k] * dpre
-        dB.append(sd.t() @ Zk)
-        db.append(sd.sum(0))
-    dres = None
-    if W_res is not None:
-        dres = dpre @ W_res
-        dB.append(dpre.t() @ res_x)
-    db.append(dpre.sum(0) if W_res is not None else torch.zeros_like(db[0]))
-    dgate = torch.stack([(ds[0] * cad).reshape(M), (ds[1] * cad).reshape(M),
-                         (ds[0] * ca * ci + ds[1] * ca * co).reshape(M), (ds[2] * ca).reshape(M),
-                         (ds[0] * cd * ci + ds[1] * cd * co + ds[2] * cu).reshape(M)])
-    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "dB": torch.cat(dB, 1),
-            "dbsum": torch.stack(db)}
-
-
 class LayerDense(torch.autograd.Function):
     """Y = act(sum_k s_k (Z_k W_k'^T + b_k') + constant[rows] + residual) (pg_directgcn_dense_f32).
 
@@ -644,15 +603,13 @@ class LayerDense(torch.autograd.Function):
         rows = rows if ctx.has_rows else None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
                                    act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
-        if out is None:  # shapes the HIP kernels do not take: the same algebra as torch GPU ops
-            if _is_bf16(Z):
-                out = _dense_backward_torch(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows,
-                                            None if res_x is None else res_x.float(), W_res, ctx.act, ctx.slope)
-                for k in ("dpre", "dZ", "dres"):
-                    if out[k] is not None:
-                        out[k] = out[k].to(torch.bfloat16)
-            else:
-                out = _dense_backward_torch(dY, Z, Y, prm, ctx.gate_mode, rows, res_x, W_res, ctx.act, ctx.slope)
+        if out is None:  # bf16 shapes the bf16 kernels do not take: the fp32 kernels on widened copies
+            out = layer_dense_backward(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows=rows,
+                                       res_x=None if res_x is None else res_x.float(), W_res=W_res, act=ctx.act,
+                                       slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
+            for k in ("dpre", "dZ", "dres"):
+                if out[k] is not None:
+                    out[k] = out[k].to(torch.bfloat16)
         dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]
         M, F_in = Z.size(0), Z.size(1) // 3
         g = {}
@@ -699,8 +656,9 @@ class LayerDense(torch.autograd.Function):
 
 class RowLinear(torch.autograd.Function):
     """y = x W^T + b over many rows (the decoder nn.Linear layers, protgram_directgcn.py:173-177, in
-    training). Forward and dx = dy W are torch GEMMs; (dW, db) -- a reduction over all M rows, which the
-    library GEMMs tile badly -- run in pg_gemm_at_b_f32."""
+    training). Forward and dx = dy W are plain library GEMMs (hipBLASLt through torch); (dW, db) -- a reduction
+    over all M rows, which the library GEMMs tile badly -- run in pg_gemm_at_b_f32 (shapes it does not take:
+    the library GEMM)."""
 
     @staticmethod
     @_fwd32

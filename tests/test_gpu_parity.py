@@ -414,14 +414,14 @@ def _dense_case(M, Fin, Fout, proj, vec, rows, seed):
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
                                                       (300, 32, 16, False, False, False), (513, 20, 12, True, True, False),
                                                       (129, 16, 40, True, True, True), (64, 128, 96, False, True, True),
-                                                      (5000, 32, 32, False, True, False), (300, 18, 10, True, True, False)])
-@pytest.mark.parametrize("hip", [True, False])
-def test_dense_backward_vs_float64(pkg, cuda, monkeypatch, M, Fin, Fout, proj, vec, rows, hip):
-    """Autograd of the fused dense layer (pg_directgcn_dense_bwd_f32, or the torch-GPU path for shapes it
-    does not take) against float64 autograd of protgram_directgcn.py:100-133 + residual + leaky_relu."""
+                                                      (5000, 32, 32, False, True, False), (300, 18, 10, True, True, False),
+                                                      (257, 7, 5, True, True, False), (100, 13, 30, False, True, True),
+                                                      (64, 6, 9, True, False, False)])
+def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+    """Autograd of the fused dense layer (pg_directgcn_dense_bwd_f32: the MFMA kernels, or its any-shape kernels
+    when F_in / F_out are not multiples of 4) against float64 autograd of protgram_directgcn.py:100-133 + residual
+    + leaky_relu."""
     from protgram_directgcn_amd import ops
-    if not hip:
-        monkeypatch.setattr(ops, "layer_dense_backward", lambda *a, **k: None)
     Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, vec, rows, 7 * M + Fin)
     gate = 0 if vec else 1
     # float64 reference through autograd
@@ -474,7 +474,7 @@ def test_dense_backward_x3_wgrad_vs_float64(pkg, cuda, monkeypatch, M, rows):
     autograd check as the default fp32 one."""
     from protgram_directgcn_amd._lib import PG_FLAG_DENSE_X3
     monkeypatch.setenv("PG_SPMM_FLAGS", hex(PG_FLAG_DENSE_X3))
-    test_dense_backward_vs_float64(pkg, cuda, monkeypatch, M, 128, 128, False, True, rows, True)
+    test_dense_backward_vs_float64(pkg, cuda, M, 128, 128, False, True, rows)
 
 
 def test_dense_backward_deterministic(pkg, cuda):

@@ -80,6 +80,46 @@ def _cpu_layer_dense_impl(Z, prm, gate_mode, rows=None, constant=None, res_x=Non
     return torch.nn.functional.leaky_relu(y, slope) if act else y
 
 
+def _cpu_layer_dense_backward(dY, Z, Y, prm, gate_mode, rows=None, res_x=None, W_res=None, b_res=None, act=False,
+                              slope=0.01, flags=None, need_dZ=True):
+    """CPU stand-in for ops.layer_dense_backward (pg_directgcn_dense_bwd_f32): the same outputs from torch ops."""
+    M, F_in = Z.size(0), Z.size(1) // 3
+    dpre = dY * torch.where(Y > 0, 1.0, slope) if act else dY
+
+    def gate(name):
+        v = prm[name]
+        if gate_mode == 1:
+            return v.reshape(1, 1).expand(M, 1)
+        return (v[rows] if rows is not None else v[:M]).reshape(M, 1)
+
+    ci, co, cd, cu, ca = (gate(k) for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"))
+    cad = ca * cd
+    s = [cad * ci, cad * co, ca * cu]
+    Wp = [prm["W_main_in"] + prm["W_shared"], prm["W_main_out"] + prm["W_shared"],
+          prm["W_undirected"] + prm["W_shared"]]
+    bp = [prm["b_main_in"] + prm["b_dir_shared_in"], prm["b_main_out"] + prm["b_dir_shared_out"],
+          prm["b_undirected"] + prm["b_undirected_shared"]]
+    dZ = torch.empty_like(Z)
+    ds, dB, db = [], [], []
+    for k in range(3):
+        Zk = Z[:, k * F_in:(k + 1) * F_in]
+        Gk = dpre @ Wp[k]
+        dZ[:, k * F_in:(k + 1) * F_in] = s[k] * Gk
+        ds.append((Gk * Zk).sum(1, keepdim=True) + dpre @ bp[k].reshape(-1, 1))
+        sd = s[k] * dpre
+        dB.append(sd.t() @ Zk)
+        db.append(sd.sum(0))
+    dres = None
+    if W_res is not None:
+        dres = dpre @ W_res
+        dB.append(dpre.t() @ res_x)
+    db.append(dpre.sum(0) if W_res is not None else torch.zeros_like(db[0]))
+    dgate = torch.stack([(ds[0] * cad).reshape(M), (ds[1] * cad).reshape(M),
+                         (ds[0] * ca * ci + ds[1] * ca * co).reshape(M), (ds[2] * ca).reshape(M),
+                         (ds[0] * cd * ci + ds[1] * cd * co + ds[2] * cu).reshape(M)])
+    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "dB": torch.cat(dB, 1), "dbsum": torch.stack(db)}
+
+
 def _worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [REPO, HERE]
@@ -133,7 +173,7 @@ def _train_worker(rank, world, port, out_q):
     ops.spmm3 = _cpu_spmm3
     ops.spmm3_t = _cpu_spmm3_t
     ops.layer_dense = _cpu_layer_dense
-    ops.layer_dense_backward = lambda *a, **k: None  # -> the torch formulation of the same backward
+    ops.layer_dense_backward = _cpu_layer_dense_backward
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         N, s, d, c = pkg.synth.de_bruijn_edges(2)

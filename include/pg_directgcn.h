@@ -184,8 +184,9 @@ int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row
 /* N-gram tile propagation (pg_ngram_spmm.hip). For a shared-pattern graph over ALL K^n n-grams (node id = the
  * base-K number of the n-gram, as the builder's sorted-string ids are when every n-gram occurs: data_builder.py
  * :164-175), the rows of each middle (n-2)-gram form a K x K grid whose out- and in-neighbour parts are dense
- * K x K blocks; one wave owns a 4 x 4 sub-block and reuses every source row it loads for 4 rows from registers
- * (11 source rows per output row at K = 20 instead of the CSR's ~41). Same aggregates as pg_spmm3_f32 /
+ * K x K blocks; a 4 x 4 sub-block is worked by two waves (forward: 2 a-rows x 4 b-columns each) or one
+ * (transposed), which reuse every source row they load for 2-4 rows from registers (16 source rows per output
+ * row in the forward at K = 20, 11 in the transposed, against the CSR's ~41). Same aggregates as pg_spmm3_f32 /
  * pg_spmm3_gated_f32 / pg_spmm3t_f32 (protgram_directgcn.py:101-112) up to fp32 summation order (FMA, slot
  * order); X must be finite (missing transitions are zero weights).
  *   pg_ngram_plan_floats: plan size in floats for (K, n, n_rows = K^n), or -1 when the shape is not supported
@@ -194,7 +195,7 @@ int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row
  *     number of entries that fit no slot -- a nonzero count means the graph is not an n-gram graph over K^n
  *     ids and the plan must not be used.
  *   pg_spmm3_ngram_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the store
- *     (as pg_spmm3_gated_f32). F = 64 or 128.
+ *     (as pg_spmm3_gated_f32). K = 20 (the amino-acid alphabet), F = 64 or 128; PG_ERR_UNSUPPORTED otherwise.
  *   pg_spmm3t_ngram_f32: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k).
  *     F = 64, 128 or 256. */
 int64_t pg_ngram_plan_floats(int K, int n, int64_t n_rows);

@@ -7,10 +7,11 @@
 //   out-source(i, c) = (M.b).c        -- the same K sources for every row a'.M.b (fixed b)
 //   in-source(i, c)  = c.(a.M)         -- the same K sources for every row a.M.b' (fixed a)
 // so the rows of one middle M form a K x K grid (a, b) whose out-part is a dense K x K block per column b and
-// whose in-part is a dense K x K block per row a. One wave owns a PA x PB sub-block of that grid: it loads the
-// PB*K out-sources and PA*K in-sources ONCE and applies each to the PA (resp. PB) rows that share it, from
-// registers. Per output row that is K(PA+PB)/(PA*PB) + 1 source rows (11 at 4x4, K=20) instead of the ~2K+1
-// the per-row CSR kernel gathers (41): the L1->VGPR gather traffic that bounds pg_spmm3_f32 drops ~3.7x.
+// whose in-part is a dense K x K block per row a. A PA x PB sub-block of that grid is worked by one wave (the
+// transposed kernel) or two (the forward, AH = PA/2 a-rows each): a wave loads its sub-block's out- and
+// in-sources ONCE per step and applies each to every row of its sub-block that shares it, from registers. Per
+// output row that is K(PA+PB)/(PA*PB) + 1 source rows (11 at 4x4, K=20; 16 in the forward's two-wave split)
+// instead of the ~2K+1 the per-row CSR kernel gathers (41).
 //
 // The weights come from the CSR (pg_ngram_plan_f32 scatters every entry into its slot): entry (i, j) goes to
 // out-slot c = j mod K if j = out-source(i, c), else to in-slot c = j div K^(n-1) if j = in-source(i, c), else to

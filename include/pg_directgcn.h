@@ -197,7 +197,9 @@ int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row
  *   pg_spmm3_ngram_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the store
  *     (as pg_spmm3_gated_f32). K = 20 (the amino-acid alphabet), F = 64 or 128; PG_ERR_UNSUPPORTED otherwise.
  *   pg_spmm3t_ngram_f32: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k).
- *     F = 64, 128 or 256. */
+ *     F = 64, 128 or 256.
+ *   pg_spmm3t_ngram_bf16: the transposed kernel on bf16 rows (the model's bf16 mode; replaces pg_spmm3t_bf16 on
+ *     such graphs): fp32 sums, rounded once to bf16. F = 64, 128 or 256. */
 int64_t pg_ngram_plan_floats(int K, int n, int64_t n_rows);
 int pg_ngram_plan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, float* plan,
                       int64_t plan_floats, int* bad, void* stream);
@@ -205,6 +207,8 @@ int pg_spmm3_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const fl
                        const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream);
 int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
                         float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
+                         uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

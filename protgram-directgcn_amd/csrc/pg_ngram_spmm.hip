@@ -24,6 +24,7 @@
 // FMAs in (out-slots, in-slots, diagonal) order instead of the CSR's ascending-column order: within fp32 rounding
 // of the reference (tests: |d| <= 1e-5 + 1e-5|ref|), not bit-exact like pg_spmm3_f32. Zero-weight slots add
 // 0 * x, so the inputs must be finite (an inf in a row adjacent in the grid would turn into NaN).
+#include "pg_bf16_util.h"
 #include "pg_common.h"
 
 namespace {
@@ -43,6 +44,8 @@ struct NgramP {
     int accumulate;
     const float *g_in, *g_out, *g_dir, *g_und, *g_all;
     int gate_scalar;
+    const uint16_t* Xb;  // bf16 mode (BF kernels): X / G and Z / dX as bf16 rows; sums stay fp32, one rounding
+    uint16_t* Zb;
 };
 
 template <int VEC>
@@ -118,6 +121,29 @@ __device__ __forceinline__ float first_of(float4 v) { return v.x; }
 // i0..i1 are one contiguous run of slots.
 __device__ __forceinline__ int plan_slot(int i, int jb, int PB) { return i * PB + jb; }
 
+// VEC consecutive bf16 of a row as fp32 / fp32 rounded to VEC bf16 (round to nearest even, as torch)
+template <int VEC>
+__device__ __forceinline__ typename VT<VEC>::T ld_bf(const uint16_t* q) {
+    if constexpr (VEC == 1) {
+        return __uint_as_float((uint32_t)*q << 16);
+    } else if constexpr (VEC == 2) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(q);
+        return make_float2(pgbf::lo(w), pgbf::hi(w));
+    } else {
+        return pgbf::unpack4(*reinterpret_cast<const uint2*>(q));
+    }
+}
+template <int VEC>
+__device__ __forceinline__ void st_bf(uint16_t* q, const typename VT<VEC>::T& v) {
+    if constexpr (VEC == 1) {
+        *q = (uint16_t)pgbf::f2bf(v);
+    } else if constexpr (VEC == 2) {
+        *reinterpret_cast<uint32_t*>(q) = pgbf::pack2(v.x, v.y);
+    } else {
+        *reinterpret_cast<uint2*>(q) = pgbf::pack4(v);
+    }
+}
+
 // Forward: Z[i] = [A_in X | A_out X | A_und X][i] (optionally gated at the store, as pg_spmm3_gated_f32).
 // A workgroup (4 waves) first stages its plan blocks in LDS (coalesced 16-B loads); each wave then owns AH of a
 // block's PA a-rows (AH = PA/2: two waves per block, which halves the accumulators and raises occupancy) and runs the
@@ -135,7 +161,7 @@ __device__ __forceinline__ int plan_slot(int i, int jb, int PB) { return i * PB 
 // shrink with the bytes; 4 x 5 plan blocks with the two blocks of a workgroup sharing their in-sources through a
 // register-staged LDS slab 0.274 (this kernel on 4 x 5 blocks: 0.170). This kernel is texture-data bound (TD
 // 90 % busy, ~30 cycles per 8-B wave load; PMC, profiles/r02_pmc_summary.txt).
-template <int K, int VEC, int PA, int PB, int AH, int NB, bool GATED>
+template <int K, int VEC, int PA, int PB, int AH, int NB, bool GATED, bool BF = false>
 __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
     static_assert(K % NB == 0, "the c loop runs in rounds of NB steps");
     using V = typename VT<VEC>::T;
@@ -165,6 +191,10 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
     const float* __restrict__ W = wl[wave / WPB];
     const V* __restrict__ X = reinterpret_cast<const V*>(p.X);
     const int64_t ldxv = p.ldx / VEC;
+    auto xrow = [&](int64_t row) -> V {  // this lane's VEC features of source row `row`
+        if constexpr (BF) return ld_bf<VEC>(p.Xb + row * p.ldx + lane * VEC);
+        else return (X + row * ldxv)[lane];
+    };
     V acc[R][3];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -174,9 +204,9 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
     const int64_t ib = (int64_t)a0 * p.Kn2 + M;  // in-source (a0 + i, c) = c*K^(n-1) + ib + i*K^(n-2)
     auto load = [&](int c, V (&o)[PB], V (&in)[AH]) {
 #pragma unroll
-        for (int j = 0; j < PB; ++j) o[j] = (X + (ob + (int64_t)j * K + c) * ldxv)[lane];
+        for (int j = 0; j < PB; ++j) o[j] = xrow(ob + (int64_t)j * K + c);
 #pragma unroll
-        for (int i = 0; i < AH; ++i) in[i] = (X + ((int64_t)c * p.Kn1 + ib + (int64_t)i * p.Kn2) * ldxv)[lane];
+        for (int i = 0; i < AH; ++i) in[i] = xrow((int64_t)c * p.Kn1 + ib + (int64_t)i * p.Kn2);
     };
     // the wave's rows are plan slots half*R .. half*R + R - 1 of each 3*RB-float (step, type) chunk
     auto step = [&](int c, const V (&o)[PB], const V (&in)[AH]) {
@@ -227,7 +257,7 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
         for (int j = 0; j < PB; ++j) {
             const int r = i * PB + j;
             const int64_t row = (int64_t)(a0 + i) * p.Kn1 + M * K + b0 + j;
-            const V xs = (X + row * ldxv)[lane];
+            const V xs = xrow(row);
             float s[3] = {1.f, 1.f, 1.f};
             if constexpr (GATED) {
                 auto gate = [&](int q) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv), r * 5 + q)); };
@@ -236,15 +266,20 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
                 s[1] = cad * gate(1);
                 s[2] = gate(4) * gate(3);
             }
-            V* zr = reinterpret_cast<V*>(p.Z + row * p.ldz);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 fma_v<VEC>(acc[r][k], ws[r * 3 + k], xs);
                 V v = acc[r][k];
                 if constexpr (GATED) v = scale_v<VEC>(v, s[k]);
-                V* dst = zr + (int64_t)k * (p.F / VEC) + lane;
-                if (p.accumulate) v = add_v<VEC>(*dst, v);
-                *dst = v;
+                if constexpr (BF) {
+                    uint16_t* dst = p.Zb + row * p.ldz + (int64_t)k * p.F + lane * VEC;
+                    if (p.accumulate) v = add_v<VEC>(ld_bf<VEC>(dst), v);
+                    st_bf<VEC>(dst, v);
+                } else {
+                    V* dst = reinterpret_cast<V*>(p.Z + row * p.ldz) + (int64_t)k * (p.F / VEC) + lane;
+                    if (p.accumulate) v = add_v<VEC>(*dst, v);
+                    *dst = v;
+                }
             }
         }
 }
@@ -254,7 +289,7 @@ __global__ __launch_bounds__(256) void ngram_spmm3_kernel(NgramP p) {
 // accumulator per row, so all PA*PB rows fit), the three slices of every source row gathered per step, weights
 // through the scalar cache. Measured at B(20,4), F=128: 0.218 ms against 0.380 for the CSR kernel; the forward
 // kernel's structure (LDS weights, two waves per block, a ring of source sets) measured 0.273 here.
-template <int VEC, int PA, int PB>
+template <int VEC, int PA, int PB, bool BF = false>
 __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
     using V = typename VT<VEC>::T;
     constexpr int R = PA * PB;
@@ -271,6 +306,10 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
     const V* __restrict__ G = reinterpret_cast<const V*>(p.X);
     const int64_t ldgv = p.ldx / VEC;
     const int Fv = p.F / VEC;
+    auto gslice = [&](int64_t row, int k) -> V {  // this lane's VEC features of slice k of row `row`
+        if constexpr (BF) return ld_bf<VEC>(p.Xb + row * p.ldx + (int64_t)k * p.F + lane * VEC);
+        else return G[row * ldgv + (int64_t)k * Fv + lane];
+    };
     V acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = zero_v<VEC>();
@@ -280,15 +319,13 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
         V xo[PB][3], xi[PA][3];
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
-            const V* src = G + (ob + (int64_t)j * p.K + c) * ldgv + lane;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) xo[j][k] = src[k * Fv];
+            for (int k = 0; k < 3; ++k) xo[j][k] = gslice(ob + (int64_t)j * p.K + c, k);
         }
 #pragma unroll
         for (int i = 0; i < PA; ++i) {
-            const V* src = G + ((int64_t)c * p.Kn1 + ib + (int64_t)i * p.Kn2) * ldgv + lane;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) xi[i][k] = src[k * Fv];
+            for (int k = 0; k < 3; ++k) xi[i][k] = gslice((int64_t)c * p.Kn1 + ib + (int64_t)i * p.Kn2, k);
         }
         const float* __restrict__ wc = W + (int64_t)c * 6 * R;
 #pragma unroll
@@ -308,13 +345,18 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
         for (int j = 0; j < PB; ++j) {
             const int r = i * PB + j, sl = plan_slot(i, j, PB);
             const int64_t row = (int64_t)(a0 + i) * p.Kn1 + M * p.K + b0 + j;
-            const V* src = G + row * ldgv + lane;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) fma_v<VEC>(acc[r], ws[sl * 3 + k], src[k * Fv]);
-            V* dst = reinterpret_cast<V*>(p.Z + row * p.ldz) + lane;
+            for (int k = 0; k < 3; ++k) fma_v<VEC>(acc[r], ws[sl * 3 + k], gslice(row, k));
             V v = acc[r];
-            if (p.accumulate) v = add_v<VEC>(*dst, v);
-            *dst = v;
+            if constexpr (BF) {
+                uint16_t* dst = p.Zb + row * p.ldz + lane * VEC;
+                if (p.accumulate) v = add_v<VEC>(ld_bf<VEC>(dst), v);
+                st_bf<VEC>(dst, v);
+            } else {
+                V* dst = reinterpret_cast<V*>(p.Z + row * p.ldz) + lane;
+                if (p.accumulate) v = add_v<VEC>(*dst, v);
+                *dst = v;
+            }
         }
 }
 
@@ -372,47 +414,51 @@ bool pow_ok(int K, int n, int64_t n_rows, int64_t& Kn1, int64_t& Kn2) {
     return v == n_rows;
 }
 
-template <int VEC, bool T>
+template <int VEC, bool T, bool BF>
 int launch(const NgramP& p, hipStream_t s, bool gated) {
     const int64_t nwb = (p.n_rows / ((int64_t)p.K * p.K)) * (p.K / PLAN_PA) * (p.K / PLAN_PB);
     const unsigned nb = (unsigned)((nwb + 3) / 4);
     if constexpr (T) {
-        hipLaunchKernelGGL((ngram_spmm3t_kernel<VEC, PLAN_PA, PLAN_PB>), dim3(nb), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((ngram_spmm3t_kernel<VEC, PLAN_PA, PLAN_PB, BF>), dim3(nb), dim3(256), 0, s, p);
     } else {
         if (p.K != 20) return pg::set_error(PG_ERR_UNSUPPORTED, "n-gram forward kernel built for K = 20");
         const unsigned nb2 = (unsigned)((nwb + 1) / 2);  // two waves per plan block
-        if (gated) hipLaunchKernelGGL((ngram_spmm3_kernel<20, VEC, PLAN_PA, PLAN_PB, PLAN_PA / 2, 2, true>), dim3(nb2), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((ngram_spmm3_kernel<20, VEC, PLAN_PA, PLAN_PB, PLAN_PA / 2, 2, false>), dim3(nb2), dim3(256), 0, s, p);
+        if (gated) hipLaunchKernelGGL((ngram_spmm3_kernel<20, VEC, PLAN_PA, PLAN_PB, PLAN_PA / 2, 2, true, BF>), dim3(nb2), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((ngram_spmm3_kernel<20, VEC, PLAN_PA, PLAN_PB, PLAN_PA / 2, 2, false, BF>), dim3(nb2), dim3(256), 0, s, p);
     }
     return PG_OK;
 }
 
+// fp32: F = 64 / 128 (forward), 64 / 128 / 256 (transposed); bf16: the transposed kernel, F = 64 / 128 / 256. (A
+// bf16 forward measured slower than pg_spmm3_bf16's 16-B gathers -- 0.154 vs 0.129 ms at B(20,4), F = 128, 0.284
+// vs 0.245 at F = 256: 4-B lane loads cost the texture path about what 8-B ones do -- and is not exported.)
+template <bool BF>
 int run(NgramP p, bool transposed, bool gated, uint32_t flags, hipStream_t s, const char* name) {
+    if (BF && !transposed) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: bf16 forward not built", name);
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     const int64_t width = transposed ? 3 * (int64_t)p.F : p.F;
-    const bool al = pg::aligned16(p.X) && pg::aligned16(p.Z) && p.ldx % 4 == 0 && p.ldz % 4 == 0;
+    const int eb = BF ? 2 : 4;  // element bytes
+    const void* xp = BF ? (const void*)p.Xb : (const void*)p.X;
+    const void* zp = BF ? (const void*)p.Zb : (const void*)p.Z;
+    const bool al = pg::aligned16(xp) && pg::aligned16(zp) && (p.ldx * eb) % 16 == 0 && (p.ldz * eb) % 16 == 0;
     if (!al || p.ldx < width) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned rows", name);
+    int rc = PG_OK;
     switch (p.F) {
-        case 64: {
-            const int rc = transposed ? launch<1, true>(p, s, false) : launch<1, false>(p, s, gated);
-            if (rc) return rc;
+        case 64:
+            if constexpr (BF) rc = launch<1, true, BF>(p, s, false);
+            else rc = transposed ? launch<1, true, BF>(p, s, false) : launch<1, false, BF>(p, s, gated);
             break;
-        }
-        case 128: {
-            const int rc = transposed ? launch<2, true>(p, s, false) : launch<2, false>(p, s, gated);
-            if (rc) return rc;
+        case 128:
+            if constexpr (BF) rc = launch<2, true, BF>(p, s, false);
+            else rc = transposed ? launch<2, true, BF>(p, s, false) : launch<2, false, BF>(p, s, gated);
             break;
-        }
         case 256:
-            if (transposed) {
-                const int rc = launch<4, true>(p, s, false);
-                if (rc) return rc;
-            } else {
-                return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F = 256 forward not built", name);
-            }
+            if (!transposed) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F = 256 forward not built", name);
+            rc = launch<4, true, BF>(p, s, false);
             break;
-        default: return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be 64 or 128 (256: transposed)", name);
+        default: return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be 64, 128 or 256", name);
     }
+    if (rc) return rc;
     return pg::check_launch(name);
 }
 
@@ -473,7 +519,7 @@ int pg_spmm3_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const fl
         p.g_all = gates->C_all;
         p.gate_scalar = gates->gate_mode == PG_GATES_SCALAR;
     }
-    return run(p, false, gates != nullptr, flags, (hipStream_t)stream, "pg_spmm3_ngram_f32");
+    return run<false>(p, false, gates != nullptr, flags, (hipStream_t)stream, "pg_spmm3_ngram_f32");
 }
 
 int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
@@ -496,7 +542,30 @@ int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const f
     p.ldz = lddx;
     p.F = (int)F;
     p.accumulate = accumulate ? 1 : 0;
-    return run(p, true, false, flags, (hipStream_t)stream, "pg_spmm3t_ngram_f32");
+    return run<false>(p, true, false, flags, (hipStream_t)stream, "pg_spmm3t_ngram_f32");
+}
+
+int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
+                         uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+    int64_t Kn1 = 0, Kn2 = 0;
+    PG_REQUIRE(pow_ok(K, n, n_rows, Kn1, Kn2) && K % PLAN_PA == 0 && K % PLAN_PB == 0, "bad n-gram shape");
+    PG_REQUIRE(plan && G && dX, "null pointer");
+    PG_REQUIRE(ldg >= 3 * F && lddx >= F, "leading dimensions too small");
+    NgramP p{};
+    p.K = K;
+    p.n = n;
+    p.Kn1 = Kn1;
+    p.Kn2 = Kn2;
+    p.n_rows = n_rows;
+    p.plan = plan;
+    p.blk = blk_floats(K, PLAN_PA, PLAN_PB);
+    p.Xb = G;
+    p.ldx = ldg;
+    p.Zb = dX;
+    p.ldz = lddx;
+    p.F = (int)F;
+    p.accumulate = accumulate ? 1 : 0;
+    return run<true>(p, true, false, flags, (hipStream_t)stream, "pg_spmm3t_ngram_bf16");
 }
 
 }  // extern "C"

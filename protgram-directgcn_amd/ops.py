@@ -86,10 +86,10 @@ def _is_bf16(t) -> bool:
 # ------------------------------------------------------------------------------------------------
 # raw kernel calls
 # ------------------------------------------------------------------------------------------------
-def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128)) -> bool:
-    """The n-gram tile kernels take this call: the graph has a plan, x is fp32 with a supported width and exactly
-    the graph's rows, and PG_FLAG_NO_NGRAM is not set."""
-    return (g.ngram is not None and not (fl & PG_FLAG_NO_NGRAM) and x.dtype == torch.float32
+def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128), dtype=torch.float32) -> bool:
+    """The n-gram tile kernels take this call: the graph has a plan, x has the kernel's dtype, a supported width
+    and exactly the graph's rows, and PG_FLAG_NO_NGRAM is not set."""
+    return (g.ngram is not None and not (fl & PG_FLAG_NO_NGRAM) and x.dtype == dtype
             and x.size(0) == g.n_rows and x.size(1) in widths)
 
 
@@ -205,6 +205,13 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
             dX = torch.empty(N, F, device=G.device, dtype=torch.bfloat16)
             ro = g.row_order if g.symmetric else None
             fl = default_flags() if flags is None else flags
+            if g.symmetric and G.size(0) == g.n_rows and _ngram_ok(g, dX, fl, (64, 128, 256), torch.bfloat16):
+                ng = g.ngram
+                rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, N, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,
+                                              fl, _stream(G))
+                if rc != _lib.PG_ERR_UNSUPPORTED:
+                    check(rc, "pg_spmm3t_ngram_bf16")
+                    return dX
             rc = lib.pg_spmm3t_bf16(N, _p(g.rowptr_t), _p(ro), _p(g.edges3_t), _p(G), G.stride(0), F, _p(dX),
                                     dX.stride(0), fl, _stream(G))
             if rc != _lib.PG_ERR_UNSUPPORTED:

@@ -94,3 +94,20 @@ def test_ngram_spmm3_vs_oracle_and_fallback_widths(pkg, cuda):
                 assert torch.equal(Z[:, j * F:(j + 1) * F], ref), j
             else:
                 assert_close(Z[:, j * F:(j + 1) * F], ref, f"oracle {j}")
+
+
+@pytest.mark.parametrize("n,keep", [(3, 1.0), (3, 0.5), (4, 1.0)])
+@pytest.mark.parametrize("F", [64, 128, 256])
+def test_ngram_transposed_bf16(pkg, cuda, n, keep, F):
+    """pg_spmm3t_ngram_bf16 (bf16 rows, fp32 sums, one rounding) against the fp32 kernel on the widened bf16 input
+    and against the bf16 CSR kernel: within one bf16 ulp (|d| <= 2^-7 |ref| + 1e-6)."""
+    from protgram_directgcn_amd import ops
+    g = _graph(pkg, cuda, n, keep)
+    G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(n * 10 + F)).to(cuda).to(torch.bfloat16)
+    got = ops.spmm3_t(g, G)
+    assert got.dtype == torch.bfloat16
+    for other, tag in ((ops.spmm3_t(g, G.float(), flags=_csr_flag()), "fp32"),
+                       (ops.spmm3_t(g, G, flags=_csr_flag()).float(), "bf16 CSR")):
+        d = (got.float() - other).abs()
+        bad = d > 2.0 ** -7 * other.abs() + 1e-6
+        assert not bool(bad.any()), (tag, int(bad.sum()), float(d.max()))

@@ -8,7 +8,9 @@
 // softmax in LDS. Replaces 6+ framework launches and two re-reads of h.
 // Fast path: F <= 256, H <= 128, C <= 64 (F, H multiples of 4); other shapes use a one-wave-per-row
 // fallback kernel. The model's own shape (F = 128 -> 64 -> C <= 32) runs head_x3_kernel (split-bf16 decoder 1;
-// head_f128_kernel, its fp32-MFMA predecessor, with -DPG_HEAD_FP32).
+// head_f128_kernel, its fp32-MFMA predecessor, with -DPG_HEAD_FP32). A persistent form of head_x3_kernel (W1 splits
+// and W2 kept in registers across a block's 32-row tiles, next tile's rows loaded behind the math; 128 VGPRs, four
+// blocks per CU) measured 0.062 ms against 0.050 for one tile per block.
 #include "pg_common.h"
 #include "pg_split3.h"
 

@@ -195,7 +195,8 @@ int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row
  *     number of entries that fit no slot -- a nonzero count means the graph is not an n-gram graph over K^n
  *     ids and the plan must not be used.
  *   pg_spmm3_ngram_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the store
- *     (as pg_spmm3_gated_f32). K = 20 (the amino-acid alphabet), F = 64 or 128; PG_ERR_UNSUPPORTED otherwise.
+ *     (as pg_spmm3_gated_f32). K = 20 (the amino-acid alphabet), F = 64, 128 or 256 (two column halves);
+ *     PG_ERR_UNSUPPORTED otherwise.
  *   pg_spmm3t_ngram_f32: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k).
  *     F = 64, 128 or 256.
  *   pg_spmm3t_ngram_bf16: the transposed kernel on bf16 rows (the model's bf16 mode; replaces pg_spmm3t_bf16 on

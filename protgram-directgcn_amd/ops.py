@@ -110,7 +110,7 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     fl = default_flags() if flags is None else flags
     s = _stream(x)
     ev = _ev_start(x)
-    if g.shared and not fused and _ngram_ok(g, x, fl):
+    if g.shared and not fused and _ngram_ok(g, x, fl, (64, 128, 256)):
         ng = g.ngram
         rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, None, _p(Z), Z.stride(0), fl, s)
         if rc != _lib.PG_ERR_UNSUPPORTED:  # unaligned operands: the CSR kernel below
@@ -177,7 +177,7 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     a, keep = _layer_args(None, prm, gate_mode, M=N)
     fl = default_flags() if flags is None else flags
     ev = _ev_start(x)
-    if _ngram_ok(g, x, fl):
+    if _ngram_ok(g, x, fl, (64, 128, 256)):
         ng = g.ngram
         rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, ctypes.byref(a), _p(Z),
                                     Z.stride(0), fl, _stream(x))

@@ -43,7 +43,7 @@ def test_plan_only_for_ngram_graphs(pkg, cuda):
 
 
 @pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
-@pytest.mark.parametrize("F", [64, 128])
+@pytest.mark.parametrize("F", [64, 128, 256])
 def test_ngram_spmm3_vs_csr(pkg, cuda, n, keep, F):
     from protgram_directgcn_amd import ops
     g = _graph(pkg, cuda, n, keep)

@@ -643,12 +643,15 @@ class LayerDense(torch.autograd.Function):
                 g[name] = full
         d_const = None
         if constant is not None and ctx.needs_input_grad[2]:
-            d_const = torch.zeros_like(constant)
             dp = dpre.to(constant.dtype)
-            if rows is not None:
-                d_const.index_add_(0, rows, dp)
+            if rows is None and constant.size(0) == M:
+                d_const = dp  # every row of the constant receives exactly its dpre row (no zero-fill + add pass)
             else:
-                d_const[:M] += dp
+                d_const = torch.zeros_like(constant)
+                if rows is not None:
+                    d_const.index_add_(0, rows, dp)
+                else:
+                    d_const[:M] += dp
         d_res = d_wres = d_bres = None
         if res_x is not None:
             if W_res is None:

@@ -660,8 +660,8 @@ def test_head_bf16_input_equals_widened(pkg, cuda, F, H, C):
                                                       (300, 32, 16, False, False, False), (5000, 256, 256, False, True, False),
                                                       (129, 16, 40, True, True, True), (300, 20, 12, True, True, False)])
 def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
-    """bf16-mode autograd of the dense layer (pg_directgcn_dense_bwd_bf16; the last case falls back to the
-    torch formulation) against float64 autograd on the same bf16-valued activations, with the leaky_relu
+    """bf16-mode autograd of the dense layer (pg_directgcn_dense_bwd_bf16; the last case, F not a multiple of 8,
+    runs the fp32 backward kernels on widened copies) against float64 autograd on the same bf16-valued activations, with the leaky_relu
     mask taken from the device's own (bf16) forward output -- near y = 0 a float64 forward can pick the
     other slope. Tolerance: bf16 rounding of dpre, s*Z and the stored gradients, 2% of each gradient's max."""
     from protgram_directgcn_amd import ops

@@ -1,0 +1,37 @@
+"""bench.py's JSON contract on the GPU (a short run of the default workload in a child process): one JSON line with
+the BASELINE.json metric, and the roofline / throughput fields consistent with each other."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(300)
+def test_bench_json_line_is_self_consistent():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-pmc"], cwd=REPO, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert out["metric"] == json.load(f)["metric"]
+    assert out["n_gpus"] == 1 and out["steps"] == 5 and out["warmup"] == 2 and out["higher_is_better"] is True
+    cfg = out["config"]
+    assert cfg["num_nodes"] == 160_000 and cfg["nnz_per_adjacency"] == 6_559_580 and cfg["feat_dim"] == 128
+    edges = 3 * cfg["nnz_per_adjacency"] * cfg["layers"]
+    assert abs(out["value"] - edges / (out["ms_per_step"] * 1e-3)) <= 2e-3 * out["value"]
+    rf = out["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    achieved = rf["algorithmic_bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
+    assert abs(rf["achieved"] - achieved) <= 1e-3 * achieved + 0.1
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) <= 1e-3
+    assert 0.0 < rf["frac"] < 1.0  # compulsory bytes: physically below peak
+    # the propagation is one of the step's kernels: its launches take less than the whole step
+    assert rf["avg_launch_ms"] < out["ms_per_step"]

@@ -147,10 +147,16 @@ def gather_plan(part: NodeRangePartition, chunks: int) -> GatherPlan:
 
 
 def _dense_local(conv, part: NodeRangePartition, Z, res: nn.Module, res_x, a: int, b: int, out=None, act=True):
+    """The dense layer over owned rows [r0 + a, r0 + b). They are one contiguous id range, so the per-node gates and
+    constant are passed as row slices (no row map): the split-bf16 kernels take the call, as on one GPU."""
     prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
     vec = conv.use_vector_coeffs
-    rows = part.rows[a:b] if vec else None
-    constant = conv.constant.detach() if vec else None
+    rows, constant = None, None
+    if vec:
+        lo, hi = part.r0 + a, part.r0 + b
+        for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+            prm[k] = prm[k][lo:hi]
+        constant = conv.constant.detach()[lo:hi] if conv.constant is not None else None
     W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
     return ops.layer_dense(Z, prm, 0 if vec else 1, rows=rows, constant=constant, res_x=res_x, W_res=W_res,
                            b_res=b_res, act=act, out=out)

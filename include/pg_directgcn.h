@@ -321,9 +321,13 @@ typedef struct pg_adam_desc {
     int64_t numel;
 } pg_adam_desc_t;
 
+/* sq_partial (optional, [nchunks]): per-chunk sums of p^2 of the parameters BEFORE the update -- the value of the
+ * trainer's L2 term (protgram_directgcn_trainer.py:96) from the pass that reads p anyway; written on skipped
+ * (found_inf) steps too. pg_multi_sum_f32 adds n partials in fixed order (deterministic). */
 int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
                 double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
-                const float* found_inf, void* stream);
+                const float* found_inf, float* sq_partial, void* stream);
+int pg_multi_sum_f32(int64_t n, const float* x, float* out, void* stream);
 
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.

@@ -5,7 +5,9 @@
 //   pg_multi_sqsum_f32 -- sum_t sum_i x_t[i]^2 over a list of tensors in one launch (fixed-order two-level
 //                         reduction: deterministic), the L2 value;
 //   pg_multi_axpy_f32  -- y_t += alpha * x_t for every tensor of a list in one launch (the L2 gradient
-//                         2*lambda*p added to p.grad).
+//                         2*lambda*p added to p.grad);
+//   pg_adam_f32        -- Adam over the list in one launch, optionally with the L2 value of the pre-update
+//                         parameters as per-chunk partials (pg_multi_sum_f32 adds them in fixed order).
 // A list is a device array of pg_tensor_desc_t; work is split into fixed 64K-element chunks.
 #include "pg_common.h"
 
@@ -100,11 +102,26 @@ __global__ __launch_bounds__(256) void axpy_chunks_kernel(int ntens, const pg_te
 //   g  = grad * inv_scale (+ weight_decay * p)
 //   m  = lerp(m, g, 1 - beta1) ; v = v * beta2 + (1 - beta2) * g * g
 //   p += (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps),   bc_k = 1 - beta_k^t  (t = step + 1, in double)
-// Skipped entirely when *found_inf != 0 (GradScaler's device-side flag; no host sync).
+// Skipped when *found_inf != 0 (GradScaler's device-side flag; no host sync). sq_partial (optional): chunk b's
+// sum of p^2 BEFORE the update into sq_partial[b] -- the trainer's L2 value from the pass that reads p anyway
+// (computed on skipped steps too, as the reference's loss includes it).
+__device__ __forceinline__ float block_sum256(float s) {
+    __shared__ float red[256];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    return red[0];
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc_t* d, const int64_t* chunk_ptr,
                                                    double lr, double beta1, double beta2, float eps, float weight_decay,
-                                                   const float* step, const float* grad_scale, const float* found_inf) {
-    if (found_inf && found_inf[0] != 0.f) return;
+                                                   const float* step, const float* grad_scale, const float* found_inf,
+                                                   float* sq_partial) {
+    const bool skip = found_inf && found_inf[0] != 0.f;
+    if (skip && !sq_partial) return;
     const int64_t b = blockIdx.x;
     int lo = 0, hi = ntens;
     while (hi - lo > 1) {
@@ -134,6 +151,13 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
     const bool vec = ((reinterpret_cast<uintptr_t>(t.g) | reinterpret_cast<uintptr_t>(t.p) |
                        reinterpret_cast<uintptr_t>(t.m) | reinterpret_cast<uintptr_t>(t.v)) & 15) == 0;
     int64_t i0 = beg;
+    float sq = 0.f;
+    if (skip) {  // L2 value only
+        for (int64_t i = beg + threadIdx.x; i < end; i += 256) sq += t.p[i] * t.p[i];
+        sq = block_sum256(sq);
+        if (threadIdx.x == 0) sq_partial[b] = sq;
+        return;
+    }
     if (vec) {
         const int64_t n4 = (end - beg) >> 2;
         for (int64_t k = threadIdx.x; k < n4; k += 256) {
@@ -142,6 +166,7 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
             float4 p = *reinterpret_cast<const float4*>(t.p + i);
             float4 m = *reinterpret_cast<const float4*>(t.m + i);
             float4 v = *reinterpret_cast<const float4*>(t.v + i);
+            sq += p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
             upd(g.x, p.x, m.x, v.x);
             upd(g.y, p.y, m.y, v.y);
             upd(g.z, p.z, m.z, v.z);
@@ -154,10 +179,15 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
     }
     for (int64_t i = i0 + threadIdx.x; i < end; i += 256) {
         float p = t.p[i], m = t.m[i], v = t.v[i];
+        sq += p * p;
         upd(t.g[i], p, m, v);
         t.p[i] = p;
         t.m[i] = m;
         t.v[i] = v;
+    }
+    if (sq_partial) {
+        sq = block_sum256(sq);
+        if (threadIdx.x == 0) sq_partial[b] = sq;
     }
 }
 
@@ -193,16 +223,22 @@ int pg_multi_axpy_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* c
     return pg::check_launch("pg_multi_axpy_f32");
 }
 
+int pg_multi_sum_f32(int64_t n, const float* x, float* out, void* stream) {
+    PG_REQUIRE(n >= 0 && out && (n == 0 || x), "bad arguments");
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, x, out);
+    return pg::check_launch("pg_multi_sum_f32");
+}
+
 int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
                 double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
-                const float* found_inf, void* stream) {
+                const float* found_inf, float* sq_partial, void* stream) {
     PG_REQUIRE(ntens >= 0 && nchunks >= 0 && step, "bad arguments");
     PG_REQUIRE(beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && lr >= 0 && eps >= 0, "bad hyper-parameters");
     hipStream_t s = (hipStream_t)stream;
     if (nchunks > 0) {
         PG_REQUIRE(descs && chunk_ptr, "null pointer");
         hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(256), 0, s, ntens, descs, chunk_ptr, lr, beta1, beta2,
-                           (float)eps, (float)weight_decay, (const float*)step, grad_scale, found_inf);
+                           (float)eps, (float)weight_decay, (const float*)step, grad_scale, found_inf, sq_partial);
     }
     hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(1), 0, s, step, found_inf);
     return pg::check_launch("pg_adam_f32");

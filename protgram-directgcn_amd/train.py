@@ -181,6 +181,9 @@ class Adam(torch.optim.Optimizer):
         grad_scale = getattr(self, "grad_scale", None)
         found_inf = getattr(self, "found_inf", None)
         lib = load_library()
+        # train_step's fused L2 value: per-chunk sums of p^2 (pre-update) from every launch, added at the end
+        want_sq = getattr(self, "_want_sqsum", False)
+        sq_parts = []
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -206,16 +209,25 @@ class Adam(torch.optim.Optimizer):
                 grads = [p.grad.contiguous() for p in members]
                 tl = TensorList(members, grads, [self.state[p]["exp_avg"] for p in members],
                                 [self.state[p]["exp_avg_sq"] for p in members])
+                if want_sq:
+                    sq_parts.append(tl.partial[:tl.nchunks])
                 check(lib.pg_adam_f32(len(members), ctypes.c_void_p(tl.desc.data_ptr()),
                                       ctypes.c_void_p(tl.chunk_ptr.data_ptr()), tl.nchunks, float(group["lr"]),
                                       float(b1), float(b2), float(group["eps"]),
                                       float(group["weight_decay"]) + float(getattr(self, "_l2_extra", 0.0)),
                                       ctypes.c_void_p(step.data_ptr()),
                                       ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
-                                      ctypes.c_void_p(fi.data_ptr()) if fi is not None else None, _stream(dev)),
+                                      ctypes.c_void_p(fi.data_ptr()) if fi is not None else None,
+                                      ctypes.c_void_p(tl.partial.data_ptr()) if want_sq else None, _stream(dev)),
                       "pg_adam_f32")
             for p in ps:  # written in place by the kernel: let autograd / version-keyed caches see it
                 torch.autograd.graph.increment_version(p)
+        if want_sq:
+            parts = torch.cat(sq_parts) if len(sq_parts) > 1 else sq_parts[0]
+            out = torch.empty((), dtype=torch.float32, device=parts.device)
+            check(lib.pg_multi_sum_f32(parts.numel(), ctypes.c_void_p(parts.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                       _stream(parts.device)), "pg_multi_sum_f32")
+            self._last_sqsum = out
         return loss
 
 
@@ -229,13 +241,16 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
     with torch.amp.autocast("cuda", enabled=use_amp):
         lp, _ = model(data=data)
         loss = nll_mean(lp.float(), y) * weight
-    l2 = l2_sqsum(params) if l2_lambda else None
+    # train.Adam takes the L2 gradient 2 * l2_lambda * p as extra weight decay inside its one launch (added to
+    # the unscaled gradient before the moments, exactly where the gradient sum would put it), and -- when it steps
+    # exactly these parameters -- the L2 value too, from the pre-update parameters it reads anyway; other
+    # optimizers get the gradient added to p.grad by one pg_multi_axpy_f32 launch
+    fold = bool(l2_lambda) and isinstance(optimizer, Adam)
+    fused_sq = fold and ({id(p) for g in optimizer.param_groups for p in g["params"]} == {id(p) for p in params}
+                         and len({p.device for p in params}) == 1)
+    l2 = l2_sqsum(params) if l2_lambda and not fused_sq else None
     scaled = scaler is not None and scaler.is_enabled()
     (scaler.scale(loss) if scaled else loss).backward()
-    # train.Adam takes the L2 gradient 2 * l2_lambda * p as extra weight decay inside its one launch (added to
-    # the unscaled gradient before the moments, exactly where the gradient sum would put it); other optimizers
-    # get it added to p.grad by one pg_multi_axpy_f32 launch
-    fold = bool(l2_lambda) and isinstance(optimizer, Adam)
     if l2_lambda and not fold:
         add_l2_grad(params, l2_lambda, scale=scaler._scale if scaled else None)  # device-side scale: no sync
     else:  # the reference's (0 *) l2 term gives every parameter a gradient, so it is stepped
@@ -244,6 +259,8 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
                 p.grad = torch.zeros_like(p)
     if fold:
         optimizer._l2_extra = 2.0 * l2_lambda
+        optimizer._want_sqsum = fused_sq
+        optimizer._last_sqsum = None
     try:
         if scaled:
             scaler.step(optimizer)
@@ -253,5 +270,10 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
     finally:
         if fold:
             optimizer._l2_extra = 0.0
+            optimizer._want_sqsum = False
+    if fused_sq:
+        l2 = optimizer._last_sqsum
+        if l2 is None:  # the step did not run the kernel (e.g. GradScaler skipped it on the host): measure it
+            l2 = l2_sqsum(params)
     total = loss.detach()
     return total + l2_lambda * l2 if l2 is not None else total

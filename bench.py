@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--fused-norm", action="store_true", help="compute edge weights inside the SpMM")
     ap.add_argument("--bf16", action="store_true", help="bf16 mode (config 5): bf16 features/activations, fp32 sums")
+    ap.add_argument("--entry", choices=("coo", "graph"), default="coo",
+                    help="coo (default): the model reads the reference trainer's COO wiring (Data.edge_index_* = "
+                    "mathcal_A_*.indices(), edge_weight_* = .values(), protgram_directgcn_trainer.py:362-367) through "
+                    "csr_from_coo; graph: a prebuilt Data.graph (build_propagation_csr)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-layers", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes that "
@@ -145,7 +149,18 @@ def main():
             raise SystemExit("--bf16 uses precomputed weights (no fused-norm bf16 kernel)")
         model.compute_dtype = torch.bfloat16
         x = x.to(torch.bfloat16)  # inputs resident in HBM in the compute dtype
-    data = pkg.Data(x=x, graph=g)
+    entry = "graph" if args.fused_norm else args.entry  # fused-norm reads the raw counts only the builder keeps
+    if entry == "coo":
+        # the trainer's wiring: coalesced COO indices()/values() of the three matrices; the model converts them once
+        # (csr_from_coo: CSR + n-gram tile plan + schedule, cached by tensor identity) in the first, untimed, call
+        data = pkg.synth.trainer_data(g, x)
+        del g
+        with torch.no_grad():
+            g = model.graph_of(data)
+        torch.cuda.synchronize()
+        log(f"[bench] entry coo: csr_from_coo -> plan {'attached' if g.ngram is not None else 'NOT attached'}")
+    else:
+        data = pkg.Data(x=x, graph=g)
 
     part = hp = None
     if world > 1 and args.partition == "halo":
@@ -199,7 +214,8 @@ def main():
         launch_graphs = [g]
     else:
         launch_graphs = [part.local]
-    ngram = all(gi.ngram is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm and Fd in (64, 128)
+    ngram = (all(gi.ngram is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm
+             and Fd in (64, 128, 256))
     if args.bf16:
         kname = "pg_spmm3_bf16"
     elif args.fused_norm:
@@ -249,6 +265,8 @@ def main():
                        "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
                        "layers": L, "layer_dims": dims, "classes": C,
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
+                       "entry": ("trainer COO (edge_index_*/edge_weight_* -> csr_from_coo)" if entry == "coo"
+                                 else "prebuilt Data.graph (build_propagation_csr)"),
                        "parallelism": ("single" if world == 1 else f"halo_recompute_x{world}" if hp is not None
                                        else f"node_range_x{world}"),
                        "exchange_chunks": args.chunks if part is not None else None,
@@ -297,7 +315,8 @@ def pmc_traffic(args, log, timeout=240):
     import pmc_traffic as pt
     out = tempfile.mkdtemp(prefix="pg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.join(REPO, "tools", "kprobe.py"), "--forward", "3", "--ngram", str(args.ngram),
-             "--feat", str(args.feat), "--layers", str(args.layers)] + (["--bf16"] if args.bf16 else []) \
+             "--feat", str(args.feat), "--layers", str(args.layers), "--entry", args.entry] \
+        + (["--bf16"] if args.bf16 else []) \
         + (["--fused-norm"] if args.fused_norm else [])
     env = dict(os.environ)
     env.setdefault("TMPDIR", "/tmp")

@@ -155,7 +155,7 @@ def apply_pe(p: dict, x, n_gram_len: int, one_gram_dim: int):
 def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew_u, original_indices=None,
                   n_gram_len: int = 0, one_gram_dim: int = 0, use_vector_coeffs: bool = True,
                   training: bool = False, dropout: float = 0.5, l2_eps: float = 1e-12, prop=propagate,
-                  act_masks=None):
+                  act_masks=None, pre_acts=None):
     """ProtGramDirectGCN.forward, protgram_directgcn.py:195-222 (eval: dropout inactive).
 
     ``act_masks`` (tests only): per layer, a boolean [N, F] mask choosing leaky_relu's branch instead of the sign of
@@ -163,7 +163,9 @@ def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew
     Comparing two fp32 computations of the same model, a pre-activation within rounding of 0 can fall on either
     side of the kink and change that element's gradient by 100x; passing the other computation's branches
     compares the two on the same piecewise-linear function. An extra last mask does the same for the decoder's
-    ReLU (where a hidden unit within rounding of 0 switches a whole term of that row's gradient on or off)."""
+    ReLU (where a hidden unit within rounding of 0 switches a whole term of that row's gradient on or off).
+    ``pre_acts`` (tests only): a list that receives this computation's own pre-activations (each layer's, then the
+    decoder's), so a test can check that the masks it passed disagree with their signs only within rounding of 0."""
     h = apply_pe(p, x, n_gram_len, one_gram_dim)
     for i in range(len(layer_dims) - 1):
         h_res = h
@@ -174,9 +176,13 @@ def model_forward(p: dict, layer_dims, x, ei_in, ew_in, ei_out, ew_out, ei_u, ew
         else:
             res = h_res
         z = out + res
+        if pre_acts is not None:
+            pre_acts.append(z.detach())
         h = F.leaky_relu(z) if act_masks is None else torch.where(act_masks[i], z, z * 0.01)
         h = F.dropout(h, p=dropout, training=training)
     z = linear(h, p["decoder_fc.0.weight"], p["decoder_fc.0.bias"])
+    if pre_acts is not None:
+        pre_acts.append(z.detach())
     nl = len(layer_dims) - 1
     z = F.relu(z) if act_masks is None or len(act_masks) <= nl else torch.where(act_masks[nl], z, z * 0)
     z = F.dropout(z, p=0.5, training=training)

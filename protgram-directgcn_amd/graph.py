@@ -123,27 +123,29 @@ class CSRGraph:
         n = self.n_rows
         nx = self.n_cols if self.n_cols is not None else n
         g = 20 * n if gated else 0
-        if self.ngram is not None and F in (64, 128) and elem == 4:  # the n-gram tile kernel reads its plan instead
+        if self.ngram is not None and F in (64, 128, 256) and elem == 4:  # the n-gram tile kernel reads its plan instead
             return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g
         if self.shared:
             return 8 * (n + 1) + 16 * self.nnz + nx * F * elem + 3 * n * F * elem + g
         return sum(8 * (n + 1) + 8 * a.nnz + nx * F * elem + n * F * elem for a in self.adj) + g
 
 
-_TAKE_CHUNK = 1 << 24  # indices per gather piece
+_TAKE_PIECE_BYTES = 1 << 28  # bytes of result per gather piece
 
 
 def take(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    """``t[idx]`` along dim 0. On the GPU, a result of 256 MiB or more is gathered in pieces of 2^24 indices:
-    ROCm torch's index gather (torch 2.10+rocm7.0 on MI355X) silently leaves the last 1 GiB of a result of
-    1 GiB or more unwritten -- measured with tools/halo_device_probe.py (profiles/r02_halo_device_probe.txt):
-    ``edges3[src]`` with 114.8M indices into the 5-gram [131M, 4] int32 records returned its last 2^26 rows
-    as zeros, index_select likewise, 2^24-index pieces exact. That was the round-1 device halo_partition
-    fault: the unwritten rows held stale ids, and the next gather by them read out of bounds."""
+    """``t[idx]`` along dim 0. On the GPU, a result of 256 MiB or more is gathered in pieces of at most 256 MiB of
+    result (max(1, 2^28 // row bytes) indices each, whatever the row width): ROCm torch's index gather (torch
+    2.10+rocm7.0 on MI355X) was seen to leave the tail of results of 1 GiB or more unwritten (round 2: ``edges3[src]``
+    with 114.8M indices into the 5-gram [131M, 4] int32 records returned its last 2^26 rows as zeros, which was the
+    round-1 device halo_partition fault). tools/gather_probe.py re-measures the raw gather
+    (profiles/r03_gather_probe.txt) and tests/test_gpu_parity.py::test_take_large_wide_rows pins take() itself
+    against a host gather at > 1 GiB with 512-B rows."""
     row = t.element_size() * (t[0].numel() if t.dim() > 1 and t.size(0) else 1)
-    if not t.is_cuda or idx.numel() * row < (1 << 28):
+    if not t.is_cuda or idx.numel() * row < _TAKE_PIECE_BYTES:
         return t[idx]
-    return torch.cat([t[idx[k:k + _TAKE_CHUNK]] for k in range(0, idx.numel(), _TAKE_CHUNK)])
+    step = max(1, _TAKE_PIECE_BYTES // max(row, 1))
+    return torch.cat([t[idx[k:k + step]] for k in range(0, idx.numel(), step)])
 
 
 def _bits(w: torch.Tensor) -> torch.Tensor:
@@ -197,9 +199,18 @@ def _key(*ts, n):
     return tuple(k)
 
 
-def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, cache: bool = True) -> CSRGraph:
-    """Convert the reference's three COO adjacencies to the device CSR (cached by tensor identity)."""
-    key = _key(ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, n=num_rows)
+def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, cache: bool = True,
+                 ngram_alphabet: Optional[int] = 20) -> CSRGraph:
+    """Convert the reference's three COO adjacencies to the device CSR (cached by tensor identity).
+
+    This is the path the reference trainer's unchanged wiring takes (``Data.edge_index_* = mathcal_A_*.indices()``,
+    ``edge_weight_* = .values()``, ``protgram_directgcn_trainer.py:362-367``, read by ``protgram_directgcn.py:196-203``).
+    When the three matrices share one pattern and the graph holds all ngram_alphabet^n n-grams in base-K id order (the
+    builder's sorted-string ids when every n-gram occurs), the n-gram tile plan (build_ngram_plan) and the middle-major
+    locality schedule (ngram_schedule) are attached, so this path runs the same kernels as a graph built by
+    build_propagation_csr. The plan kernel rejects (and the graph keeps the CSR kernels for) any pattern with an entry
+    that is neither a transition, a reverse transition nor the diagonal. ngram_alphabet=None: no plan."""
+    key = _key(ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, n=num_rows) + (ngram_alphabet,)
     if cache:
         hit = _CACHE.get(key)
         if hit is not None:
@@ -240,6 +251,10 @@ def csr_from_coo(num_rows: int, ei_in, ew_in, ei_out, ew_out, ei_und, ew_und, ca
             rowptr_t, edges3_t = rowptr, edges3
         g = CSRGraph(n_rows=n, shared=True, rowptr=rowptr, edges3=edges3, rowptr_t=rowptr_t, edges3_t=edges3_t,
                      symmetric=sym, nnz=nnz)
+        if ngram_alphabet and rowptr.is_cuda:
+            g.ngram = build_ngram_plan(g, ngram_alphabet)
+            if g.ngram is not None:
+                g.row_order = ngram_schedule(g.ngram.K, g.ngram.n, rowptr.device)
     else:
         g = CSRGraph(n_rows=n, shared=False,
                      adj=[_single(ei_in, ew_in, n), _single(ei_out, ew_out, n), _single(ei_und, ew_und, n)])
@@ -282,6 +297,18 @@ def locality_schedule(n: int, src: torch.Tensor, dst: torch.Tensor) -> torch.Ten
     min_in = big.clone().scatter_reduce_(0, dst, src, reduce="amin") if src.numel() else big.clone()
     key = min_out * (n + 1) + min_in
     return torch.sort(key, stable=True).indices.to(torch.int32)
+
+
+def ngram_schedule(K: int, n: int, device="cpu") -> torch.Tensor:
+    """The locality schedule of a graph over all K^n n-grams in base-K id order, in closed form: rows sorted by
+    (middle s_2..s_{n-1}, last letter, first letter). For a complete transition graph this is exactly the order
+    locality_schedule computes from the transitions (min out-neighbour M.b.0, then min in-neighbour 0.a.M); it is
+    used where only the symmetric propagation pattern is at hand (csr_from_coo). A schedule, never a result change."""
+    Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
+    mid = torch.arange(Kn2, dtype=torch.int64, device=device).view(-1, 1, 1)
+    b = torch.arange(K, dtype=torch.int64, device=device).view(1, -1, 1)
+    a = torch.arange(K, dtype=torch.int64, device=device).view(1, 1, -1)
+    return (a * Kn1 + mid * K + b).reshape(-1).to(torch.int32)
 
 
 def ngram_raw_csr(num_nodes: int, src, dst, cnt, device="cpu", schedule: bool = True) -> RawNgramCSR:

@@ -12,6 +12,7 @@ kernel's epilogue. Decoder, log_softmax and the L2 normalisation are small [N, F
 """
 from __future__ import annotations
 
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -26,10 +27,11 @@ _ROWS_OK: dict = {}
 
 def _check_rows(rows: torch.Tensor, limit: int):
     """Range check of original_indices (the dense kernel gathers gates/constant rows by them), cached per
-    tensor: the entry holds the tensor itself, so a new tensor at a reused address never hits it."""
+    tensor: the entry holds a weak reference to the tensor, so a new tensor at a reused address never hits it and
+    the cache keeps no index tensor alive."""
     k = _key(rows, n=limit)
     hit = _ROWS_OK.get(k)
-    if hit is not None and hit is rows:
+    if hit is not None and hit() is rows:
         return
     if rows.numel():
         lo, hi = int(rows.min()), int(rows.max())
@@ -37,7 +39,7 @@ def _check_rows(rows: torch.Tensor, limit: int):
             raise IndexError(f"original_indices in [{lo}, {hi}] outside [0, {limit})")
     if len(_ROWS_OK) > 64:
         _ROWS_OK.clear()
-    _ROWS_OK[k] = rows
+    _ROWS_OK[k] = weakref.ref(rows)
 
 
 class DirectGCNLayer(nn.Module):

@@ -96,7 +96,14 @@ def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128), dtype=tor
 def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
           flags: Optional[int] = None) -> torch.Tensor:
     """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels. bf16 x -> bf16 Z
-    (pg_spmm3_bf16: fp32 sums, one rounding)."""
+    (pg_spmm3_bf16: fp32 sums, one rounding).
+
+    Numerics: on a graph with an n-gram tile plan (g.ngram: every K^n n-gram present, attached by
+    build_propagation_csr and csr_from_coo) the default is the tile kernel, which sums the same w*x terms in another
+    order with FMAs: within |d| <= 1e-5 + 1e-5|ref| of the reference's propagate(), not bit-exact, and it applies
+    0 * x for missing transitions, so x must be finite (an inf in a grid-adjacent row becomes NaN). Pass
+    flags=default_flags() | PG_FLAG_NO_NGRAM for the CSR kernels: bit-exact to the reference and tolerant of
+    non-finite inputs. Graphs without a plan (any other node set) always run the CSR kernels."""
     lib = load_library()
     if _is_bf16(x):
         return _spmm3_bf16(lib, g, x, out, fused, flags)
@@ -194,7 +201,10 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
 
 
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
-    """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX."""
+    """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX.
+    Same numerics note as spmm3: the n-gram tile kernel (symmetric graphs with a plan) needs finite G and matches the
+    CSR kernel within fp32 rounding; PG_FLAG_NO_NGRAM selects the CSR kernel (under AMP, GradScaler's scaled
+    gradients can overflow to inf: the step is skipped either way, but the skipped values differ)."""
     lib = load_library()
     if _is_bf16(G):
         G = _bf16c(G)

@@ -402,8 +402,8 @@ def halo_partition(g: CSRGraph, rank: int, world: int, layers: int,
         owner = halo_owner(g, world)
     # The index work (halo sets, relabelling, the permuted CSR) runs on the host and the result moves to the
     # device once: it is setup, and the host path is the one the CPU tests exercise. (A device version of the same
-    # steps returned wrong records at 5-gram: ROCm torch's index gather drops the last 1 GiB of results >= 1 GiB,
-    # see graph.take; with take() it matches this host construction -- tools/halo_device_probe.py.)
+    # steps returned wrong records at 5-gram in round 1: ROCm torch's index gather was seen to drop the tail of
+    # results >= 1 GiB, see graph.take, tools/gather_probe.py and profiles/r03_gather_probe.txt.)
     owner = owner.to(device="cpu", dtype=torch.int64)
     if owner.numel() != n or (n and (int(owner.min()) < 0 or int(owner.max()) >= world)):
         raise ValueError("owner must assign every node a rank in [0, world)")

@@ -76,3 +76,32 @@ def fasta_edges(n: int, sequences: list[str]):
     dst = np.array([k[1] for k in keys], dtype=np.int64)
     cnt = np.array([pairs[k] for k in keys], dtype=np.float32)
     return len(ordered), src, dst, cnt, ordered
+
+
+def trainer_coo(g):
+    """The three propagation matrices of a shared-pattern CSRGraph in the form the reference trainer hands them to
+    the model: ``edge_index_* = mathcal_A_*.indices()`` and ``edge_weight_* = mathcal_A_*.values()`` of a coalesced
+    torch sparse COO (``protgram_directgcn_trainer.py:362-367``; coalesced by ``graph_utils.py:154, 193-195, 269``),
+    i.e. entries sorted by (row, col) with PyG's flow ``out[ei[1]] += w * x[ei[0]]``: ei[0] = source, ei[1] =
+    destination. Returns (ei_in, w_in, ei_out, w_out, ei_und, w_und) on g's device; the three index tensors are
+    distinct tensors with equal values, as the trainer's are. Test and bench input construction only."""
+    import torch
+    from .graph import take
+    if not g.shared:
+        raise ValueError("trainer_coo needs a shared-pattern graph")
+    dev = g.rowptr.device
+    dst = torch.repeat_interleave(torch.arange(g.n_rows, device=dev), g.rowptr[1:] - g.rowptr[:-1])
+    src = g.edges3[:, 0].to(torch.int64)
+    order = torch.sort(src * g.n_rows + dst).indices  # coalesced: by (row = source, col = destination)
+    ei = torch.stack([take(src, order), take(dst, order)])
+    w = [take(g.edges3[:, 1 + k].contiguous(), order).view(torch.float32) for k in range(3)]
+    return ei, w[0], ei.clone(), w[1], ei.clone(), w[2]
+
+
+def trainer_data(g, x):
+    """A Data object wired like the reference trainer's (``protgram_directgcn_trainer.py:343-344, 362-367``): x plus
+    the COO tensors of trainer_coo(g) under the attribute names the model reads (``protgram_directgcn.py:196-203``)."""
+    from .data import Data
+    ei_in, w_in, ei_out, w_out, ei_und, w_und = trainer_coo(g)
+    return Data(x=x, edge_index_in=ei_in, edge_weight_in=w_in, edge_index_out=ei_out, edge_weight_out=w_out,
+                edge_index_undirected_norm=ei_und, edge_weight_undirected_norm=w_und)

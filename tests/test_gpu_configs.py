@@ -78,6 +78,21 @@ def _grad_close_or_as_exact(got, ref32, ref64, what):
         f"{float(got.flatten()[i]):.6e} fp32 oracle {float(ref32.flatten()[i]):.6e} f64 {float(ref64.flatten()[i]):.6e}")
 
 
+def _count_tile_launches(monkeypatch):
+    """Count the calls of the n-gram tile kernels' entry points (a dict, filled as they run)."""
+    from collections import Counter
+    from protgram_directgcn_amd import ops
+    lib, calls = ops.load_library(), Counter()
+    for name in ("pg_spmm3_ngram_f32", "pg_spmm3t_ngram_f32", "pg_spmm3t_ngram_bf16"):
+        fn = getattr(lib, name)
+
+        def wrap(*a, _fn=fn, _name=name):
+            calls[_name] += 1
+            return _fn(*a)
+        monkeypatch.setattr(lib, name, wrap)
+    return calls
+
+
 def _labels(N, n):
     return torch.arange(N) // 20 ** (n - 1)  # the first letter (SURVEY §8d config 3)
 
@@ -86,7 +101,7 @@ def _labels(N, n):
 # config 3
 # ---------------------------------------------------------------------------------------------------------------
 @pytest.mark.timeout(1200)
-def test_config3_4gram_training_step_vs_oracle(pkg, cuda):
+def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     from protgram_directgcn_amd import train
     n, F, dims = 4, 128, [128, 128, 128]
     N, s, d, c = pkg.synth.de_bruijn_edges(n)
@@ -116,11 +131,35 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda):
         lp_m, emb_m = m(pkg.Data(x=xd, graph=g))
     assert_close(lp_m, lp.detach(), "model forward vs the written-out forward")
 
+    # the reference trainer's own wiring (protgram_directgcn_trainer.py:362-367): coalesced COO indices()/values() of
+    # the three matrices, converted by csr_from_coo -- it must reach the same n-gram tile kernels (plan + schedule
+    # attached) and give the prebuilt-graph path's bits
+    data_coo = pkg.synth.trainer_data(g, x.to(cuda))
+    gc = m.graph_of(data_coo)
+    assert gc.ngram is not None and gc.symmetric and gc.row_order is not None
+    assert torch.equal(gc.edges3, g.edges3) and torch.equal(gc.ngram.plan, g.ngram.plan)
+    assert torch.equal(gc.row_order, g.row_order)  # closed-form schedule == locality_schedule on a complete graph
+    calls = _count_tile_launches(monkeypatch)
+    with torch.no_grad():
+        lp_c, emb_c = m(data_coo)
+    assert calls["pg_spmm3_ngram_f32"] == len(m.convs), calls
+    assert torch.equal(lp_c, lp_m) and torch.equal(emb_c, emb_m)
+
     ei, w = _csr_coo(g)
     p = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
     xr = x.clone().requires_grad_(True)
+    pre = []
     lp_r, emb_r = oc.model_forward(p, dims, xr, ei, w[0], ei, w[1], ei, w[2], n_gram_len=n, prop=oc.propagate_chunked,
-                                   act_masks=masks)
+                                   act_masks=masks, pre_acts=pre)
+    # the GPU's branch choices handed to the oracle may disagree with the oracle's own signs only where its
+    # pre-activation is within the fp32 output tolerance of the kink (|z| <= 1e-5 + 1e-5|z|, i.e. rounding), and
+    # only on a handful of elements
+    for i, (mk, z) in enumerate(zip(masks, pre)):
+        flip = mk != (z > 0)
+        nflip = int(flip.sum())
+        assert nflip <= 1e-5 * z.numel() + 8, (i, nflip, z.numel())
+        if nflip:
+            assert float(z[flip].abs().max()) <= 2e-5, (i, nflip, float(z[flip].abs().max()))
     loss_r = Fn.nll_loss(lp_r, y) + LAM * sum(v.norm(2).pow(2) for v in p.values())
     loss_r.backward()
 
@@ -151,7 +190,9 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda):
     g_gpu = {k: prm.grad.detach().cpu() for k, prm in m.named_parameters()}
     m.zero_grad(set_to_none=True)
     opt = train.Adam(m.parameters(), lr=LR)
-    loss_s = train.train_step(m, pkg.Data(x=x.to(cuda), graph=g), yd, opt, l2_lambda=LAM, scaler=None)
+    calls.clear()
+    loss_s = train.train_step(m, data_coo, yd, opt, l2_lambda=LAM, scaler=None)  # through the trainer's COO wiring
+    assert calls["pg_spmm3_ngram_f32"] == len(m.convs) and calls["pg_spmm3t_ngram_f32"] == len(m.convs) - 1, calls
     assert abs(float(loss_s) - loss_r) <= 1e-5 * abs(loss_r)
     for k, prm in m.named_parameters():
         gref = p[k].grad

@@ -57,10 +57,15 @@ def test_spmm3_bitexact(pkg, cuda, name, F):
     ref = [oc.propagate(ei[k], x, ew[k]) for k in ("in", "out", "und")]
     dei, dew = dev_graph(ei, ew, cuda)
     g = pkg.graph.csr_from_coo(N, dei["in"], dew["in"], dei["out"], dew["out"], dei["und"], dew["und"])
-    for fl in FLAG_VARIANTS:
-        Z = ops.spmm3(g, x.to(cuda), flags=fl).cpu()
+    for fl in FLAG_VARIANTS:  # the CSR kernels (PG_FLAG_NO_NGRAM): bit-exact to the reference's propagate()
+        Z = ops.spmm3(g, x.to(cuda), flags=fl | _lib_csr()).cpu()
         for k in range(3):
             assert torch.equal(Z[:, k * F:(k + 1) * F], ref[k]), (name, F, fl, k)
+    if g.ngram is not None:  # a complete 20^n graph through the COO boundary: the tile kernel by default
+        assert name == "f1_debruijn2"
+        Z = ops.spmm3(g, x.to(cuda)).cpu()
+        for k in range(3):
+            assert_close(Z[:, k * F:(k + 1) * F], ref[k], f"{name} tile kernel slice {k}")
 
 
 @pytest.mark.parametrize("name", ["f1_fasta2", "f1_debruijn2", "f2_edge", "f5_fasta3", "f6_pe1"])
@@ -1021,3 +1026,18 @@ def test_spmm3_gated_bitexact(pkg, cuda, name, F, vec):
     s = [cad * prm["C_in"], cad * prm["C_out"], prm["C_all"] * prm["C_undirected"]]
     ref = torch.cat([Z[:, k * F:(k + 1) * F] * s[k].view(-1, 1) for k in range(3)], 1)
     assert torch.equal(Zg, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_take_large_wide_rows(pkg, cuda):
+    """graph.take on a > 1 GiB result of 512-B rows (the halo inputs' take(x_full, perm) shape at 5-gram, F = 128)
+    equals the host gather bit for bit: pieces are sized by bytes, so no piece reaches the size at which ROCm
+    torch's index gather was seen to drop a result's tail (tools/gather_probe.py)."""
+    rows = (1 << 30) // 512 + 300_000  # 1.15 GiB of result
+    gen = torch.Generator().manual_seed(7)
+    t = torch.randn(rows, 128, generator=gen)
+    idx = torch.randperm(rows, generator=gen)
+    got = pkg.graph.take(t.to(cuda), idx.to(cuda))
+    assert got.shape == (rows, 128)
+    assert torch.equal(got.cpu(), t[idx])

@@ -27,6 +27,7 @@ ap.add_argument("--feat", type=int, default=128)
 ap.add_argument("--layers", type=int, default=2)
 ap.add_argument("--bf16", action="store_true")
 ap.add_argument("--fused-norm", action="store_true")
+ap.add_argument("--entry", choices=("coo", "graph"), default="coo")
 args = ap.parse_args()
 reps = args.reps
 dev = torch.device("cuda:0")
@@ -41,7 +42,11 @@ if args.forward:
     if args.bf16:
         model.compute_dtype = torch.bfloat16
         x = x.to(torch.bfloat16)
-    data = pkg.Data(x=x, graph=g)
+    if args.entry == "coo" and not args.fused_norm:  # bench.py's default: the trainer's COO wiring
+        data = pkg.synth.trainer_data(g, x)
+        del g
+    else:
+        data = pkg.Data(x=x, graph=g)
     with torch.no_grad():
         for _ in range(reps):
             model(data)

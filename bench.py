@@ -221,7 +221,8 @@ def main():
     elif args.fused_norm:
         kname = "pg_spmm3_fusednorm_f32"
     elif ngram:  # n-gram tile kernel; inference gates the aggregates at its store
-        kname = "pg_spmm3_ngram_f32" + (" (gated)" if gated else "")
+        mid = all(gi.ngram.mplan is not None for gi in launch_graphs) and Fd % 16 == 0
+        kname = ("pg_spmm3_ngram_mid_f32" if mid else "pg_spmm3_ngram_f32") + (" (gated)" if gated else "")
     else:
         kname = "pg_spmm3_gated_f32" if gated else "pg_spmm3_f32"
     comp = sum(gi.compulsory_bytes(Fd, elem=el, gated=gated) for gi in launch_graphs) // len(launch_graphs)

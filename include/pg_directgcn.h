@@ -78,6 +78,8 @@ typedef struct pg_edge1 {
                                             kernels apply (F_out = 128, K = 384 or 256, no row map: the default) */
 #define PG_FLAG_DENSE_X3 (1u << 16)       /* dense backward: the split-bf16 weight gradient (opt-in) */
 #define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */
+#define PG_FLAG_NGRAM_BLOCK4 (1u << 21)   /* host-side: the 4x4-block n-gram forward (pg_spmm3_ngram_f32) instead of the
+                                             middle-tile kernel (pg_spmm3_ngram_mid_f32) */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -210,6 +212,22 @@ int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const f
                         float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
                          uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+
+/* N-gram MIDDLE-tile propagation (pg_ngram_mid.hip; replaces, on graphs over all K^n n-grams, the six propagate
+ * calls of protgram_directgcn.py:101-112 like pg_spmm3_ngram_f32). A work item is one middle (n-2)-gram M and a
+ * 16-feature column chunk: the K^2 out-sources M.b.c and K^2 in-sources c.a.M of the middle's K x K rows are staged
+ * once in LDS (LDS-DMA, double-buffered, one persistent workgroup per CU), and a lane pair per row runs the 2K slot
+ * steps from LDS. K = 20; F a multiple of 16; 16-B aligned rows; PG_ERR_UNSUPPORTED otherwise. Numerics as
+ * pg_spmm3_ngram_f32 (fp32 FMA in slot order; X must be finite).
+ *   pg_ngram_mplan_floats: middle-plan size in floats for (K, n, n_rows = K^n), or -1 (K != 20, n < 2).
+ *   pg_ngram_mplan_f32: scatters the CSR's weights into the middle plan (zeroed first); *bad as pg_ngram_plan_f32.
+ *   pg_spmm3_ngram_mid_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the
+ *     store (as pg_spmm3_gated_f32). */
+int64_t pg_ngram_mplan_floats(int K, int n, int64_t n_rows);
+int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, float* plan,
+                       int64_t plan_floats, int* bad, void* stream);
+int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
+                           const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

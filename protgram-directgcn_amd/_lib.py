@@ -20,6 +20,7 @@ PG_FLAG_DENSE_PREGATED = 1 << 14
 PG_FLAG_DENSE_TILED = 1 << 15
 PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_NO_NGRAM = 1 << 20
+PG_FLAG_NGRAM_BLOCK4 = 1 << 21
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -70,6 +71,10 @@ SIGNATURES = {
     "pg_ngram_plan_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pg_spmm3_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,
                                           ctypes.POINTER(LayerArgs), c_vp, c_i64, c_u32, c_vp]),
+    "pg_ngram_mplan_floats": (c_i64, [ctypes.c_int, ctypes.c_int, c_i64]),
+    "pg_ngram_mplan_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "pg_spmm3_ngram_mid_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,
+                                              ctypes.POINTER(LayerArgs), c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                            ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,

@@ -54,7 +54,8 @@ class NgramPlan:
     (pg_ngram_plan_f32 / pg_spmm3_ngram_f32 / pg_spmm3t_ngram_f32): node id = base-K number of the n-gram."""
     K: int
     n: int
-    plan: torch.Tensor  # fp32 [pg_ngram_plan_floats(K, n, K^n)]
+    plan: torch.Tensor  # fp32 [pg_ngram_plan_floats(K, n, K^n)]: 4x4-block layout (transposed kernels, block-4 forward)
+    mplan: Optional[torch.Tensor] = None  # fp32 [pg_ngram_mplan_floats(K, n, K^n)]: middle layout (middle-tile forward)
 
 
 @dataclass
@@ -95,12 +96,14 @@ class CSRGraph:
             g.rowptr_t, g.edges3_t = mv(self.rowptr_t), mv(self.edges3_t)
         g.adj = [ShapedAdjacency(mv(a.rowptr), mv(a.edges), mv(a.rowptr_t), mv(a.edges_t), a.nnz) for a in self.adj]
         if self.ngram is not None:
-            g.ngram = NgramPlan(self.ngram.K, self.ngram.n, self.ngram.plan.to(device))
+            g.ngram = NgramPlan(self.ngram.K, self.ngram.n, self.ngram.plan.to(device),
+                                None if self.ngram.mplan is None else self.ngram.mplan.to(device))
         return g
 
     def tensors(self):
         ts = [self.rowptr, self.edges3, self.rowptr_t, self.edges3_t, self.row_order,
-              self.ngram.plan if self.ngram is not None else None]
+              self.ngram.plan if self.ngram is not None else None,
+              self.ngram.mplan if self.ngram is not None else None]
         for a in self.adj:
             ts += [a.rowptr, a.edges, a.rowptr_t, a.edges_t]
         return [t for t in ts if t is not None]
@@ -123,6 +126,8 @@ class CSRGraph:
         n = self.n_rows
         nx = self.n_cols if self.n_cols is not None else n
         g = 20 * n if gated else 0
+        if self.ngram is not None and self.ngram.mplan is not None and F % 16 == 0 and elem == 4:
+            return 4 * self.ngram.mplan.numel() + nx * F * elem + 3 * n * F * elem + g  # middle-tile kernel: its plan
         if self.ngram is not None and F in (64, 128, 256) and elem == 4:  # the n-gram tile kernel reads its plan instead
             return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g
         if self.shared:
@@ -378,12 +383,18 @@ def build_ngram_plan(g: CSRGraph, K: int = 20) -> Optional[NgramPlan]:
     if floats < 0:
         return None
     plan = torch.empty(floats, dtype=torch.float32, device=g.rowptr.device)
-    bad = torch.zeros(1, dtype=torch.int32, device=g.rowptr.device)
+    bad = torch.zeros(2, dtype=torch.int32, device=g.rowptr.device)
     ops.check(lib.pg_ngram_plan_f32(K, n, g.n_rows, ops._p(g.rowptr), ops._p(g.edges3), ops._p(plan), floats,
                                     ops._p(bad), ops._stream(plan)), "pg_ngram_plan_f32")
-    if int(bad.item()) != 0:
+    mplan = None
+    mfloats = int(lib.pg_ngram_mplan_floats(K, n, g.n_rows))
+    if mfloats > 0:
+        mplan = torch.empty(mfloats, dtype=torch.float32, device=g.rowptr.device)
+        ops.check(lib.pg_ngram_mplan_f32(K, n, g.n_rows, ops._p(g.rowptr), ops._p(g.edges3), ops._p(mplan), mfloats,
+                                         ops._p(bad[1:]), ops._stream(mplan)), "pg_ngram_mplan_f32")
+    if int(bad[0].item()) != 0 or (mplan is not None and int(bad[1].item()) != 0):
         return None
-    return NgramPlan(K, n, plan)
+    return NgramPlan(K, n, plan, mplan)
 
 
 def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,

@@ -15,7 +15,7 @@ from typing import Optional
 import torch
 
 from . import _lib
-from ._lib import PG_FLAG_NO_NGRAM, LayerArgs, check, default_flags, load_library
+from ._lib import PG_FLAG_NGRAM_BLOCK4, PG_FLAG_NO_NGRAM, LayerArgs, check, default_flags, load_library
 from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
@@ -93,6 +93,26 @@ def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128), dtype=tor
             and x.size(0) == g.n_rows and x.size(1) in widths)
 
 
+def _mid_ok(g: CSRGraph, x: torch.Tensor, fl: int) -> bool:
+    """The middle-tile forward (pg_spmm3_ngram_mid_f32) takes this call: fp32 x with the graph's rows, F a multiple
+    of 16, a middle plan, and neither PG_FLAG_NO_NGRAM nor PG_FLAG_NGRAM_BLOCK4."""
+    return (g.ngram is not None and g.ngram.mplan is not None and not (fl & (PG_FLAG_NO_NGRAM | PG_FLAG_NGRAM_BLOCK4))
+            and x.dtype == torch.float32 and x.size(0) == g.n_rows and x.size(1) % 16 == 0)
+
+
+def _ngram_fwd(lib, g, x, a, Z, fl, s):
+    """Launch the n-gram forward (middle-tile kernel by default, 4x4-block kernel under PG_FLAG_NGRAM_BLOCK4 or where
+    the middle kernel does not take the shape); returns the library's return code."""
+    ng, N, F = g.ngram, g.n_rows, x.size(1)
+    if _mid_ok(g, x, fl):
+        rc = lib.pg_spmm3_ngram_mid_f32(ng.K, ng.n, N, _p(ng.mplan), _p(x), x.stride(0), F, a, _p(Z), Z.stride(0), fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            return rc
+    if _ngram_ok(g, x, fl, (64, 128, 256)):
+        return lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, a, _p(Z), Z.stride(0), fl, s)
+    return _lib.PG_ERR_UNSUPPORTED
+
+
 def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
           flags: Optional[int] = None) -> torch.Tensor:
     """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels. bf16 x -> bf16 Z
@@ -117,11 +137,10 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     fl = default_flags() if flags is None else flags
     s = _stream(x)
     ev = _ev_start(x)
-    if g.shared and not fused and _ngram_ok(g, x, fl, (64, 128, 256)):
-        ng = g.ngram
-        rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, None, _p(Z), Z.stride(0), fl, s)
-        if rc != _lib.PG_ERR_UNSUPPORTED:  # unaligned operands: the CSR kernel below
-            check(rc, "pg_spmm3_ngram_f32")
+    if g.shared and not fused and g.ngram is not None:
+        rc = _ngram_fwd(lib, g, x, None, Z, fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:  # unaligned operands / other widths: the CSR kernel below
+            check(rc, "pg_spmm3_ngram_(mid_)f32")
             _ev_end(x, ev)
             return Z
     if g.shared:
@@ -173,6 +192,9 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     then gate inside the dense kernel)."""
     if _is_bf16(x) or not g.shared or g.edges3 is None:
         return None
+    fl = default_flags() if flags is None else flags
+    if _mid_ok(g, x, fl):  # the middle-tile kernel has no gated store: the dense kernel applies the gates
+        return None
     lib = load_library()
     x = _f32c(x)
     _require_gpu(x)
@@ -182,14 +204,11 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
         raise ValueError("x has fewer rows than the graph")
     Z = out if out is not None else torch.empty(N, 3 * F, device=x.device, dtype=torch.float32)
     a, keep = _layer_args(None, prm, gate_mode, M=N)
-    fl = default_flags() if flags is None else flags
     ev = _ev_start(x)
-    if _ngram_ok(g, x, fl, (64, 128, 256)):
-        ng = g.ngram
-        rc = lib.pg_spmm3_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(x), x.stride(0), F, ctypes.byref(a), _p(Z),
-                                    Z.stride(0), fl, _stream(x))
+    if g.ngram is not None:
+        rc = _ngram_fwd(lib, g, x, ctypes.byref(a), Z, fl, _stream(x))
         if rc != _lib.PG_ERR_UNSUPPORTED:
-            check(rc, "pg_spmm3_ngram_f32")
+            check(rc, "pg_spmm3_ngram_(mid_)f32")
             _ev_end(x, ev)
             del keep
             return Z

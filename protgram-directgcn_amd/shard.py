@@ -163,10 +163,8 @@ def _dense_local(conv, part: NodeRangePartition, Z, res: nn.Module, res_x, a: in
 
 
 def _all_gather_chunk(send: torch.Tensor, dst: torch.Tensor, part: NodeRangePartition, group=None):
-    """send [cs, F] from every rank -> dst [world * cs, F] (rank-major). Async on RCCL (returns the work)."""
-    if dist.get_backend(group) == "gloo":  # rehearsal backend: synchronous list form
-        dist.all_gather(list(dst.view(part.world, send.size(0), -1).unbind(0)), send, group=group)
-        return None
+    """send [cs, F] from every rank -> dst [world * cs, F] (rank-major), asynchronous (returns the work). The same
+    tensor collective on RCCL and on gloo (the CPU rehearsal backend), so the tests run the product's calls."""
     return dist.all_gather_into_tensor(dst, send, group=group, async_op=True)
 
 
@@ -226,10 +224,7 @@ def all_gather_rows(h_local: torch.Tensor, part: NodeRangePartition, group=None,
         h_local = pad
     if out is None:
         out = h_local.new_empty(part.per * part.world, Fd)
-    if dist.get_backend(group) == "gloo":  # rehearsal backend (CPU tests, one-GPU dry runs)
-        dist.all_gather(list(out.view(part.world, part.per, Fd).unbind(0)), h_local.contiguous(), group=group)
-    else:
-        dist.all_gather_into_tensor(out, h_local.contiguous(), group=group)
+    dist.all_gather_into_tensor(out, h_local.contiguous(), group=group)  # RCCL / gloo alike
     return out[:part.n]
 
 
@@ -237,14 +232,14 @@ def reduce_scatter_rows(d_full: torch.Tensor, part: NodeRangePartition, group=No
     """[N, F] partial sums on every rank -> this rank's rows [n_local, F] of their sum over ranks
     (RCCL reduce-scatter; the backward of all_gather_rows)."""
     Fd = d_full.size(1)
-    buf = d_full.new_zeros(part.per * part.world, Fd)
+    # bf16 partials are summed in fp32 (one rounding of the total, as the single-GPU bf16 backward rounds once)
+    wide = d_full.dtype == torch.bfloat16
+    buf = d_full.new_zeros(part.per * part.world, Fd, dtype=torch.float32 if wide else d_full.dtype)
     buf[:part.n] = d_full
-    if dist.get_backend(group) == "gloo":  # gloo has no reduce_scatter
-        dist.all_reduce(buf, group=group)
-        return buf[part.rank * part.per:part.rank * part.per + part.n_local].clone()
-    out = d_full.new_empty(part.per, Fd)
-    dist.reduce_scatter_tensor(out, buf, group=group)
-    return out[:part.n_local]
+    out = buf.new_empty(part.per, Fd)
+    dist.reduce_scatter_tensor(out, buf, group=group)  # RCCL / gloo alike
+    out = out[:part.n_local]
+    return out.to(d_full.dtype) if wide else out
 
 
 class _GatherRows(torch.autograd.Function):
@@ -258,27 +253,45 @@ class _GatherRows(torch.autograd.Function):
         return reduce_scatter_rows(d_full.contiguous(), ctx.part, ctx.group), None, None
 
 
-def _layer_local_train(conv, part: NodeRangePartition, h_full, res: nn.Module, act=True):
+_GATE_NAMES = ("C_in_vec", "C_out_vec", "C_directed_vec", "C_undirected_vec", "C_all_vec")
+
+
+def _layer_local_train(conv, part: NodeRangePartition, h_full, res: nn.Module, act=True, own: Optional[dict] = None):
+    """One layer over this rank's rows with autograd. ``own`` (ShardedTrainer): the layer's per-node parameters as
+    owned-row leaves ([n_local, ...], sharing storage with the model's full parameters) -- the dense kernels then
+    read contiguous row slices (no row map) and the gradients come out [n_local, ...]; without it the full parameters
+    are read at the owned global rows (and their gradients are full-size)."""
     if part.local.rowptr_t is None:
         raise ValueError("training needs partition(..., transpose=True)")
     Z = ops.Propagate3.apply(h_full, part.local, False)
     vec = conv.use_vector_coeffs
-    rows = part.rows if vec else None
-    constant = conv.constant if vec else None
     res_x = h_full[part.r0:part.r1]
     W_res, b_res = (res.weight, res.bias) if isinstance(res, nn.Linear) else (None, None)
-    return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, 0 if vec else 1, act, ops.LEAKY_SLOPE,
-                                *conv._dense_params())
+    params = conv._dense_params()
+    if vec and own is not None:
+        params = params[:10] + tuple(own[k] for k in _GATE_NAMES)
+        rows, constant = None, own["constant"]
+    else:
+        rows = part.rows if vec else None
+        constant = conv.constant if vec else None
+    return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, 0 if vec else 1, act, ops.LEAKY_SLOPE, *params)
 
 
-def sharded_forward_train(model, part: NodeRangePartition, x_full: torch.Tensor, group=None):
+def sharded_forward_train(model, part: NodeRangePartition, x_full: torch.Tensor, group=None,
+                          own: Optional[List[dict]] = None):
     """ProtGramDirectGCN.forward on this rank's rows with autograd (dropout as in the model: training mode
-    only, per-rank RNG). Returns (log_probs, emb) for rows [r0, r1)."""
+    only, per-rank RNG). Honours ``model.compute_dtype``: in bf16 mode the features, aggregates, layer outputs and
+    the exchanged rows are bf16 (half the all-gather bytes), sums fp32, the head fp32. ``own``: per layer, the
+    owned-row parameter leaves of ShardedTrainer. Returns (log_probs, emb) for rows [r0, r1)."""
     h_full = model._apply_pe(x_full)
+    if model.compute_dtype == torch.bfloat16:
+        h_full = h_full.to(torch.bfloat16)
+    elif model.compute_dtype != torch.float32:
+        raise ValueError("compute_dtype must be torch.float32 or torch.bfloat16")
     L = len(model.convs)
     h_local = None
     for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
-        h_local = _layer_local_train(conv, part, h_full, res)
+        h_local = _layer_local_train(conv, part, h_full, res, own=None if own is None else own[i])
         h_local = F.dropout(h_local, p=model.dropout, training=model.training)
         if i + 1 < L:
             h_full = _GatherRows.apply(h_local, part, group) if part.world > 1 else h_local
@@ -325,6 +338,105 @@ def sharded_train_step(model, part: NodeRangePartition, x_full: torch.Tensor, y_
     if part.world > 1:
         dist.all_reduce(tot, group=group)
     return float(tot)
+
+
+class ShardedTrainer:
+    """The reference trainer's full-batch step (``protgram_directgcn_trainer.py:91-100``: zero_grad -> forward ->
+    ``nll_loss`` (mean over all N nodes) + ``l2_lambda * sum_p ||p||^2`` -> backward -> Adam step) on P ranks, with
+    train.train_step's device-side semantics and the per-node state sharded:
+
+    * per-node parameters (``C_*_vec``, ``constant``): this rank owns rows [r0, r1). It trains owned-row leaves
+      that share storage with the model's full parameters, so gradients, Adam moments and the update cover ONLY the
+      owned rows (1/P of the N x F ``constant`` state per rank; rows owned elsewhere are stale here and never read
+      -- ``gather_node_params`` makes them whole for a checkpoint);
+    * replicated parameters (weights, biases, residual projections, decoder): their gradients accumulate into views
+      of ONE flat buffer, summed over ranks by one all-reduce (no cat / copy-back);
+    * the optimizer is ``train.Adam`` (one launch per step) with the L2 gradient folded into its decay, after the
+      all-reduce (so it is added once, not P times); any other optimizer gets ``p.grad += 2 l2_lambda p``;
+    * the loss (nll over the owned rows / N plus the L2 value: replicated parameters once, owned rows summed over
+      ranks) comes back as a device scalar, all-reduced on the device: no host sync per step;
+    * ``model.compute_dtype = torch.bfloat16`` trains in bf16 mode (config 5): bf16 features, aggregates and
+      exchanged rows, fp32 sums, parameters and optimizer.
+
+    No GradScaler: the bf16 and fp32 modes need none (the reference's scaler serves its fp16 autocast)."""
+
+    def __init__(self, model, part: NodeRangePartition, lr: float = 1e-3, l2_lambda: float = 1e-7, group=None,
+                 optimizer_factory=None, **adam_kw):
+        from . import train
+        self.model, self.part, self.group, self.l2_lambda = model, part, group, float(l2_lambda)
+        self.own: List[dict] = []
+        node_leaves, dense = [], []
+        full_of = {}
+        for conv in model.convs:
+            d = {}
+            for name, p in conv.named_parameters(recurse=False):
+                if _is_node_param(name, p, part.n):
+                    leaf = nn.Parameter(p.data[part.r0:part.r1], requires_grad=p.requires_grad)
+                    d[name] = leaf
+                    full_of[id(p)] = leaf
+                    node_leaves.append(leaf)
+            self.own.append(d)
+        for name, p in model.named_parameters():
+            if id(p) not in full_of and p.requires_grad:
+                dense.append(p)
+        self.dense = dense
+        self.node = node_leaves
+        dev = dense[0].device if dense else part.local.rowptr.device
+        self.flat = torch.zeros(sum(p.numel() for p in dense), dtype=torch.float32, device=dev)
+        self.params = dense + [p for p in node_leaves if p.requires_grad]
+        if optimizer_factory is None:
+            self.opt = train.Adam(self.params, lr=lr, **adam_kw)
+        else:
+            self.opt = optimizer_factory(self.params)
+        self._train = train
+
+    def _grads_into_flat(self):
+        off = 0
+        for p in self.dense:
+            k = p.numel()
+            p.grad = self.flat[off:off + k].view_as(p)
+            off += k
+
+    def step(self, x_full: torch.Tensor, y_local: torch.Tensor) -> torch.Tensor:
+        """One step; returns the global loss as a device scalar (call .item() only when the value is needed)."""
+        part, lam, train = self.part, self.l2_lambda, self._train
+        for p in self.node:
+            p.grad = None
+        self.flat.zero_()
+        self._grads_into_flat()  # autograd accumulates into the flat buffer's views in place
+        lp, _ = sharded_forward_train(self.model, part, x_full, self.group, own=self.own)
+        nll = -lp.float().gather(1, y_local.view(-1, 1)).sum() / part.n
+        nll.backward()
+        for p in self.node:  # parameters with no gradient path still get the L2 gradient and are stepped
+            if p.requires_grad and p.grad is None:
+                p.grad = torch.zeros_like(p)
+        if lam:
+            l2_rep = train.l2_sqsum(self.dense) if self.dense else nll.new_zeros(())
+            l2_own = train.l2_sqsum(self.node) if self.node else nll.new_zeros(())
+        else:
+            l2_rep = l2_own = nll.new_zeros(())
+        parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
+        if part.world > 1:
+            if self.flat.numel():
+                dist.all_reduce(self.flat, group=self.group)  # sum of the ranks' partial gradients
+            dist.all_reduce(parts, group=self.group)
+        fold = bool(lam) and isinstance(self.opt, train.Adam)
+        if lam and not fold:
+            ps = [p for p in self.params if p.grad is not None]
+            torch._foreach_add_([p.grad for p in ps], [p.detach() for p in ps], alpha=2.0 * lam)
+        if fold:
+            self.opt._l2_extra = 2.0 * lam
+        try:
+            self.opt.step()
+        finally:
+            if fold:
+                self.opt._l2_extra = 0.0
+        return parts.sum() + lam * l2_rep
+
+    @torch.no_grad()
+    def gather(self):
+        """All ranks' per-node parameters whole again (checkpointing): see gather_node_params."""
+        gather_node_params(self.model, self.part, self.group)
 
 
 @torch.no_grad()

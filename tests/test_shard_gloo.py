@@ -227,11 +227,126 @@ def _train_worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def _run(target, world):
+def _any_dtype(fn, out_keys=None):
+    """A CPU stand-in run in fp32 on bf16 inputs, its outputs rounded back to bf16 (the kernels' bf16 storage)."""
+    def wrapped(*args, **kw):
+        dt = next((a.dtype for a in args if torch.is_tensor(a) and a.is_floating_point()), torch.float32)
+        args = [a.float() if torch.is_tensor(a) and a.dtype == torch.bfloat16 else a for a in args]
+        kw = {k: (v.float() if torch.is_tensor(v) and v.dtype == torch.bfloat16 else v) for k, v in kw.items()}
+        r = fn(*args, **kw)
+        if dt != torch.bfloat16:
+            return r
+        if isinstance(r, dict):
+            return {k: (v.to(dt) if k in out_keys and v is not None else v) for k, v in r.items()}
+        return r.to(dt)
+    return wrapped
+
+
+def _trainer_worker(rank, world, port, out_q, bf16):
+    """shard.ShardedTrainer (owned-row per-node state, flat-buffer all-reduce, device-side loss) for two steps, fp32
+    or bf16 mode, against the single-process oracle's autograd + Adam (fp32): fp32 within the gradient tolerance,
+    bf16 within bf16 rounding (loss within 2 %, gradient cosine > 0.99)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard, train
+    from oracle import directgcn_cpu as oc
+    from oracle import graph_cpu as og
+    import torch.nn.functional as F
+    ops.spmm3 = _any_dtype(_cpu_spmm3)
+    ops.spmm3_t = _any_dtype(_cpu_spmm3_t)
+    ops.layer_dense = _any_dtype(_cpu_layer_dense)
+    ops.layer_dense_backward = _any_dtype(_cpu_layer_dense_backward, out_keys=("dpre", "dZ", "dres"))
+    train.l2_sqsum = lambda ps: sum((p.detach().float() ** 2).sum() for p in ps)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, s, d, c = pkg.synth.de_bruijn_edges(2)
+        m = og.build_matrices(N, s, d, c)
+        g = pkg.graph.csr_from_coo(N, *m["in"], *m["out"], *m["und"], cache=False)
+        dims = [16, 16, 16, 12]
+        torch.manual_seed(0)
+        model = pkg.ProtGramDirectGCN(dims, N, 5, 2, 0, 512, 0.5, True).eval()
+        with torch.no_grad():
+            gen = torch.Generator().manual_seed(5)
+            for name, p in model.named_parameters():
+                leaf = name.split(".")[-1]
+                if leaf.startswith("C_"):
+                    p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+                elif "bias" in leaf:
+                    p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+        if bf16:
+            model.compute_dtype = torch.bfloat16
+        ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+        x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
+        y = (torch.arange(N) // 20) % 5
+        lam, steps, lr = 1e-3, 2, 1e-2
+        part = shard.partition(g, rank, world, transpose=True)
+        tr = shard.ShardedTrainer(model, part, l2_lambda=lam,
+                                  optimizer_factory=lambda ps: torch.optim.Adam(ps, lr=lr))
+        # the node state is owned-row sized
+        owned = [p for d in tr.own for p in d.values()]
+        assert owned and all(p.size(0) == part.n_local for p in owned)
+        losses, grads = [], []
+        for _ in range(steps):
+            loss = tr.step(x, y[part.r0:part.r1])
+            assert torch.is_tensor(loss) and loss.dim() == 0
+            losses.append(float(loss))
+            gd = {}
+            for name, p in model.named_parameters():
+                if shard._is_node_param(name, p, N):
+                    conv = model.convs[int(name.split(".")[1])]
+                    gd[name] = tr.own[list(model.convs).index(conv)][name.split(".")[-1]].grad.clone()
+                else:
+                    gd[name] = p.grad.clone()
+            grads.append(gd)
+        ropt = torch.optim.Adam(list(ref.values()), lr=lr)
+        rlosses, rgrads = [], []
+        for _ in range(steps):
+            ropt.zero_grad()
+            lp, _ = oc.model_forward(ref, dims, x, *m["in"], *m["out"], *m["und"], n_gram_len=2)
+            loss = F.nll_loss(lp, y) + lam * sum(v.norm(2).pow(2) for v in ref.values())
+            loss.backward()
+            rgrads.append({k: v.grad.clone() for k, v in ref.items()})
+            ropt.step()
+            rlosses.append(float(loss))
+        bad = []
+        for st in range(steps):
+            if bf16:
+                if abs(losses[st] - rlosses[st]) > 2e-2 * abs(rlosses[st]):
+                    bad.append(("loss", st, losses[st], rlosses[st]))
+            elif abs(losses[st] - rlosses[st]) > 1e-5 * abs(rlosses[st]) + 1e-6:
+                bad.append(("loss", st, losses[st], rlosses[st]))
+            if st:  # the second step's gradients depend on the first update: compare step 0 only
+                continue
+            for name, gg in grads[st].items():
+                r = rgrads[st][name]
+                if shard._is_node_param(name, r, N):
+                    r = r[part.r0:part.r1]
+                if bf16:
+                    cos = float((gg * r).sum() / (gg.norm() * r.norm() + 1e-30))
+                    if cos < 0.99:
+                        bad.append((name, "cos", cos))
+                else:
+                    err = float((gg - r).abs().max())
+                    if err > 2e-5 * float(r.abs().max()) + 1e-6:
+                        bad.append((name, "grad", err))
+        tr.gather()
+        if not bf16:
+            for name, p in model.named_parameters():
+                err = float((p.detach() - ref[name].detach()).abs().max())
+                if err > 2e-5:
+                    bad.append(("gathered " + name, err))
+        out_q.put((rank, part.r0, part.r1, not bad, str(bad[:4])))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(target, world, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *extra)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
@@ -266,3 +381,11 @@ def test_node_range_partition_gloo(world):
         assert a[2] == b[1]
     for r in res:
         assert r[3], f"rank {r[0]} mismatch (max |d| {r[4]:.2e})"
+
+
+@pytest.mark.parametrize("world,bf16", [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_trainer_gloo(world, bf16):
+    """Config 5's multi-GPU training path (ShardedTrainer: owned-row per-node state, fp32 / bf16) on gloo ranks."""
+    res = _run(_trainer_worker, world, bf16)
+    for r in res:
+        assert r[3], f"rank {r[0]}: {r[4]}"

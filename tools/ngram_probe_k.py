@@ -13,7 +13,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
-from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM  # noqa: E402
+from protgram_directgcn_amd._lib import PG_FLAG_NGRAM_BLOCK4, PG_FLAG_NO_NGRAM  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 128
@@ -43,19 +43,29 @@ prm = {k: torch.rand(N, 1, device=dev) + 0.5 for k in ("C_in", "C_out", "C_direc
 prm["W_main_in"] = torch.zeros(F, F, device=dev)
 ALT = [int(a, 0) for a in os.environ.get("PG_PROBE_ALT", "").split(",") if a]
 cases = {"fwd_ngram": lambda: ops.spmm3(g, x), "gated_ngram": lambda: ops.spmm3_gated(g, x, prm, 0),
+         "fwd_block4": lambda: ops.spmm3(g, x, flags=PG_FLAG_NGRAM_BLOCK4),
+         "gated_block4": lambda: ops.spmm3_gated(g, x, prm, 0, flags=PG_FLAG_NGRAM_BLOCK4),
          "fwd_csr": lambda: ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM),
          "bwd_ngram": lambda: ops.spmm3_t(g, G), "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
 for a in ALT:
     cases[f"fwd_alt{a:#x}"] = (lambda a: lambda: ops.spmm3(g, x, flags=a))(a)
     cases[f"gated_alt{a:#x}"] = (lambda a: lambda: ops.spmm3_gated(g, x, prm, 0, flags=a))(a)
+cases = {k: fn for k, fn in cases.items() if fn() is not None}
 best = {k: 1e9 for k in cases}
 for _ in range(4):
     for k, fn in cases.items():
         best[k] = min(best[k], timeit(fn))
 ref = ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM)
-for k in ["fwd_ngram"] + [f"fwd_alt{a:#x}" for a in ALT]:
+for k in [c for c in ["fwd_ngram", "fwd_block4"] + [f"fwd_alt{a:#x}" for a in ALT] if c in cases]:
     z = cases[k]()
     print(f"{k}: max |d| vs csr {float((z - ref).abs().max()):.3e}")
+refg = ops.spmm3_gated(g, x, prm, 0, flags=PG_FLAG_NO_NGRAM)
+for k in [c for c in ("gated_ngram", "gated_block4") if c in cases]:
+    z = cases[k]()
+    if z is None:
+        print(f"{k}: no gated kernel for this graph (the dense kernel gates)")
+        continue
+    print(f"{k}: max |d| vs csr {float((z - refg).abs().max()):.3e} (max |ref| {float(refg.abs().max()):.3e})")
 comp = g.compulsory_bytes(F)
 print(" ".join(f"{k}={v:.4f}ms" for k, v in best.items()), f"compulsory_fwd={comp / 1e6:.1f}MB "
       f"-> {comp / best['fwd_ngram'] / 1e6:.0f} GB/s")

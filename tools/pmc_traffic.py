@@ -4,7 +4,7 @@
 Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reports half the bytes of wide coalesced
 (16 B/lane) reads on gfx950 -> read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KiB) is exact for
 16 B/lane stores -> write bytes = WRITE_SIZE * 1024. Averages over all dispatches of each kernel.
-The "dominant" kernel is the one with the largest total duration in the FETCH_SIZE pass's kernel trace.
+The "dominant" kernel is the propagation kernel with the largest total duration in the FETCH_SIZE pass's trace.
 Used by bench.py (live, every N=1 run) and from the command line:
 usage: tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> <workload-tag>
 """
@@ -36,7 +36,10 @@ def durations(d):
     return {k: (tot[k], tot[k] / cnt[k]) for k in tot}
 
 
-def reduce(fetch_dir, write_dir):
+def reduce(fetch_dir, write_dir, prefer=("ngram", "spmm")):
+    """Per-kernel traffic; "kernel" = the propagation kernel (a name containing one of `prefer`) with the largest
+    total duration, else the kernel with the largest total duration (a pass over the trainer's COO entry also traces
+    the one-time COO -> CSR sorts, which must not be mistaken for the dominant kernel)."""
     fetch, nf = per_kernel(fetch_dir, "FETCH_SIZE")
     write, nw = per_kernel(write_dir, "WRITE_SIZE")
     dur = durations(fetch_dir)
@@ -51,6 +54,8 @@ def reduce(fetch_dir, write_dir):
     res = {"correction": "read = 2*FETCH_SIZE KiB (gfx950 half-count on 16B/lane reads); write = WRITE_SIZE KiB",
            "kernels": kernels}
     ranked = sorted((k for k in kernels if k in dur), key=lambda k: -dur[k][0])
+    pref = [k for k in ranked if any(t in k for t in prefer)]
+    ranked = pref or ranked
     if ranked:
         res["kernel"] = ranked[0]
         res["kernel_bytes_per_launch"] = kernels[ranked[0]]["bytes_per_launch"]

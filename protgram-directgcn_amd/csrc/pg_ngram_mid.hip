@@ -4,18 +4,20 @@
 // Structure (pg_ngram_spmm.hip has the derivation): row i = a.M.b (a = first letter, M = the middle
 // n-2 letters, b = last letter). Its out-sources are M.b.c, its in-sources c.a.M (c = 0..K-1). For one middle M and
 // one 16-feature column chunk f:
-//   out-phase, per b:  P[(k, a), f] = sum_c Wout_k[a, b, c] X[M.b.c, f]      a GEMM (3K rows (k,a)) x (K) x (16)
-//   in-phase,  per a:  Z[(k, b), f] = P[(k, a) of b] + sum_c Win_k[a, b, c] X[c.a.M, f] + Wdiag_k[a, b] X[a.M.b, f]
+//   out-phase, per b:  P[(k, a), f] = sum_c Wout_k[a, b, c] X[M.b.c, f] + Wdiag_k[a, b] X[a.M.b, f]
+//                      (a GEMM (3K rows (k,a)) x (K) x (16), plus the diagonal by a VALU FMA)
+//   in-phase,  per a:  Z[(k, b), f] = P[(k, a) of b] + sum_c Win_k[a, b, c] X[c.a.M, f]
 // Each phase is 20 dense 60 x 20 x 16 products (rows padded to 64): 80 MFMA tiles of 16 x 16 (K = 20 = 5 steps of
 // 4), shared by 8 compute waves (10 tiles each). The out-phase results are handed to the in-phase through an LDS
 // partial buffer laid out in the in-phase's accumulator order (the two phases group the rows differently: by b, then
 // by a), read back as the in-phase MFMAs' initial accumulators.
 //
-// Operands: the weights are the MFMA A fragments, loaded ONCE per work item into registers (the plan is stored in
-// fragment order, 256 B per fragment: one coalesced dword per lane) and reused for every column chunk of the item;
-// the source rows are the B fragments, read from LDS, where two loader waves bring each chunk's 800 source rows and
-// 400 self rows by LDS-DMA (64 B per row chunk), one phase ahead of their use. A work item is (M, group of NCG
-// consecutive 16-feature chunks); the kernel is persistent (one workgroup of 8 compute + 2 loader waves per CU).
+// Operands: the weights are the MFMA A fragments, loaded into registers once per middle a workgroup visits (the plan is stored in
+// fragment order, 256 B per fragment: one coalesced dword per lane) and reused for every column chunk of it;
+// the source rows are the B fragments, read from LDS, where four loader waves bring each chunk's 800 source rows and
+// 400 self rows by LDS-DMA (64 B per row chunk), one phase ahead of their use. The kernel is persistent (one workgroup
+// of 8 compute + 4 loader waves per CU), each workgroup walking a contiguous range of the (middle, 16-feature chunk)
+// stream.
 //
 // Plan layout (pg_ngram_mplan_f32, built from the CSR; slot rules as pg_ngram_plan_f32: an entry goes to its
 // out-slot, else its in-slot, else the diagonal; a missing transition leaves 0; an entry that fits no slot marks the
@@ -25,9 +27,10 @@
 //   diag [a][b][k]
 // Rows i >= 3K are zero padding.
 //
-// Numerics: each aggregate is the same sum of w*x terms as the reference's propagate(), accumulated in fp32 by the
-// MFMA (exact fp32 FMA chain, k-ordered: out-slots, in-slots, then the diagonal by a VALU FMA): within fp32 rounding
-// of the reference (|d| <= 1e-5 + 1e-5|ref|), like pg_spmm3_ngram_f32. Zero weights add 0 * x: X must be finite.
+// Numerics: each aggregate is the same sum of w*x terms as the reference's propagate(), accumulated in fp32 (the
+// MFMA sums in groups of 4 c: out-slots, then the diagonal by a VALU FMA, then in-slots) in another order than the
+// reference's scatter_add: within fp32 rounding of it (|d| <= 1e-5 + 1e-5|ref|), like pg_spmm3_ngram_f32. Zero
+// weights add 0 * x: X must be finite.
 #include "pg_common.h"
 
 namespace {
@@ -50,11 +53,13 @@ constexpr int XPD = 2 * XPI;                        // diagonal weights [a][b][k
 constexpr int XMB = XPD + XR * 3;                   // floats per middle: 52,400
 // LDS image (bytes)
 constexpr int LOUT = 0;                             // out-sources [b][c][16 f]   400 rows x 64 B
-constexpr int LIN = LOUT + XR * 64;                 // in-sources  [a][c][16 f]
-constexpr int LSELF = LIN + XR * 64;                // self rows   [a][b][16 f]
+constexpr int XCB = XK + 1;                         // in-source c-block rows (one pad row: bank offset 16)
+constexpr int LIN = LOUT + XR * 64;                 // in-sources  [c][a (+pad)][16 f]
+constexpr int LINB = (XK * XCB * 64 + 1023) / 1024 * 1024;  // in-region bytes: whole LDS-DMA wave-instructions
+constexpr int LSELF = LIN + LINB;                   // self rows   [a][b][16 f]
 constexpr int LPART = LSELF + XR * 64;              // partial     [a][row k K + b (3K)][16 f] fp32
 constexpr int LDIAG = LPART + XK * 3 * XK * 64;     // diagonal weights [a][b][k]
-constexpr int LBYTES = LDIAG + XR * 3 * 4;          // 158,400 B
+constexpr int LBYTES = LDIAG + XR * 3 * 4;          // 160,448 B
 static_assert(LBYTES <= 163840, "LDS image exceeds 160 KiB");
 static_assert(XTILES % XCW == 0 && XTPW % 2 == 0, "tiles per wave");
 
@@ -67,9 +72,7 @@ struct XP {
     int64_t ldz;
     int F;
     int nch;               // F / 16
-    int ncg;               // chunks per work item
-    int ngrp;              // work items per middle = ceil(nch / ncg)
-    int items;             // K^(n-2) * ngrp
+    int chunks;            // K^(n-2) * nch: the (middle, chunk) stream, middle-major
     int remap;
     unsigned long long* stamps;  // diagnostics build only (PG_MID_STAMPS): s_memtime per block, chunk and point
 };
@@ -93,43 +96,66 @@ __device__ __forceinline__ void glds16(const float* src, const void* lds_base) {
 }
 
 struct Chunk {
-    int M, ch, first;  // middle, chunk index, first chunk of its work item
+    int M, ch, first;  // middle, chunk index, first chunk of this middle in the workgroup's range
 };
 
-__global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
+__global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     extern __shared__ __attribute__((aligned(16))) char L[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int first = (int)pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
-    const int stride = gridDim.x;
-
-    // the chunk stream of this workgroup: items first, first + stride, ..., each NCG chunks (fewer in a last group)
-    auto chunk_at = [&](int item, int cc) -> Chunk {
-        const int M = item / p.ngrp;
-        const int g = item - M * p.ngrp;
-        return Chunk{M, g * p.ncg + cc, cc == 0};
-    };
-    auto chunks_of = [&](int item) {
-        const int g = item % p.ngrp;
-        const int n = p.nch - g * p.ncg;
-        return n < p.ncg ? n : p.ncg;
+    XSTAMP(0, 5);  // kernel entry
+    // This workgroup's share of the chunk stream: the contiguous range [g0, g1) of (middle, chunk) pairs in
+    // middle-major order (ranges differ by at most one chunk: no tail of whole middles; the weights reload only where
+    // the middle changes; neighbouring ranges, which share a middle, sit on the same XCD)
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int g0 = (int)(lb * p.chunks / gridDim.x), g1 = (int)((lb + 1) * p.chunks / gridDim.x);
+    auto chunk_at = [&](int g) -> Chunk {
+        const int M = g / p.nch;
+        const int ch = g - M * p.nch;
+        return Chunk{M, ch, g == g0 || ch == 0};
     };
 
     if (wave >= XCW) {  // ---------------- loader waves: LDS-DMA only (same barrier sequence as the compute waves)
         const int lw = wave - XCW;
-        // one region of 400 rows x 64 B = 25 wave-instructions, split over the loader waves
+        // One region = 400 rows x 64 B = 25 wave-instructions (in-sources: 420 rows with the pad rows, 27), split over
+        // the loader waves; piece order = LDS order; the in-sources are fetched c-major (one wave-instruction: rows
+        // c.a.M of one c, within 4 MB). The per-lane part of every piece's element offset does not depend on the
+        // middle or the chunk: computed once here (64-bit, in registers), so a DMA costs one add per instruction.
+        constexpr int NO = (XR * 4 / 64 + XLW - 1) / XLW, NI = (LINB / 1024 + XLW - 1) / XLW;
+        int64_t off_o[NO], off_i[NI], off_s[NO];
+        const int64_t ldx = p.ldx;
+#pragma unroll
+        for (int t = 0; t < NO; ++t) {
+            const int it = lw + t * XLW;
+            const int rl = (it * 64 + lane) >> 2, q = lane & 3;
+            off_o[t] = (int64_t)rl * ldx + q * 4;                                    // out: row M.b.c = 400 M + rl
+            const int a = rl / XK, b = rl - a * XK;
+            off_s[t] = (a * p.Kn1 + b) * ldx + q * 4;                                 // self: a.M.b = a K^(n-1) + 20 M + b
+        }
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            const int it = lw + t * XLW;
+            const int rl = (it * 64 + lane) >> 2, q = lane & 3;
+            const int c = rl / XCB, a = rl - c * XCB;
+            off_i[t] = (a >= XK || c >= XK) ? q * 4 : (c * p.Kn1 + a * p.Kn2) * ldx + q * 4;  // in: c.a.M (+ M); pad: row M
+        }
         auto dma_rows = [&](int region, int kind, int M, int ch) {
             const float* xc = p.X + ch * XFC;
-#pragma unroll 1
-            for (int it = lw; it < XR * 4 / 64; it += XLW) {
-                const int P = it * 64 + lane;
-                const int rl = P >> 2, q = P & 3;
-                const int u = rl / XK, v = rl - u * XK;
-                int64_t row;
-                if (kind == 0) row = (int64_t)M * XR + u * XK + v;                   // out: (b = u, c = v) -> M.b.c
-                else if (kind == 1) row = v * p.Kn1 + u * p.Kn2 + M;                 // in:  (a = u, c = v) -> c.a.M
-                else row = u * p.Kn1 + (int64_t)M * XK + v;                          // self: (a = u, b = v) -> a.M.b
-                glds16(xc + row * p.ldx + q * 4, L + region + it * 1024);
+            if (kind == 0) {
+                const float* base = xc + (int64_t)M * XR * ldx;
+#pragma unroll
+                for (int t = 0; t < NO; ++t)
+                    if (lw + t * XLW < XR * 4 / 64) glds16(base + off_o[t], L + region + (lw + t * XLW) * 1024);
+            } else if (kind == 1) {
+                const float* base = xc + (int64_t)M * ldx;
+#pragma unroll
+                for (int t = 0; t < NI; ++t)
+                    if (lw + t * XLW < LINB / 1024) glds16(base + off_i[t], L + region + (lw + t * XLW) * 1024);
+            } else {
+                const float* base = xc + (int64_t)M * XK * ldx;
+#pragma unroll
+                for (int t = 0; t < NO; ++t)
+                    if (lw + t * XLW < XR * 4 / 64) glds16(base + off_s[t], L + region + (lw + t * XLW) * 1024);
             }
         };
         auto dma_diag = [&](int M) {  // 4,800 B = 300 pieces: wave-instructions 0..4 (the last one partial)
@@ -140,45 +166,39 @@ __global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
                 if (P < XR * 3 / 4) glds16(d + P * 4, L + LDIAG + it * 1024);
             }
         };
-        int item = first, cc = 0;
-        if (item < p.items) {
-            const Chunk c0 = chunk_at(item, 0);
+        if (g0 < g1) {
+            const Chunk c0 = chunk_at(g0);
             dma_rows(LOUT, 0, c0.M, c0.ch);
             dma_rows(LIN, 1, c0.M, c0.ch);
             dma_rows(LSELF, 2, c0.M, c0.ch);
             dma_diag(c0.M);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        XSTAMP(0, 6);
         asm volatile("s_barrier" ::: "memory");  // S(-1)
         int ci = 0;
 #pragma unroll 1
-        while (item < p.items) {
-            int nitem = item, ncc = cc + 1;  // next chunk of the stream
-            if (ncc >= chunks_of(item)) {
-                nitem = item + stride;
-                ncc = 0;
-            }
-            const bool more = nitem < p.items;
-            const Chunk nx = more ? chunk_at(nitem, ncc) : Chunk{0, 0, 0};
+        for (int g = g0; g < g1; ++g) {
+            const bool more = g + 1 < g1;
+            const Chunk nx = more ? chunk_at(g + 1) : Chunk{0, 0, 0};
             XSTAMP(ci, 0);
-            asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done, partial written, out-region free
+            asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done, partial written; out / self / diag free
             XSTAMP(ci, 1);
-            if (more) dma_rows(LOUT, 0, nx.M, nx.ch);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            XSTAMP(ci, 2);
-            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in / self / diag / partial free
-            XSTAMP(ci, 3);
             if (more) {
-                dma_rows(LIN, 1, nx.M, nx.ch);
+                dma_rows(LOUT, 0, nx.M, nx.ch);
                 dma_rows(LSELF, 2, nx.M, nx.ch);
                 if (nx.first) dma_diag(nx.M);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            XSTAMP(ci, 2);
+            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in / partial free
+            XSTAMP(ci, 3);
+            if (more) dma_rows(LIN, 1, nx.M, nx.ch);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             XSTAMP(ci, 4);
-            item = nitem;
-            cc = ncc;
             ++ci;
         }
+        XSTAMP(0, 7);
         return;
     }
 
@@ -187,18 +207,22 @@ __global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
     // 2 j + (w >> 2), j = 0..9, so every LDS address below is a per-lane base plus a compile-time offset in j and s.
     const int q4 = lane >> 4, fl = lane & 15;
     const int mw = wave & 3, wb = wave >> 2;
-    float Ao[XTPW][XS], Ai[XTPW][XS];  // A fragments of this wave's out / in tiles (item-resident)
-    auto load_A = [&](int M) {
-        const float* pm = p.plan + (int64_t)M * XMB + lane;
+    float Ao[XTPW][XS], Ai[XTPW][XS];  // A fragments of this wave's out / in tiles (middle-resident)
+    // A fragments of the next middle are prefetched where the registers are free: Ao after the last chunk's
+    // out-phase (consumed by the next middle's first out-phase), Ai before its first chunk's out-phase
+    auto load_Ao = [&](int M) {
+        const float* pm = p.plan + (int64_t)M * XMB + XPO + lane;
 #pragma unroll
-        for (int j = 0; j < XTPW; ++j) {
-            const int t = (2 * j + wb) * 4 + mw;  // tile t = (b or a) * 4 + m
+        for (int j = 0; j < XTPW; ++j)
 #pragma unroll
-            for (int s = 0; s < XS; ++s) {
-                Ao[j][s] = pm[XPO + (t * XS + s) * 64];
-                Ai[j][s] = pm[XPI + (t * XS + s) * 64];
-            }
-        }
+            for (int s = 0; s < XS; ++s) Ao[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+    };
+    auto load_Ai = [&](int M) {
+        const float* pm = p.plan + (int64_t)M * XMB + XPI + lane;
+#pragma unroll
+        for (int j = 0; j < XTPW; ++j)
+#pragma unroll
+            for (int s = 0; s < XS; ++s) Ai[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
     };
     // this lane's four accumulator rows i = 16 mw + 4 q4 + r: (k, a) in the out-phase, (k, b) in the in-phase
     int rk[4], rv[4];
@@ -211,22 +235,34 @@ __global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
         rv[r] = rok[r] ? i - rk[r] * XK : 0;
     }
     // LDS byte offsets: sources [row][16 f] (64 B rows); partial [a][row k K + b][16 f]
-    const int src_lane = (q4 * 16 + fl) * 4;                 // + (col * K + 4 s) * 64
+    const int src_lane = (q4 * 16 + fl) * 4;                 // out: + (b * K + 4 s) * 64
+    const int in_lane = (q4 * XCB * 16 + fl) * 4;            // in:  + (4 s * XCB + a) * 64
     int part_w[4], part_r[4], self_r[4], diag_r[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         part_w[r] = LPART + ((rv[r] * 3 * XK + rk[r] * XK + wb) * 16 + fl) * 4;  // out: a = rv, row k K + b; + 2 j * 64
         part_r[r] = LPART + ((wb * 3 * XK + 16 * mw + 4 * q4 + r) * 16 + fl) * 4;  // in: + 2 j * 60 * 64
-        self_r[r] = LSELF + ((wb * XK + rv[r]) * 16 + fl) * 4;                     // in: (a, b = rv); + 2 j * K * 64
-        diag_r[r] = LDIAG + ((wb * XK + rv[r]) * 3 + rk[r]) * 4;                   // + 2 j * K * 12
+        self_r[r] = LSELF + ((rv[r] * XK + wb) * 16 + fl) * 4;                     // out: (a = rv, b); + 2 j * 64
+        diag_r[r] = LDIAG + ((rv[r] * XK + wb) * 3 + rk[r]) * 4;                   // + 2 j * 12
+    }
+    // store-out of a finished in-phase tile: lane l writes 16 B = features 4 (l & 3) .. + 3 of tile row l >> 2
+    const int so_i = 16 * mw + (lane >> 2);
+    const bool so_ok = so_i < 3 * XK;
+    const int so_k = so_ok ? so_i / XK : 0, so_b = so_ok ? so_i - so_k * XK : 0;
+    const int so_lds = LPART + ((wb * 3 * XK + so_i) * 16 + 4 * (lane & 3)) * 4;  // + 2 j * 60 * 64
+    const int64_t zstep = 2 * p.Kn1 * p.ldz;                                        // a -> a + 2
+    if (g0 < g1) {
+        load_Ao(chunk_at(g0).M);
+        load_Ai(chunk_at(g0).M);
     }
     asm volatile("s_barrier" ::: "memory");  // S(-1)
-    int item = first, cc = 0, ci = 0;
+    XSTAMP(0, 6);
+    int ci = 0;
 #pragma unroll 1
-    while (item < p.items) {
-        const Chunk cu = chunk_at(item, cc);
+    for (int g = g0; g < g1; ++g) {
+        const Chunk cu = chunk_at(g);
         XSTAMP(ci, 0);
-        if (cu.first) load_A(cu.M);
+        const bool next_mid = g + 1 < g1 && cu.ch + 1 == p.nch;  // the next chunk starts another middle
         // ---- out-phase: tiles (b = 2 j + wb, m = mw); hand-over of row (k, a) to the in-phase row k K + b of a
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
@@ -241,22 +277,25 @@ __global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                if (rok[r]) {
-                    *reinterpret_cast<float*>(L + part_w[r] + 2 * j * 64) = acc0[r];
-                    *reinterpret_cast<float*>(L + part_w[r] + (2 * j + 2) * 64) = acc1[r];
+                if (rok[r]) {  // + the diagonal term Wdiag_k[a, b] X[a.M.b, f]
+                    const float w0 = *reinterpret_cast<const float*>(L + diag_r[r] + 2 * j * 12);
+                    const float w1 = *reinterpret_cast<const float*>(L + diag_r[r] + (2 * j + 2) * 12);
+                    const float s0 = *reinterpret_cast<const float*>(L + self_r[r] + 2 * j * 64);
+                    const float s1 = *reinterpret_cast<const float*>(L + self_r[r] + (2 * j + 2) * 64);
+                    *reinterpret_cast<float*>(L + part_w[r] + 2 * j * 64) = __builtin_fmaf(w0, s0, acc0[r]);
+                    *reinterpret_cast<float*>(L + part_w[r] + (2 * j + 2) * 64) = __builtin_fmaf(w1, s1, acc1[r]);
                 }
             asm volatile("" ::: "memory");
         }
+        if (next_mid) load_Ao(cu.M + 1);
         XSTAMP(ci, 1);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // M(t)
         XSTAMP(ci, 2);
-        // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer
+        // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
+        // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
-        float* zb[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            zb[r] = p.Z + ((int64_t)wb * p.Kn1 + (int64_t)M * XK + rv[r]) * p.ldz + (int64_t)rk[r] * p.F + cu.ch * XFC + fl;
-        const int64_t zstep = 2 * p.Kn1 * p.ldz;  // a -> a + 2
+        float* zso = p.Z + ((int64_t)wb * p.Kn1 + (int64_t)M * XK + so_b) * p.ldz + (int64_t)so_k * p.F +
+                     cu.ch * XFC + 4 * (lane & 3);
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
             f4_t acc0, acc1;
@@ -267,33 +306,35 @@ __global__ __launch_bounds__(XTHREADS) void ngram_x_kernel(XP p) {
             }
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
-                const float x0 = *reinterpret_cast<const float*>(L + LIN + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
+                const float x0 = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
                 const float x1 =
-                    *reinterpret_cast<const float*>(L + LIN + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
+                    *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j][s], x0, acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j + 1][s], x1, acc1, 0, 0, 0);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 if (rok[r]) {
-                    const float w0 = *reinterpret_cast<const float*>(L + diag_r[r] + 2 * j * XK * 12);
-                    const float w1 = *reinterpret_cast<const float*>(L + diag_r[r] + (2 * j + 2) * XK * 12);
-                    const float s0 = *reinterpret_cast<const float*>(L + self_r[r] + 2 * j * XK * 64);
-                    const float s1 = *reinterpret_cast<const float*>(L + self_r[r] + (2 * j + 2) * XK * 64);
-                    zb[r][(int64_t)j * zstep] = __builtin_fmaf(w0, s0, acc0[r]);
-                    zb[r][(int64_t)(j + 1) * zstep] = __builtin_fmaf(w1, s1, acc1[r]);
+                    *reinterpret_cast<float*>(L + part_r[r] + 2 * j * 3 * XK * 64) = acc0[r];
+                    *reinterpret_cast<float*>(L + part_r[r] + (2 * j + 2) * 3 * XK * 64) = acc1[r];
                 }
+            // the wave's own tile rows: in-order LDS, no barrier (the empty asm keeps the compiler's order)
+            asm volatile("" ::: "memory");
+            const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
+            const f4_t v1 = *reinterpret_cast<const f4_t*>(L + so_lds + (2 * j + 2) * 3 * XK * 64);
+            if (so_ok) {
+                *reinterpret_cast<f4_t*>(zso + (int64_t)j * zstep) = v0;
+                *reinterpret_cast<f4_t*>(zso + (int64_t)(j + 1) * zstep) = v1;
+            }
             asm volatile("" ::: "memory");
         }
         XSTAMP(ci, 3);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // S(t)
         XSTAMP(ci, 4);
         ++ci;
-        if (++cc >= chunks_of(item)) {
-            item += stride;
-            cc = 0;
-        }
+        if (next_mid) load_Ai(cu.M + 1);
     }
+    XSTAMP(0, 7);
 }
 
 // Plan construction: one thread per CSR row scatters its entries into the fragment-ordered slots.
@@ -402,9 +443,9 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
         return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: no gated store (the dense kernel gates)");
     if (F <= 0 || F % XFC)
         return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: F must be a multiple of %d", XFC);
-    if (!pg::aligned16(X) || !pg::aligned16(plan) || (ldx * 4) % 16)
-        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: needs 16-B aligned X rows");
-    PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 30), "too many work items");
+    if (!pg::aligned16(X) || !pg::aligned16(plan) || !pg::aligned16(Z) || (ldx * 4) % 16 || (ldz * 4) % 16)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: needs 16-B aligned X and Z rows");
+    PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 30), "too many column chunks");
     XP p{};
     p.Kn1 = Kn1;
     p.Kn2 = Kn2;
@@ -415,25 +456,20 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     p.ldz = ldz;
     p.F = (int)F;
     p.nch = (int)(F / XFC);
-    // chunks per work item: the weights (A fragments) load once per item; smaller items balance the persistent grid
-    const int req = (int)((flags >> 24) & 15u);
-    p.ncg = req ? req : 4;
-    if (p.ncg > p.nch) p.ncg = p.nch;
-    p.ngrp = (p.nch + p.ncg - 1) / p.ncg;
-    p.items = (int)(Kn2 * p.ngrp);
+    p.chunks = (int)(Kn2 * p.nch);
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.stamps = stamps;
     const int64_t cap = grid_cap();
-    const unsigned grid = (unsigned)(p.items < cap ? p.items : cap);
+    const unsigned grid = (unsigned)(p.chunks < cap ? p.chunks : cap);
     hipStream_t s = (hipStream_t)stream;
     static bool attr_set = false;  // the kernel's dynamic LDS exceeds the 64 KiB default (set once; idempotent)
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_x_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_mid_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 LBYTES) != hipSuccess)
             return pg::set_error(PG_ERR_HIP, "pg_spmm3_ngram_mid_f32: cannot raise the LDS limit");
         attr_set = true;
     }
-    hipLaunchKernelGGL(ngram_x_kernel, dim3(grid), dim3(XTHREADS), LBYTES, s, p);
+    hipLaunchKernelGGL(ngram_mid_kernel, dim3(grid), dim3(XTHREADS), LBYTES, s, p);
     return pg::check_launch("pg_spmm3_ngram_mid_f32");
 }
 

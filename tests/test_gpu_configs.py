@@ -83,7 +83,7 @@ def _count_tile_launches(monkeypatch):
     from collections import Counter
     from protgram_directgcn_amd import ops
     lib, calls = ops.load_library(), Counter()
-    for name in ("pg_spmm3_ngram_f32", "pg_spmm3t_ngram_f32", "pg_spmm3t_ngram_bf16"):
+    for name in ("pg_spmm3_ngram_f32", "pg_spmm3_ngram_mid_f32", "pg_spmm3t_ngram_f32", "pg_spmm3t_ngram_bf16"):
         fn = getattr(lib, name)
 
         def wrap(*a, _fn=fn, _name=name):
@@ -91,6 +91,11 @@ def _count_tile_launches(monkeypatch):
             return _fn(*a)
         monkeypatch.setattr(lib, name, wrap)
     return calls
+
+
+def _fwd_tile(calls):
+    """Forward n-gram tile launches: the middle-tile kernel (default) or the 4x4-block kernel."""
+    return calls["pg_spmm3_ngram_mid_f32"] + calls["pg_spmm3_ngram_f32"]
 
 
 def _labels(N, n):
@@ -142,7 +147,7 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     calls = _count_tile_launches(monkeypatch)
     with torch.no_grad():
         lp_c, emb_c = m(data_coo)
-    assert calls["pg_spmm3_ngram_f32"] == len(m.convs), calls
+    assert _fwd_tile(calls) == len(m.convs), calls
     assert torch.equal(lp_c, lp_m) and torch.equal(emb_c, emb_m)
 
     ei, w = _csr_coo(g)
@@ -192,7 +197,7 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     opt = train.Adam(m.parameters(), lr=LR)
     calls.clear()
     loss_s = train.train_step(m, data_coo, yd, opt, l2_lambda=LAM, scaler=None)  # through the trainer's COO wiring
-    assert calls["pg_spmm3_ngram_f32"] == len(m.convs) and calls["pg_spmm3t_ngram_f32"] == len(m.convs) - 1, calls
+    assert _fwd_tile(calls) == len(m.convs) and calls["pg_spmm3t_ngram_f32"] == len(m.convs) - 1, calls
     assert abs(float(loss_s) - loss_r) <= 1e-5 * abs(loss_r)
     for k, prm in m.named_parameters():
         gref = p[k].grad
@@ -314,6 +319,51 @@ def test_config4_5gram_halo_partition_bitexact(pkg, cuda, five_gram, rank):
     lp, emb = shard.halo_forward(f["m"], hp, inp)
     rows = hp.global_rows
     assert torch.equal(lp, f["lp_csr"][rows]) and torch.equal(emb, f["emb_csr"][rows])
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("rank", [0, 7])
+def test_config4_5gram_exchange_partition_bitexact(pkg, cuda, five_gram, rank, monkeypatch):
+    """The node-range exchange partition (config 4's RCCL design: shard.sharded_forward, chunked all-gather between
+    the layers) at 5-gram for ranks 0 and 7 of P = 8, on this one GPU: the all-gather is replaced by a copy that
+    fills the other ranks' rows from the single-GPU layer-1 output (this rank's own chunk is what it computed), so
+    the rank runs exactly its production code -- row-chunked layer 1 on the row-sliced CSR, remapped CSR reading the
+    chunk-major gathered buffer in layer 2, dense layer on row slices of the per-node parameters. Its rows equal the
+    single-GPU forward on the same (CSR, ungated) kernels bit for bit, layer 1 and the outputs."""
+    from protgram_directgcn_amd import ops, shard
+    f = five_gram
+    g, m, xd, N = f["g"], f["m"], f["xd"], f["N"]
+    gc = dataclasses.replace(g, ngram=None)  # a rank's row-sliced CSR has no tile plan: compare on the CSR kernels
+    monkeypatch.setattr(ops, "PREGATED_INFERENCE", False)  # sharded_forward gates in the dense kernel
+    with torch.no_grad():
+        h1 = m.convs[0].fused_forward(xd, gc, None, res_x=xd, act=True)
+        h2 = m.convs[1].fused_forward(h1, gc, None, res_x=h1, act=True)
+        lp_ref, emb_ref = m.head(h2)
+    part = shard.partition(g, rank, 8)
+    calls = [0]
+    own_ok = []
+
+    def fake_gather(send, dst, prt, group=None):
+        k = calls[0]
+        calls[0] += 1
+        W, cs = prt.world, send.size(0)
+        v = dst.view(W, cs, -1)
+        for q in range(W):
+            lo = q * prt.per + k * cs
+            hi = min(lo + cs, (q + 1) * prt.per, prt.n)
+            if q == prt.rank:
+                v[q].copy_(send)
+                if hi > lo:
+                    own_ok.append(torch.equal(send[:hi - lo], h1[lo:hi]))
+            elif hi > lo:
+                v[q, :hi - lo] = h1[lo:hi]
+        return None
+
+    monkeypatch.setattr(shard, "_all_gather_chunk", fake_gather)
+    lp, emb = shard.sharded_forward(m, part, xd, chunks=4)
+    assert calls[0] == 4 and own_ok and all(own_ok)  # layer 1's own rows: bit-exact
+    assert lp.shape[0] == part.n_local
+    assert torch.equal(lp, lp_ref[part.r0:part.r1]) and torch.equal(emb, emb_ref[part.r0:part.r1])
 
 
 # ---------------------------------------------------------------------------------------------------------------

@@ -295,6 +295,49 @@ def test_full_size_4gram_layer_vs_oracle(pkg, cuda, n, F):
         assert_close(Zn[:, j * F:(j + 1) * F], ref, f"n-gram tile propagation {j}")
 
 
+@pytest.mark.parametrize("n,F,drop", [(2, 16, 0.0), (2, 48, 0.3), (3, 64, 0.0), (3, 128, 0.5), (3, 256, 0.2),
+                                      (4, 32, 0.1)])
+def test_ngram_mid_kernel_vs_csr(pkg, cuda, monkeypatch, n, F, drop):
+    """The middle-tile forward (pg_spmm3_ngram_mid_f32, the default n-gram kernel for F % 16 == 0) against the
+    bit-exact CSR kernel, on complete de Bruijn graphs and on graphs with a random share of the transitions dropped
+    (zero plan slots), at F not served by the 4x4-block kernel; also called through the C-ABI with padded rows
+    (ldx > F, ldz > 3F) that must stay untouched."""
+    from protgram_directgcn_amd import _lib, ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    if drop:
+        keep = np.random.default_rng(n * 1000 + F).random(s.size) >= drop
+        s, d, c = s[keep], d[keep], c[keep]
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    assert g.ngram is not None and g.ngram.mplan is not None
+    x = torch.randn(N, F, generator=torch.Generator().manual_seed(7)).to(cuda)
+    lib = ops.load_library()
+    hits = []
+    real = lib.pg_spmm3_ngram_mid_f32
+    monkeypatch.setattr(lib, "pg_spmm3_ngram_mid_f32", lambda *a: hits.append(1) or real(*a))
+    Z = ops.spmm3(g, x)
+    assert hits, "the middle-tile kernel did not run"
+    Zc = ops.spmm3(g, x, flags=_lib_csr())
+    assert_close(Z, Zc, f"mid kernel n={n} F={F} drop={drop}")
+    if F in (64, 128, 256):
+        Zb = ops.spmm3(g, x, flags=ops.default_flags() | _lib.PG_FLAG_NGRAM_BLOCK4)
+        assert_close(Zb, Zc, f"4x4-block kernel n={n} F={F}")
+    # raw C-ABI call on padded rows
+    xp = torch.randn(N, F + 16, generator=torch.Generator().manual_seed(8)).to(cuda)
+    xp[:, :F] = x
+    Zp = torch.full((N, 3 * F + 32), 7.0, device=cuda)
+    ng = g.ngram
+    torch.cuda.synchronize()
+    rc = real(ng.K, ng.n, N, ops._p(ng.mplan), ops._p(xp), xp.stride(0), F, None, ops._p(Zp), Zp.stride(0),
+              ops.default_flags(), ops._stream(xp))
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    assert torch.equal(Zp[:, :3 * F], Z)  # same kernel, same order: the same bits
+    assert bool((Zp[:, 3 * F:] == 7.0).all())
+    # shapes it does not take answer PG_ERR_UNSUPPORTED (the caller falls back), never launch
+    assert real(ng.K, ng.n, N, ops._p(ng.mplan), ops._p(xp), xp.stride(0), F + 8, None, ops._p(Zp), Zp.stride(0),
+                ops.default_flags(), ops._stream(xp)) == _lib.PG_ERR_UNSUPPORTED
+
+
 @pytest.mark.parametrize("F,H,C", [(128, 64, 20), (128, 64, 32), (128, 64, 1), (32, 16, 5), (256, 128, 50), (16, 8, 400),
                                    (34, 17, 3), (12, 6, 1)])
 def test_head_kernel_vs_torch(pkg, cuda, F, H, C):
@@ -1020,8 +1063,14 @@ def test_spmm3_gated_bitexact(pkg, cuda, name, F, vec):
     prm = {k: (torch.rand(shape, generator=gen) + 0.5).to(cuda) for k in ("C_in", "C_out", "C_directed", "C_undirected",
                                                                           "C_all")}
     prm["W_main_in"] = torch.zeros(F, F, device=cuda)  # shape only
+    fl = None
     Zg = ops.spmm3_gated(g, x, prm, 0 if vec else 1)
-    Z = ops.spmm3(g, x)
+    if Zg is None:  # the middle-tile kernel (default on complete n-gram graphs) leaves the gates to the dense kernel
+        from protgram_directgcn_amd import _lib
+        assert ops._mid_ok(g, x, ops.default_flags())
+        fl = ops.default_flags() | _lib.PG_FLAG_NGRAM_BLOCK4  # the 4x4-block tile kernel's gated store
+        Zg = ops.spmm3_gated(g, x, prm, 0 if vec else 1, flags=fl)
+    Z = ops.spmm3(g, x, flags=fl)
     cad = prm["C_all"] * prm["C_directed"]
     s = [cad * prm["C_in"], cad * prm["C_out"], prm["C_all"] * prm["C_undirected"]]
     ref = torch.cat([Z[:, k * F:(k + 1) * F] * s[k].view(-1, 1) for k in range(3)], 1)

@@ -104,6 +104,95 @@ def test_sharded_training_two_ranks_one_gpu(pkg, cuda):
         assert r[1], f"rank {r[0]}: {r[2]}"
 
 
+def _trainer_worker(rank, world, port, out_q, bf16):
+    """shard.ShardedTrainer (config 5's multi-GPU step: owned-row per-node state, flat all-reduce, device-side loss)
+    with the HIP kernels on 2 gloo ranks sharing cuda:0, against the single-GPU train.train_step: fp32 with SGD
+    (linear in the gradients) to the gradient tolerance; bf16 mode with train.Adam: loss within 2 % and gradient
+    cosine > 0.99 (different bf16 rounding points: the exchange and the ranks' partial sums)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import shard, train
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, g, model, x, y = _setup(pkg, dev)
+        ref = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        lam = 1e-3
+        dt = torch.bfloat16 if bf16 else torch.float32
+        model.compute_dtype = dt
+        part = shard.partition(g, rank, world, transpose=True)
+        fac = None if bf16 else (lambda ps: torch.optim.SGD(ps, lr=0.1))
+        tr = shard.ShardedTrainer(model, part, lr=1e-3, l2_lambda=lam, optimizer_factory=fac)
+        for d in tr.own:
+            for leaf in d.values():
+                assert leaf.size(0) == part.n_local and leaf.data_ptr() != 0
+        steps = 1 if bf16 else 2
+        losses, grads = [], {}
+        for _ in range(steps):
+            losses.append(float(tr.step(x, y[part.r0:part.r1])))
+        if bf16:  # the per-node Adam moments cover the owned rows only
+            for leaf in tr.node:
+                assert tr.opt.state[leaf]["exp_avg"].shape == leaf.shape
+            for li, conv in enumerate(model.convs):
+                for k, leaf in tr.own[li].items():
+                    grads[f"convs.{li}.{k}"] = leaf.grad.detach().float().clone()
+            for name, p in model.named_parameters():
+                if name not in grads:
+                    grads[name] = p.grad.detach().float().clone()
+        tr.gather()
+        # single-GPU reference: train.train_step on the whole graph
+        _, g1, m1, _, _ = _setup(pkg, dev)
+        m1.load_state_dict(ref)
+        m1.compute_dtype = dt
+        opt1 = train.Adam(m1.parameters(), lr=1e-3) if bf16 else torch.optim.SGD(m1.parameters(), lr=0.1)
+        rl = [float(train.train_step(m1, pkg.Data(x=x, graph=g1), y, opt1, l2_lambda=lam, scaler=None))
+              for _ in range(steps)]
+        bad = []
+        for a, b in zip(losses, rl):
+            if abs(a - b) > (2e-2 if bf16 else 1e-5) * abs(b) + 1e-6:
+                bad.append(("loss", losses, rl))
+        if bf16:
+            for name, p in m1.named_parameters():
+                r = p.grad.detach().float()
+                if shard._is_node_param(name, p, N):
+                    r = r[part.r0:part.r1]
+                gg = grads[name]
+                cos = float((gg * r).sum() / (gg.norm() * r.norm() + 1e-30))
+                if cos < 0.99:
+                    bad.append((name, "cos", cos))
+        else:
+            p1 = dict(m1.named_parameters())
+            for name, p in model.named_parameters():
+                r = p1[name].detach()
+                tol = 2e-5 * float(r.abs().max()) + 1e-6
+                err = float((p.detach() - r).abs().max())
+                if err > tol:
+                    bad.append((name, err, tol))
+        out_q.put((rank, not bad, str(bad[:4])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_sharded_trainer_two_ranks_one_gpu(pkg, cuda, bf16):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, bf16)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        assert r[1], f"rank {r[0]}: {r[2]}"
+
+
 @pytest.mark.parametrize("n,dims", [(3, [128, 128, 128]), (3, [64, 64, 32]), (2, [32, 32, 32, 16])])
 def test_halo_forward_bitexact_vs_single_gpu(pkg, cuda, n, dims):
     """Every rank of the halo-recompute partition (world 2, 3, 8; each rank run in turn on cuda:0, which is

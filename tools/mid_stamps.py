@@ -42,12 +42,16 @@ f.argtypes = [ctypes.c_int, ctypes.c_int, i64, vp, vp, i64, i64, vp, i64, ctypes
 CH, PT = 32, 8
 st = torch.zeros(256 * 2 * CH * PT, dtype=torch.int64, device=dev)
 stream = vp(torch.cuda.current_stream().cuda_stream)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for rep in range(3):
     st.zero_()
+    e0.record()
     rc = f(20, n, N, vp(g.ngram.mplan.data_ptr()), vp(x.data_ptr()), F, F, vp(Z.data_ptr()), 3 * F, flags,
            vp(st.data_ptr()), stream)
     assert rc == 0, rc
+    e1.record()
     torch.cuda.synchronize()
+ms = e0.elapsed_time(e1)
 ref = pkg.ops.spmm3(g, x, flags=pkg._lib.PG_FLAG_NO_NGRAM)
 print("max |d| vs csr", float((Z - ref).abs().max()))
 a = st.view(256, 2, CH, PT).cpu().numpy().astype(np.int64)
@@ -70,3 +74,11 @@ r = a[:, 0]
 tot = r[:, 1:, 0] - r[:, :-1, 0]
 v = tot[(r[:, 1:, 0] > 0) & (r[:, :-1, 0] > 0)]
 print(f"compute chunk-to-chunk median {np.median(v):.0f} cycles; blocks x chunks = {int((r[:, :, 0] > 0).sum())}")
+# whole-kernel timeline (pt 5: entry, 6: after the first chunk's operands are in, 7: exit), compute wave 0
+c0 = a[:, 0, 0]
+t0 = a[:, :, 0, 5][a[:, :, 0, 5] > 0].min()
+ent, rdy, ext = c0[:, 5] - t0, c0[:, 6] - t0, c0[:, 7] - t0
+span = max(a[:, :, 0, 7].max() - t0, 1)
+print(f"kernel {ms * 1e3:.1f} us (events, incl. launch); stamp span {span} cycles -> {span / (ms * 1e3):.0f} cycles/us")
+for nm, v in (("entry", ent), ("first operands in", rdy), ("exit", ext), ("busy (exit - entry)", ext - ent)):
+    print(f"  {nm:20s} min {v.min():8d} median {int(np.median(v)):8d} max {v.max():8d} cycles")

@@ -9,8 +9,8 @@ import sys
 
 
 def classify(k):
-    if "ngram_mid_fwd_kernel" in k:
-        return "ngram_mid_gated" if "true>" in k else "ngram_mid"
+    if "ngram_mid_kernel" in k:
+        return "ngram_mid"
     if "ngram_spmm3t_kernel" in k:
         return "ngram_spmm3t"
     if "ngram_spmm3_lds_kernel" in k:

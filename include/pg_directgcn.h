@@ -213,16 +213,21 @@ int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const f
 int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
                          uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
-/* N-gram MIDDLE-tile propagation (pg_ngram_mid.hip; replaces, on graphs over all K^n n-grams, the six propagate
- * calls of protgram_directgcn.py:101-112 like pg_spmm3_ngram_f32). A work item is one middle (n-2)-gram M and a
- * 16-feature column chunk: the K^2 out-sources M.b.c and K^2 in-sources c.a.M of the middle's K x K rows are staged
- * once in LDS (LDS-DMA, double-buffered, one persistent workgroup per CU), and a lane pair per row runs the 2K slot
- * steps from LDS. K = 20; F a multiple of 16; 16-B aligned rows; PG_ERR_UNSUPPORTED otherwise. Numerics as
- * pg_spmm3_ngram_f32 (fp32 FMA in slot order; X must be finite).
+/* N-gram MIDDLE-tile propagation on the fp32 matrix cores (pg_ngram_mid.hip; replaces, on graphs over all K^n
+ * n-grams, the six propagate calls of protgram_directgcn.py:101-112, like pg_spmm3_ngram_f32, and is the default
+ * forward there). The rows a.M.b of one middle (n-2)-gram M form a K x K grid; per 16-feature column chunk its K^2
+ * out-sources M.b.c, K^2 in-sources c.a.M and K^2 self rows are staged in LDS by LDS-DMA (loader waves, one phase
+ * ahead), and each adjacency becomes two dense (3K x K) x (K x 16) products per grid column / row on
+ * v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation), the out-part handed to the in-part through LDS.
+ * One persistent workgroup per CU walks a contiguous range of the (middle, chunk) stream; the weights of a middle
+ * (the plan, in MFMA fragment order) stay in registers across its chunks. K = 20; F a multiple of 16; 16-B aligned
+ * X, Z rows; PG_ERR_UNSUPPORTED otherwise (no launch). Numerics: the reference's w*x terms summed in another
+ * order: within fp32 rounding of it, not bit-exact; zero weights for missing transitions add 0*x, so X must be
+ * finite (PG_FLAG_NO_NGRAM selects the bit-exact CSR kernels).
  *   pg_ngram_mplan_floats: middle-plan size in floats for (K, n, n_rows = K^n), or -1 (K != 20, n < 2).
  *   pg_ngram_mplan_f32: scatters the CSR's weights into the middle plan (zeroed first); *bad as pg_ngram_plan_f32.
- *   pg_spmm3_ngram_mid_f32: Z = [A_in X | A_out X | A_und X]; gates != NULL applies the DirectGCN gates at the
- *     store (as pg_spmm3_gated_f32). */
+ *   pg_spmm3_ngram_mid_f32: Z = [A_in X | A_out X | A_und X]; gates must be NULL (PG_ERR_UNSUPPORTED otherwise:
+ *     the dense kernel applies the gates). */
 int64_t pg_ngram_mplan_floats(int K, int n, int64_t n_rows);
 int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, const pg_edge3_t* edges, float* plan,
                        int64_t plan_floats, int* bad, void* stream);

@@ -25,7 +25,8 @@
 //   out  [b][m][s][lane]  lane l holds A[i = 16 m + (l & 15)][c = 4 s + (l >> 4)] = Wout_k[a, b, c], (k, a) = divmod(i, K)
 //   in   [a][m][s][lane]  the same with (k, b) = divmod(i, K) and Win
 //   diag [a][b][k]
-// Rows i >= 3K are zero padding.
+// The padding rows i = 3K..3K+3 (60..63) repeat rows 56..59 (the compute waves' lanes of those rows then need no
+// branch: they write what the lanes of rows 56..59 write).
 //
 // Numerics: each aggregate is the same sum of w*x terms as the reference's propagate(), accumulated in fp32 (the
 // MFMA sums in groups of 4 c: out-slots, then the diagonal by a VALU FMA, then in-slots) in another order than the
@@ -74,22 +75,33 @@ struct XP {
     int nch;               // F / 16
     int chunks;            // K^(n-2) * nch: the (middle, chunk) stream, middle-major
     int remap;
+    int exp;               // diagnostics build only: timing experiments (bit 0: no Z stores, 1: no out/self DMA, 2: no in DMA)
     unsigned long long* stamps;  // diagnostics build only (PG_MID_STAMPS): s_memtime per block, chunk and point
 };
 
 #ifdef PG_MID_STAMPS
-constexpr int XSTAMP_CH = 32, XSTAMP_PT = 8;
+constexpr int XSTAMP_CH = 32, XSTAMP_PT = 8, XSTAMP_LAST = XSTAMP_CH - 1;  // chunk slots; the last: entry/exit
 #define XSTAMP(ci, pt)                                                                                              \
     do {                                                                                                            \
-        if (p.stamps && lane == 0 && (ci) < XSTAMP_CH)                                                              \
+        if (p.stamps && lane == 0 && ((ci) < XSTAMP_LAST || (pt) >= 5))                                                              \
             p.stamps[((int64_t)blockIdx.x * 2 + (wave >= XCW)) * XSTAMP_CH * XSTAMP_PT + (ci) * XSTAMP_PT + (pt)] = \
                 __builtin_amdgcn_s_memtime();                                                                       \
     } while (0)
+#define XEXP(bit) ((p.exp >> (bit)) & 1)
 #else
+#define XEXP(bit) 0
 #define XSTAMP(ci, pt) \
     do {               \
     } while (0)
 #endif
+
+// Hide a per-lane LDS offset from the optimiser: the per-tile compile-time parts then stay ds_read/ds_write
+// immediate offsets (< 64 KiB) instead of being folded with the region base into one constant per tile, each
+// needing its own register.
+__device__ __forceinline__ int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 __device__ __forceinline__ void glds16(const float* src, const void* lds_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
@@ -103,7 +115,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     extern __shared__ __attribute__((aligned(16))) char L[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    XSTAMP(0, 5);  // kernel entry
+    XSTAMP(XSTAMP_LAST, 5);  // kernel entry
     // This workgroup's share of the chunk stream: the contiguous range [g0, g1) of (middle, chunk) pairs in
     // middle-major order (ranges differ by at most one chunk: no tail of whole middles; the weights reload only where
     // the middle changes; neighbouring ranges, which share a middle, sit on the same XCD)
@@ -174,7 +186,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             dma_diag(c0.M);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        XSTAMP(0, 6);
+        XSTAMP(XSTAMP_LAST, 6);
         asm volatile("s_barrier" ::: "memory");  // S(-1)
         int ci = 0;
 #pragma unroll 1
@@ -184,21 +196,22 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             XSTAMP(ci, 0);
             asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done, partial written; out / self / diag free
             XSTAMP(ci, 1);
-            if (more) {
+            if (more && !XEXP(1)) {
                 dma_rows(LOUT, 0, nx.M, nx.ch);
                 dma_rows(LSELF, 2, nx.M, nx.ch);
                 if (nx.first) dma_diag(nx.M);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             XSTAMP(ci, 2);
-            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in / partial free
+            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in-region free
             XSTAMP(ci, 3);
-            if (more) dma_rows(LIN, 1, nx.M, nx.ch);
+            if (more && !XEXP(2)) dma_rows(LIN, 1, nx.M, nx.ch);
+            asm volatile("s_barrier" ::: "memory");  // W(t): chunk t's results have left the partial buffer
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             XSTAMP(ci, 4);
             ++ci;
         }
-        XSTAMP(0, 7);
+        XSTAMP(XSTAMP_LAST, 7);
         return;
     }
 
@@ -224,15 +237,16 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
 #pragma unroll
             for (int s = 0; s < XS; ++s) Ai[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
     };
-    // this lane's four accumulator rows i = 16 mw + 4 q4 + r: (k, a) in the out-phase, (k, b) in the in-phase
+    // this lane's four accumulator rows i = 16 mw + 4 q4 + r: (k, a) in the out-phase, (k, b) in the in-phase. The
+    // padding rows i = 60..63 repeat rows 56..59 (the plan holds their weights twice): their lanes compute the same
+    // values and write them to the same places as the lanes of rows 56..59, so no lane needs a branch
     int rk[4], rv[4];
-    bool rok[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const int i = 16 * mw + 4 * q4 + r;
-        rok[r] = i < 3 * XK;
-        rk[r] = rok[r] ? i / XK : 0;
-        rv[r] = rok[r] ? i - rk[r] * XK : 0;
+        int i = 16 * mw + 4 * q4 + r;
+        if (i >= 3 * XK) i -= 4;
+        rk[r] = i / XK;
+        rv[r] = i - rk[r] * XK;
     }
     // LDS byte offsets: sources [row][16 f] (64 B rows); partial [a][row k K + b][16 f]
     const int src_lane = (q4 * 16 + fl) * 4;                 // out: + (b * K + 4 s) * 64
@@ -241,50 +255,66 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         part_w[r] = LPART + ((rv[r] * 3 * XK + rk[r] * XK + wb) * 16 + fl) * 4;  // out: a = rv, row k K + b; + 2 j * 64
-        part_r[r] = LPART + ((wb * 3 * XK + 16 * mw + 4 * q4 + r) * 16 + fl) * 4;  // in: + 2 j * 60 * 64
+        part_r[r] = LPART + ((wb * 3 * XK + rk[r] * XK + rv[r]) * 16 + fl) * 4;   // in: + 2 j * 60 * 64
         self_r[r] = LSELF + ((rv[r] * XK + wb) * 16 + fl) * 4;                     // out: (a = rv, b); + 2 j * 64
         diag_r[r] = LDIAG + ((rv[r] * XK + wb) * 3 + rk[r]) * 4;                   // + 2 j * 12
+        part_w[r] = opaque(part_w[r]);
+        part_r[r] = opaque(part_r[r]);
+        self_r[r] = opaque(self_r[r]);
+        diag_r[r] = opaque(diag_r[r]);
     }
     // store-out of a finished in-phase tile: lane l writes 16 B = features 4 (l & 3) .. + 3 of tile row l >> 2
-    const int so_i = 16 * mw + (lane >> 2);
-    const bool so_ok = so_i < 3 * XK;
-    const int so_k = so_ok ? so_i / XK : 0, so_b = so_ok ? so_i - so_k * XK : 0;
-    const int so_lds = LPART + ((wb * 3 * XK + so_i) * 16 + 4 * (lane & 3)) * 4;  // + 2 j * 60 * 64
+    const int so_i = 16 * mw + (lane >> 2) - (16 * mw + (lane >> 2) >= 3 * XK ? 4 : 0);  // padding rows: as above
+    const int so_k = so_i / XK, so_b = so_i - so_k * XK;
+    const int so_lds = opaque(LPART + ((wb * 3 * XK + so_i) * 16 + 4 * (lane & 3)) * 4);  // + 2 j * 60 * 64
     const int64_t zstep = 2 * p.Kn1 * p.ldz;                                        // a -> a + 2
     if (g0 < g1) {
         load_Ao(chunk_at(g0).M);
         load_Ai(chunk_at(g0).M);
     }
     asm volatile("s_barrier" ::: "memory");  // S(-1)
-    XSTAMP(0, 6);
+    XSTAMP(XSTAMP_LAST, 6);
     int ci = 0;
 #pragma unroll 1
     for (int g = g0; g < g1; ++g) {
         const Chunk cu = chunk_at(g);
         XSTAMP(ci, 0);
         const bool next_mid = g + 1 < g1 && cu.ch + 1 == p.nch;  // the next chunk starts another middle
-        // ---- out-phase: tiles (b = 2 j + wb, m = mw); hand-over of row (k, a) to the in-phase row k K + b of a
+        // ---- out-phase: tiles (b = 2 j + wb, m = mw); hand-over of row (k, a) to the in-phase row k K + b of a.
+        // Software-pipelined over tile pairs: the B fragments of pair j + 2 are read while pair j's MFMAs run.
+        auto rd_out = [&](int j, float (&x)[2][XS]) {
+#pragma unroll
+            for (int s = 0; s < XS; ++s) {
+                x[0][s] = *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
+                x[1][s] = *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
+            }
+        };
+        float xo[2][2][XS];
+        rd_out(0, xo[0]);
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
+            float(&xc)[2][XS] = xo[(j >> 1) & 1];
+            if (j + 2 < XTPW) rd_out(j + 2, xo[((j >> 1) + 1) & 1]);
+            float w0[4], w1[4], s0[4], s1[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                w0[r] = *reinterpret_cast<const float*>(L + diag_r[r] + 2 * j * 12);
+                w1[r] = *reinterpret_cast<const float*>(L + diag_r[r] + (2 * j + 2) * 12);
+                s0[r] = *reinterpret_cast<const float*>(L + self_r[r] + 2 * j * 64);
+                s1[r] = *reinterpret_cast<const float*>(L + self_r[r] + (2 * j + 2) * 64);
+            }
+            asm volatile("" ::: "memory");  // the reads above are issued before the MFMAs below
             f4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
-                const float x0 = *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
-                const float x1 =
-                    *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j][s], x0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j + 1][s], x1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j][s], xc[0][s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j + 1][s], xc[1][s], acc1, 0, 0, 0);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (rok[r]) {  // + the diagonal term Wdiag_k[a, b] X[a.M.b, f]
-                    const float w0 = *reinterpret_cast<const float*>(L + diag_r[r] + 2 * j * 12);
-                    const float w1 = *reinterpret_cast<const float*>(L + diag_r[r] + (2 * j + 2) * 12);
-                    const float s0 = *reinterpret_cast<const float*>(L + self_r[r] + 2 * j * 64);
-                    const float s1 = *reinterpret_cast<const float*>(L + self_r[r] + (2 * j + 2) * 64);
-                    *reinterpret_cast<float*>(L + part_w[r] + 2 * j * 64) = __builtin_fmaf(w0, s0, acc0[r]);
-                    *reinterpret_cast<float*>(L + part_w[r] + (2 * j + 2) * 64) = __builtin_fmaf(w1, s1, acc1[r]);
-                }
+            for (int r = 0; r < 4; ++r) {  // + the diagonal term Wdiag_k[a, b] X[a.M.b, f]
+                *reinterpret_cast<float*>(L + part_w[r] + 2 * j * 64) = __builtin_fmaf(w0[r], s0[r], acc0[r]);
+                *reinterpret_cast<float*>(L + part_w[r] + (2 * j + 2) * 64) = __builtin_fmaf(w1[r], s1[r], acc1[r]);
+            }
             asm volatile("" ::: "memory");
         }
         if (next_mid) load_Ao(cu.M + 1);
@@ -296,45 +326,59 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         const int M = cu.M;
         float* zso = p.Z + ((int64_t)wb * p.Kn1 + (int64_t)M * XK + so_b) * p.ldz + (int64_t)so_k * p.F +
                      cu.ch * XFC + 4 * (lane & 3);
+        auto rd_in = [&](int j, float (&x)[2][XS]) {
+#pragma unroll
+            for (int s = 0; s < XS; ++s) {
+                x[0][s] = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
+                x[1][s] = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
+            }
+        };
+        float xi[2][2][XS];
+        rd_in(0, xi[0]);
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
+            float(&xc)[2][XS] = xi[(j >> 1) & 1];
             f4_t acc0, acc1;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 acc0[r] = *reinterpret_cast<const float*>(L + part_r[r] + 2 * j * 3 * XK * 64);
                 acc1[r] = *reinterpret_cast<const float*>(L + part_r[r] + (2 * j + 2) * 3 * XK * 64);
             }
+            if (j + 2 < XTPW) rd_in(j + 2, xi[((j >> 1) + 1) & 1]);
+            asm volatile("" ::: "memory");  // the reads above are issued before the MFMAs below
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
-                const float x0 = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
-                const float x1 =
-                    *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j][s], x0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j + 1][s], x1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j][s], xc[0][s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j + 1][s], xc[1][s], acc1, 0, 0, 0);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (rok[r]) {
-                    *reinterpret_cast<float*>(L + part_r[r] + 2 * j * 3 * XK * 64) = acc0[r];
-                    *reinterpret_cast<float*>(L + part_r[r] + (2 * j + 2) * 3 * XK * 64) = acc1[r];
-                }
-            // the wave's own tile rows: in-order LDS, no barrier (the empty asm keeps the compiler's order)
-            asm volatile("" ::: "memory");
-            const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
-            const f4_t v1 = *reinterpret_cast<const f4_t*>(L + so_lds + (2 * j + 2) * 3 * XK * 64);
-            if (so_ok) {
-                *reinterpret_cast<f4_t*>(zso + (int64_t)j * zstep) = v0;
-                *reinterpret_cast<f4_t*>(zso + (int64_t)(j + 1) * zstep) = v1;
+            for (int r = 0; r < 4; ++r) {
+                *reinterpret_cast<float*>(L + part_r[r] + 2 * j * 3 * XK * 64) = acc0[r];
+                *reinterpret_cast<float*>(L + part_r[r] + (2 * j + 2) * 3 * XK * 64) = acc1[r];
             }
             asm volatile("" ::: "memory");
         }
         XSTAMP(ci, 3);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // S(t)
         XSTAMP(ci, 4);
+        // ---- store-out of chunk t, in the next out-phase's shadow (the out/self DMA of the in-phase is done; only
+        // the smaller in-source DMA shares the CU's memory pipeline with these stores): every row of the partial
+        // buffer as 16-B pieces, then W(t) before the next out-phase overwrites it
+#pragma unroll
+        for (int j = 0; j < XTPW; j += 2) {
+            const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
+            const f4_t v1 = *reinterpret_cast<const f4_t*>(L + so_lds + (2 * j + 2) * 3 * XK * 64);
+            if (!XEXP(0)) {
+                *reinterpret_cast<f4_t*>(zso + (int64_t)j * zstep) = v0;
+                *reinterpret_cast<f4_t*>(zso + (int64_t)(j + 1) * zstep) = v1;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // W(t)
+        XSTAMP(ci, 5);
         ++ci;
         if (next_mid) load_Ai(cu.M + 1);
     }
-    XSTAMP(0, 7);
+    XSTAMP(XSTAMP_LAST, 7);
 }
 
 // Plan construction: one thread per CSR row scatters its entries into the fragment-ordered slots.
@@ -375,6 +419,7 @@ __global__ __launch_bounds__(256) void ngram_mplan_kernel(int64_t Kn1, int64_t n
                 const int m = rr >> 4, li = rr & 15;
                 const int s = c >> 2, lk = c & 3;
                 off = (type == 0 ? XPO : XPI) + ((int64_t)((grp * 4 + m) * XS + s) * 64 + lk * 16 + li);
+                if (rr >= 3 * K - 4) W[off + 4] = w3[k];  // rows 56..59 again as the padding rows 60..63
             }
             W[off] = w3[k];
         }
@@ -459,6 +504,7 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     p.chunks = (int)(Kn2 * p.nch);
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.stamps = stamps;
+    p.exp = stamps ? (int)((flags >> 24) & 15u) : 0;
     const int64_t cap = grid_cap();
     const unsigned grid = (unsigned)(p.chunks < cap ? p.chunks : cap);
     hipStream_t s = (hipStream_t)stream;

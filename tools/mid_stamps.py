@@ -55,7 +55,7 @@ ms = e0.elapsed_time(e1)
 ref = pkg.ops.spmm3(g, x, flags=pkg._lib.PG_FLAG_NO_NGRAM)
 print("max |d| vs csr", float((Z - ref).abs().max()))
 a = st.view(256, 2, CH, PT).cpu().numpy().astype(np.int64)
-names_c = ["start->outdone", "outdone->M", "M->indone", "indone->S"]
+names_c = ["start->outdone", "outdone->M", "M->indone", "indone->S", "S->stored+W"]
 names_l = ["(chunk)->M", "M->dmaout_done", "dmaout_done->S", "S->dmain_done"]
 for role, names in ((0, names_c), (1, names_l)):
     r = a[:, role]
@@ -74,11 +74,22 @@ r = a[:, 0]
 tot = r[:, 1:, 0] - r[:, :-1, 0]
 v = tot[(r[:, 1:, 0] > 0) & (r[:, :-1, 0] > 0)]
 print(f"compute chunk-to-chunk median {np.median(v):.0f} cycles; blocks x chunks = {int((r[:, :, 0] > 0).sum())}")
-# whole-kernel timeline (pt 5: entry, 6: after the first chunk's operands are in, 7: exit), compute wave 0
-c0 = a[:, 0, 0]
-t0 = a[:, :, 0, 5][a[:, :, 0, 5] > 0].min()
+# whole-kernel timeline (slot CH-1, pt 5: entry, 6: after the first chunk's operands are in, 7: exit), compute wave 0
+c0 = a[:, 0, CH - 1]
+t0 = a[:, :, CH - 1, 5][a[:, :, CH - 1, 5] > 0].min()
 ent, rdy, ext = c0[:, 5] - t0, c0[:, 6] - t0, c0[:, 7] - t0
-span = max(a[:, :, 0, 7].max() - t0, 1)
+span = max(a[:, :, CH - 1, 7].max() - t0, 1)
 print(f"kernel {ms * 1e3:.1f} us (events, incl. launch); stamp span {span} cycles -> {span / (ms * 1e3):.0f} cycles/us")
 for nm, v in (("entry", ent), ("first operands in", rdy), ("exit", ext), ("busy (exit - entry)", ext - ent)):
     print(f"  {nm:20s} min {v.min():8d} median {int(np.median(v)):8d} max {v.max():8d} cycles")
+nchunks = (a[:, 0, :CH - 1, 0] > 0).sum(1)
+busy = ext - ent
+for k in sorted(set(nchunks.tolist())):
+    sel = nchunks == k
+    print(f"  blocks with {k:2d} chunks: {int(sel.sum()):3d}, busy median {int(np.median(busy[sel]))} max {busy[sel].max()}")
+xcd = np.arange(a.shape[0]) % 8
+print("  busy median by XCD (blockIdx % 8):", [int(np.median(busy[xcd == i])) for i in range(8)])
+print("  first operands in by XCD:", [int(np.median(rdy[xcd == i] - ent[xcd == i])) for i in range(8)])
+per_chunk = np.diff(a[:, 0, :, 0], axis=1)
+ok = (a[:, 0, 1:, 0] > 0) & (a[:, 0, :-1, 0] > 0)
+print("  chunk median by XCD:", [int(np.median(per_chunk[(xcd == i)[:, None] & ok])) for i in range(8)])

@@ -8,11 +8,12 @@ identity residuals), C=20 classes, eval mode, fp32. One step = one full model fo
 decoder, log_softmax, L2-normalised embeddings), inputs resident in HBM.
   edges/s = 3 * nnz * L / t_step   (each adjacency entry counted once per layer)
 
---gpus N (torchrun, one process per GPU; "scaling": "strong": total work fixed). Default --partition halo:
-rank p owns a contiguous chunk of the graph's locality schedule and recomputes the 1-hop halo of its rows
-in layer 1 (shard.halo_partition): no collective on the data path, since the graph fits every GPU's HBM
-(the north star's RCCL halo exchange is for graphs that outgrow it). --partition exchange: node-range rows
-and an RCCL all-gather of the layer-1 output rows between the layers (shard.sharded_forward).
+--gpus N (torchrun, one process per GPU; "scaling": "strong": total work fixed). Default --partition middle (complete
+n-gram graphs, n >= 3): rank p owns the nodes a.M.b of a contiguous range of middle (n-2)-grams M and runs the
+middle-tile kernel over them; between the layers each rank receives exactly the ghost rows its middles read from
+their owners (one RCCL all_to_all_single; shard.middle_partition / middle_forward). --partition halo: each rank
+recomputes the 1-hop halo of its rows in layer 1 on the CSR kernels, no collective (shard.halo_partition).
+--partition exchange: node-range rows and an RCCL all-gather of all layer-1 rows (shard.sharded_forward).
 Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
 over ranks is reported. Rank 0 prints one JSON line.
 
@@ -41,6 +42,8 @@ def parse():
     # 0.846 ms at B(20,4)); the whole default run is still well under a second of GPU work
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--clock-warmup-s", type=float, default=1.0,
+                    help="untimed seconds of steps before the warm-up steps (clock ramp)")
     ap.add_argument("--ngram", type=int, default=4)
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--layers", type=int, default=2)
@@ -57,9 +60,11 @@ def parse():
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
     ap.add_argument("--chunks", type=int, default=4, help="N>1: layer-boundary all-gather in this many pieces, "
                     "overlapped with the compute (1 = one exchange after the layer)")
-    ap.add_argument("--partition", choices=("halo", "exchange"), default="halo",
-                    help="N>1: 'halo' = each rank recomputes the (L-1)-hop halo of its rows (no collective on the data "
-                    "path; the graph fits every GPU's HBM); 'exchange' = node-range rows + RCCL all-gather per layer")
+    ap.add_argument("--partition", choices=("middle", "halo", "exchange"), default="middle",
+                    help="N>1: 'middle' = middle (n-2)-gram ranges + RCCL ghost-row all_to_all per layer boundary "
+                    "(default; falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the "
+                    "(L-1)-hop halo of its rows (no collective on the data path); 'exchange' = node-range rows + RCCL "
+                    "all-gather of all rows per layer")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     ap.add_argument("--launch-check", action="store_true", help="N>1 plumbing check without a GPU: start the ranks, "
@@ -162,8 +167,16 @@ def main():
     else:
         data = pkg.Data(x=x, graph=g)
 
-    part = hp = None
-    if world > 1 and args.partition == "halo":
+    part = hp = mp = None
+    partition = args.partition
+    if world > 1 and partition == "middle" and (shard.ngram_shape(g) is None or shard.ngram_shape(g)[1] < 3):
+        partition = "halo"
+    if world > 1 and partition == "middle":
+        mp = shard.middle_partition(g, rank, world)
+        mid_in = shard.middle_inputs(model, mp)
+        log(f"[bench] middle partition: rank {rank} owns middles [{mp.m0}, {mp.m1}) = {mp.n_own} rows, receives "
+            f"{int(mp.recv_ids.numel())} ghost rows per layer boundary (N={N})")
+    elif world > 1 and partition == "halo":
         hp = shard.halo_partition(g, rank, world, L)
         halo_in = shard.halo_inputs(model, hp, x)  # this rank's resident inputs in its node order (setup)
         log(f"[bench] halo partition: rank 0 computes {hp.layer_rows} rows per layer (N={N})")
@@ -172,12 +185,22 @@ def main():
 
     def step():
         with torch.no_grad():
+            if mp is not None:
+                return shard.middle_forward(model, mp, x, mid_in)
             if hp is not None:
                 return shard.halo_forward(model, hp, halo_in)
             if part is None:
                 return model(data)
             return shard.sharded_forward(model, part, x, chunks=args.chunks)
 
+    # untimed clock ramp: the GPU's clocks take ~100 ms of load to settle (5 warm-up steps measured 0.915 ms/step,
+    # 50 or 200 gave 0.62): run steps for args.clock_warmup_s seconds before the W counted warm-up steps, so a short
+    # --warmup (the driver passes 5) does not time a cold GPU. Outside the timed region, like every warm-up step.
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < args.clock_warmup_s:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -208,7 +231,9 @@ def main():
     # each X row once, 3 output rows, gates): the floor of HBM traffic for one propagation launch
     el = 2 if args.bf16 else 4
     gated = (world == 1 or hp is not None) and ops.PREGATED_INFERENCE and not args.fused_norm and not args.bf16
-    if hp is not None:  # launches alternate over the layers' row prefixes: their mean
+    if mp is not None:
+        launch_graphs = [g]
+    elif hp is not None:  # launches alternate over the layers' row prefixes: their mean
         launch_graphs = hp.graphs
     elif part is None:
         launch_graphs = [g]
@@ -222,10 +247,21 @@ def main():
         kname = "pg_spmm3_fusednorm_f32"
     elif ngram:  # n-gram tile kernel; inference gates the aggregates at its store
         mid = all(gi.ngram.mplan is not None for gi in launch_graphs) and Fd % 16 == 0
+        gated = gated and not mid  # the middle-tile kernel stores ungated aggregates (the dense kernel gates)
         kname = ("pg_spmm3_ngram_mid_f32" if mid else "pg_spmm3_ngram_f32") + (" (gated)" if gated else "")
     else:
         kname = "pg_spmm3_gated_f32" if gated else "pg_spmm3_f32"
     comp = sum(gi.compulsory_bytes(Fd, elem=el, gated=gated) for gi in launch_graphs) // len(launch_graphs)
+    if mp is not None:  # a rank's launch: its middles' plan share, the rows they read once, its rows' aggregates
+        mid_launch = ngram and g.ngram.mplan is not None and Fd % 16 == 0 and not args.bf16
+        if mid_launch:
+            kname = "pg_spmm3_ngram_mid_rows_f32"
+            reads = shard._middle_reads(mp.K, mp.ngram, mp.m0, mp.m1, mp.own.device).numel()
+            comp = (g.ngram.mplan.numel() * 4 * (mp.m1 - mp.m0) // (N // mp.K ** 2) + reads * Fd * el
+                    + mp.n_own * 3 * Fd * el)
+        else:
+            kname = "pg_spmm3_bf16" if args.bf16 else "pg_spmm3_f32"
+            comp = mp.own_csr.compulsory_bytes(Fd, elem=el, gated=False)
     noreuse = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in launch_graphs) // len(launch_graphs)
     achieved = comp / (spmm_avg_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "kernel": kname,
@@ -268,8 +304,9 @@ def main():
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
                        "entry": ("trainer COO (edge_index_*/edge_weight_* -> csr_from_coo)" if entry == "coo"
                                  else "prebuilt Data.graph (build_propagation_csr)"),
-                       "parallelism": ("single" if world == 1 else f"halo_recompute_x{world}" if hp is not None
-                                       else f"node_range_x{world}"),
+                       "parallelism": ("single" if world == 1 else f"middle_ghost_a2a_x{world}" if mp is not None
+                                       else f"halo_recompute_x{world}" if hp is not None else f"node_range_x{world}"),
+                       "ghost_rows_rank0": int(mp.recv_ids.numel()) if mp is not None else None,
                        "exchange_chunks": args.chunks if part is not None else None,
                        "halo_rows_rank0": hp.layer_rows if hp is not None else None},
             "nodes_per_sec": round(N * L * args.steps / elapsed, 1),

@@ -233,6 +233,11 @@ int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, cons
                        int64_t plan_floats, int* bad, void* stream);
 int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                            const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream);
+/* The same kernel over the middles [m_begin, m_end) only (a rank's share in the middle partition, shard.py), X in
+ * the global row layout (only the rows those middles read must be valid: their out-sources M.b.c, in-sources c.a.M
+ * and own rows), Z in MIDDLE-MAJOR order: row (M - m_begin) K^2 + a K + b holds node a.M.b. */
+int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
+                                int64_t m_begin, int64_t m_end, float* Z, int64_t ldz, uint32_t flags, void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

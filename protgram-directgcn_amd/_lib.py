@@ -75,6 +75,8 @@ SIGNATURES = {
     "pg_ngram_mplan_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "pg_spmm3_ngram_mid_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,
                                               ctypes.POINTER(LayerArgs), c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3_ngram_mid_rows_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_i64,
+                                                   c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                            ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,

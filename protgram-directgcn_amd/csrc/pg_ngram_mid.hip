@@ -66,6 +66,8 @@ static_assert(XTILES % XCW == 0 && XTPW % 2 == 0, "tiles per wave");
 
 struct XP {
     int64_t Kn1, Kn2;      // K^(n-1), K^(n-2) (= number of middles)
+    int64_t m0;            // first middle of the launch (the chunk stream covers middles m0 .. m0 + chunks / nch - 1)
+    int64_t zsa, zsm;      // Z row of a.M.b = a zsa + (M - m0) zsm + b: (K^(n-1), K) global, (K, K^2) middle-major
     const float* plan;
     const float* X;
     int64_t ldx;
@@ -122,9 +124,9 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
     const int g0 = (int)(lb * p.chunks / gridDim.x), g1 = (int)((lb + 1) * p.chunks / gridDim.x);
     auto chunk_at = [&](int g) -> Chunk {
-        const int M = g / p.nch;
-        const int ch = g - M * p.nch;
-        return Chunk{M, ch, g == g0 || ch == 0};
+        const int Mr = g / p.nch;
+        const int ch = g - Mr * p.nch;
+        return Chunk{(int)p.m0 + Mr, ch, g == g0 || ch == 0};
     };
 
     if (wave >= XCW) {  // ---------------- loader waves: LDS-DMA only (same barrier sequence as the compute waves)
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     const int so_i = 16 * mw + (lane >> 2) - (16 * mw + (lane >> 2) >= 3 * XK ? 4 : 0);  // padding rows: as above
     const int so_k = so_i / XK, so_b = so_i - so_k * XK;
     const int so_lds = opaque(LPART + ((wb * 3 * XK + so_i) * 16 + 4 * (lane & 3)) * 4);  // + 2 j * 60 * 64
-    const int64_t zstep = 2 * p.Kn1 * p.ldz;                                        // a -> a + 2
+    const int64_t zstep = 2 * p.zsa * p.ldz;                                        // a -> a + 2
     if (g0 < g1) {
         load_Ao(chunk_at(g0).M);
         load_Ai(chunk_at(g0).M);
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
         // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
-        float* zso = p.Z + ((int64_t)wb * p.Kn1 + (int64_t)M * XK + so_b) * p.ldz + (int64_t)so_k * p.F +
+        float* zso = p.Z + ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz + (int64_t)so_k * p.F +
                      cu.ch * XFC + 4 * (lane & 3);
         auto rd_in = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
@@ -478,10 +480,14 @@ int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, cons
 }
 
 static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
-                      const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, unsigned long long* stamps,
-                      void* stream) {
+                      int64_t m_begin, int64_t m_end, bool middle_major, const pg_layer_args_t* gates, float* Z,
+                      int64_t ldz, uint32_t flags, unsigned long long* stamps, void* stream) {
     int64_t Kn1 = 0, Kn2 = 0;
     PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
+    if (m_end < 0) m_end = Kn2;
+    PG_REQUIRE(0 <= m_begin && m_begin <= m_end && m_end <= Kn2, "middle range [%lld, %lld) outside [0, %lld)",
+               (long long)m_begin, (long long)m_end, (long long)Kn2);
+    if (m_begin == m_end) return PG_OK;
     PG_REQUIRE(plan && X && Z, "null pointer");
     PG_REQUIRE(ldz >= 3 * F && ldx >= F, "leading dimensions too small");
     if (gates)
@@ -494,6 +500,9 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     XP p{};
     p.Kn1 = Kn1;
     p.Kn2 = Kn2;
+    p.m0 = m_begin;
+    p.zsa = middle_major ? XK : Kn1;
+    p.zsm = middle_major ? XR : XK;
     p.plan = plan;
     p.X = X;
     p.ldx = ldx;
@@ -501,7 +510,7 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     p.ldz = ldz;
     p.F = (int)F;
     p.nch = (int)(F / XFC);
-    p.chunks = (int)(Kn2 * p.nch);
+    p.chunks = (int)((m_end - m_begin) * p.nch);
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.stamps = stamps;
     p.exp = stamps ? (int)((flags >> 24) & 15u) : 0;
@@ -521,14 +530,19 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
 
 int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                            const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream) {
-    return mid_launch(K, n, n_rows, plan, X, ldx, F, gates, Z, ldz, flags, nullptr, stream);
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, gates, Z, ldz, flags, nullptr, stream);
+}
+
+int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
+                                int64_t m_begin, int64_t m_end, float* Z, int64_t ldz, uint32_t flags, void* stream) {
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, m_begin, m_end, true, nullptr, Z, ldz, flags, nullptr, stream);
 }
 
 #ifdef PG_MID_STAMPS
 // diagnostics library only (tools/mid_stamps.py): the same launch with per-block time stamps
 int pg_mid_stamped(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F, float* Z,
                    int64_t ldz, uint32_t flags, unsigned long long* stamps, void* stream) {
-    return mid_launch(K, n, n_rows, plan, X, ldx, F, nullptr, Z, ldz, flags, stamps, stream);
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, stamps, stream);
 }
 #endif
 }  // extern "C"

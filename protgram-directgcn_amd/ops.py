@@ -160,6 +160,32 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
     return Z
 
 
+def spmm3_middles(g: CSRGraph, x: torch.Tensor, m_begin: int, m_end: int, flags: Optional[int] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """pg_spmm3_ngram_mid_rows_f32: Z = [A_in x | A_out x | A_und x] for the nodes a.M.b of the middles
+    M in [m_begin, m_end) only, in middle-major order (row (M - m_begin) K^2 + a K + b), x in the global row layout
+    (only the rows those middles read need be valid). The middle partition's per-rank propagation (shard.py).
+    Needs g.ngram with a middle plan and fp32 x with F % 16 == 0: raises otherwise (callers check `_mid_ok`)."""
+    lib = load_library()
+    x = _f32c(x)
+    _require_gpu(x)
+    _require_graph_on(g, x)
+    fl = default_flags() if flags is None else flags
+    if not _mid_ok(g, x, fl):
+        raise ValueError("spmm3_middles needs a graph with a middle plan and fp32 x with F % 16 == 0")
+    ng, N, F = g.ngram, g.n_rows, x.size(1)
+    K2 = ng.K * ng.K
+    rows = (m_end - m_begin) * K2
+    Z = out if out is not None else torch.empty(rows, 3 * F, device=x.device, dtype=torch.float32)
+    if Z.shape != (rows, 3 * F) or Z.stride(1) != 1:
+        raise ValueError("out must be [(m_end - m_begin) K^2, 3F] with unit column stride")
+    ev = _ev_start(x)
+    check(lib.pg_spmm3_ngram_mid_rows_f32(ng.K, ng.n, N, _p(ng.mplan), _p(x), x.stride(0), F, m_begin, m_end, _p(Z),
+                                          Z.stride(0), fl, _stream(x)), "pg_spmm3_ngram_mid_rows_f32")
+    _ev_end(x, ev)
+    return Z
+
+
 def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
     x = _bf16c(x)
     _require_gpu(x)

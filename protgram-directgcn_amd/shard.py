@@ -611,3 +611,202 @@ def halo_forward(model, hp: HaloPartition, inputs) -> tuple:
             Z = ops.spmm3(g, h)
             h = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=h[:R], W_res=W_res, b_res=b_res, act=True)
     return model.head(h)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Middle partition with a ghost-row exchange (complete n-gram graphs: every K^n n-gram a node, the middle plan
+# attached). Rank p owns the nodes a.M.b of a contiguous range of middle (n-2)-grams M in [m0, m1): exactly the
+# work units of the middle-tile kernel, so each rank runs pg_spmm3_ngram_mid_rows_f32 over its middles -- the same
+# kernel and the same per-row sums as one GPU -- and its rows are bit-identical to the single-GPU forward's. A row
+# a.M.b reads only M.b.c (out), c.a.M (in) and itself, so the rows a rank's middles read are a fixed set: its own
+# rows plus the ghost rows other ranks own. Layer 1 reads the replicated input. After each other layer, every rank
+# sends each other rank exactly the rows of its output that rank reads (one RCCL all_to_all_single, the
+# personalised all-gather of the halo rows; ~(1-(1-1/P)^3) N rows received in total at P ranks instead of the
+# (P-1)/P N of the node-range all-gather) and scatters what it receives into a global-layout buffer.
+# ---------------------------------------------------------------------------------------------------------------
+@dataclass
+class MiddlePartition:
+    rank: int
+    world: int
+    n: int                      # N = K^ngram
+    K: int
+    ngram: int
+    m0: int                     # owned middles [m0, m1)
+    m1: int
+    own: torch.Tensor           # int64 [n_own]: global ids of the owned rows, middle-major ((M - m0) K^2 + a K + b)
+    own_csr: CSRGraph           # the global CSR's rows `own` (global column ids): the CSR-kernel path
+    send_pos: torch.Tensor      # int64: positions (in the owned-row order) of the rows sent, grouped by destination
+    send_counts: List[int]
+    recv_ids: torch.Tensor      # int64: global ids of the rows received, grouped by source rank (ascending ids)
+    recv_counts: List[int]
+    graph: CSRGraph             # the global graph (its middle plan)
+    cache: dict = field(default_factory=dict)
+
+    @property
+    def n_own(self) -> int:
+        return int(self.own.numel())
+
+    @property
+    def global_rows(self) -> torch.Tensor:
+        """Global ids of the rows this rank outputs (in its output order)."""
+        return self.own
+
+
+def ngram_shape(g: CSRGraph):
+    """(K, n) of a graph over all K^n n-grams (the tile plan's, else K = 20 when n_rows is a power of 20), or None."""
+    if g.ngram is not None:
+        return g.ngram.K, g.ngram.n
+    N, n, v = g.n_rows, 0, 1
+    while v < N:
+        v *= 20
+        n += 1
+    return (20, n) if v == N and n >= 1 else None
+
+
+def middle_bounds(n_middles: int, world: int) -> List[tuple]:
+    """Balanced contiguous middle ranges, one per rank."""
+    return [(r * n_middles // world, (r + 1) * n_middles // world) for r in range(world)]
+
+
+def _middle_rows(K: int, n: int, m0: int, m1: int, dev) -> torch.Tensor:
+    """Global ids a.M.b for M in [m0, m1), middle-major ((M, a, b) order)."""
+    Kn1 = K ** (n - 1)
+    M = torch.arange(m0, m1, dtype=torch.int64, device=dev)
+    a = torch.arange(K, dtype=torch.int64, device=dev)
+    return (a.view(1, K, 1) * Kn1 + M.view(-1, 1, 1) * K + a.view(1, 1, K)).reshape(-1)
+
+
+def _middle_reads(K: int, n: int, m0: int, m1: int, dev) -> torch.Tensor:
+    """Sorted global ids of every row the middles [m0, m1) read: M.b.c, c.a.M and a.M.b."""
+    Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
+    M = torch.arange(m0, m1, dtype=torch.int64, device=dev)
+    t = torch.arange(K * K, dtype=torch.int64, device=dev)
+    c = torch.arange(K, dtype=torch.int64, device=dev)
+    out_src = (M.view(-1, 1) * (K * K) + t.view(1, -1)).reshape(-1)
+    in_src = (c.view(K, 1, 1) * Kn1 + c.view(1, K, 1) * Kn2 + M.view(1, 1, -1)).reshape(-1)
+    return torch.unique(torch.cat([out_src, in_src, _middle_rows(K, n, m0, m1, dev)]))
+
+
+def middle_partition(g: CSRGraph, rank: int, world: int) -> MiddlePartition:
+    """This rank's middle partition of a complete n-gram graph (see the section comment). Setup work, once per
+    graph: the exchange lists of every rank pair are built from the closed-form read sets (and checked against
+    the CSR's own columns), so both ends of each pair agree without communication."""
+    shape = ngram_shape(g)
+    if shape is None or not g.shared:
+        raise NotImplementedError("middle partition needs a shared-pattern graph over all K^n n-grams")
+    K, n = shape
+    if n < 3:
+        raise NotImplementedError("middle partition needs n >= 3 (one middle per (n-2)-gram)")
+    Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
+    if world > Kn2:
+        raise ValueError(f"{world} ranks but only {Kn2} middles")
+    dev = g.rowptr.device
+    bounds = middle_bounds(Kn2, world)
+    starts = torch.tensor([b[0] for b in bounds], dtype=torch.int64, device=dev)
+    m0, m1 = bounds[rank]
+
+    def owner_and_pos(x):
+        Mx = (x % Kn1) // K
+        q = torch.searchsorted(starts, Mx, right=True) - 1
+        pos = (Mx - starts[q]) * (K * K) + (x // Kn1) * K + x % K
+        return q, pos
+
+    own = _middle_rows(K, n, m0, m1, dev)
+    send_pos, send_counts, recv_ids, recv_counts = [], [0] * world, None, [0] * world
+    for p in range(world):
+        reads = _middle_reads(K, n, *bounds[p], dev)
+        q, pos = owner_and_pos(reads)
+        if p == rank:
+            ghost = q != rank
+            gq, gid = q[ghost], reads[ghost]
+            order = torch.sort(gq, stable=True).indices  # by source rank, ascending ids within
+            recv_ids = gid[order]
+            recv_counts = torch.bincount(gq, minlength=world).tolist()
+        else:
+            mine = q == rank
+            send_pos.append(pos[mine])
+            send_counts[p] = int(mine.sum())
+    send_pos = torch.cat(send_pos) if send_pos else torch.zeros(0, dtype=torch.int64, device=dev)
+    # the owned rows' CSR (global column ids), and the check that it reads nothing outside the closed-form set
+    rp = g.rowptr
+    cnt = rp[own + 1] - rp[own]
+    lrp = torch.zeros(own.numel() + 1, dtype=torch.int64, device=dev)
+    lrp[1:] = torch.cumsum(cnt, 0)
+    tot = int(lrp[-1])
+    src = (torch.arange(tot, dtype=torch.int64, device=dev) - torch.repeat_interleave(lrp[:-1], cnt)
+           + torch.repeat_interleave(rp[own], cnt))
+    e = take(g.edges3, src)
+    reads = _middle_reads(K, n, m0, m1, dev)
+    if tot and not bool(torch.isin(e[:, 0].to(torch.int64), reads).all()):
+        raise ValueError("the graph has entries outside the n-gram out/in/self slots: not a middle-partitionable graph")
+    own_csr = CSRGraph(n_rows=own.numel(), shared=True, rowptr=lrp, edges3=e, symmetric=False, nnz=tot,
+                       row_order=None, n_cols=g.n_rows)
+    return MiddlePartition(rank, world, g.n_rows, K, n, m0, m1, own, own_csr, send_pos, send_counts, recv_ids,
+                           recv_counts, g)
+
+
+@torch.no_grad()
+def middle_inputs(model, mp: MiddlePartition):
+    """Per layer, the per-node parameters (gates, constant) at the owned rows, in the owned-row order. Built once per
+    parameter set (rebuild after the parameters change), like halo_inputs."""
+    layers = []
+    for conv in model.convs:
+        prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+        if conv.use_vector_coeffs:
+            rows = mp.own.to(conv.constant.device)
+            for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+                prm[k] = prm[k].index_select(0, rows).contiguous()
+            const = conv.constant.detach().index_select(0, rows).contiguous()
+        else:
+            const = None
+        layers.append((prm, const))
+    return layers
+
+
+def _owned_spmm3(mp: MiddlePartition, X: torch.Tensor) -> torch.Tensor:
+    """Aggregates of the owned rows (owned-row order) from X in the global row layout: the middle-tile kernel over
+    the owned middles where it takes the call (fp32, F % 16 == 0), else the CSR kernels over the owned rows' CSR."""
+    if mp.graph.ngram is not None and ops._mid_ok(mp.graph, X, ops.default_flags()):
+        return ops.spmm3_middles(mp.graph, X, mp.m0, mp.m1)
+    return ops.spmm3(mp.own_csr, X)
+
+
+def _exchange_rows(mp: MiddlePartition, h_own: torch.Tensor, group=None) -> torch.Tensor:
+    """The next layer's input in the global row layout: this rank's rows plus the ghost rows it reads, received
+    from their owners by one all_to_all_single (the same tensor collective on RCCL and on gloo). Rows nobody
+    reads stay unwritten."""
+    F_ = h_own.size(1)
+    X = h_own.new_empty(mp.n, F_)
+    X.index_copy_(0, mp.own, h_own)
+    if mp.world > 1:
+        send = take(h_own, mp.send_pos)
+        stage = h_own.is_cuda and dist.get_backend(group) == "gloo"  # gloo (CPU rehearsal backend): host buffers
+        if stage:
+            send = send.cpu()
+        recv = send.new_empty(int(mp.recv_ids.numel()), F_)
+        dist.all_to_all_single(recv, send, mp.recv_counts, mp.send_counts, group=group)
+        X.index_copy_(0, mp.recv_ids, recv.to(X.device) if stage else recv)
+    return X
+
+
+@torch.no_grad()
+def middle_forward(model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None, group=None) -> tuple:
+    """ProtGramDirectGCN.forward (eval) for this rank's rows; returns (log_probs, emb) for the rows mp.global_rows,
+    in that order. `inputs` = middle_inputs(model, mp) (built here when None)."""
+    layers = inputs if inputs is not None else middle_inputs(model, mp)
+    if len(layers) != len(model.convs):
+        raise ValueError("middle inputs were built for a different number of layers")
+    h = model._apply_pe(x_full)
+    if model.compute_dtype == torch.bfloat16:
+        h = h.to(torch.bfloat16)
+    X, res_x = h, take(h, mp.own)
+    L = len(model.convs)
+    for i, (conv, res, (prm, const)) in enumerate(zip(model.convs, model.res_projs, layers)):
+        gate_mode = 0 if conv.use_vector_coeffs else 1
+        W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
+        Z = _owned_spmm3(mp, X)
+        h_own = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=res_x, W_res=W_res, b_res=b_res, act=True)
+        if i + 1 < L:
+            X = _exchange_rows(mp, h_own, group)
+        res_x = h_own
+    return model.head(h_own)

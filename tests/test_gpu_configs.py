@@ -366,6 +366,70 @@ def test_config4_5gram_exchange_partition_bitexact(pkg, cuda, five_gram, rank, m
     assert torch.equal(lp, lp_ref[part.r0:part.r1]) and torch.equal(emb, emb_ref[part.r0:part.r1])
 
 
+def _middle_rank_check(pkg, m, g, xd, lp_ref, emb_ref, rank, world, monkeypatch):
+    """One rank of the middle partition (shard.middle_forward) on this GPU, the ghost-row exchange replaced by a
+    copy from the single-GPU layer-1 output into a NaN-filled buffer (so a read outside the rank's own + ghost
+    rows would show): its layer-1 rows and its outputs must equal the single-GPU forward's bit for bit (the same
+    middle-tile kernel over the rank's middles, the same dense kernel on its rows)."""
+    from protgram_directgcn_amd import ops, shard
+    conv = m.convs[0]
+    vec = conv.use_vector_coeffs
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    with torch.no_grad():
+        h0 = m._apply_pe(xd)
+        h1 = ops.layer_dense(ops.spmm3(g, h0), prm, 0 if vec else 1,
+                             constant=conv.constant.detach() if vec else None, res_x=h0, act=True)
+    mp = shard.middle_partition(g, rank, world)
+    calls, own_ok = [0], []
+
+    def fake_exchange(mp_, h_own, group=None):
+        calls[0] += 1
+        own_ok.append(torch.equal(h_own, h1[mp_.own]))
+        X = torch.full_like(h1, float("nan"))
+        X[mp_.own] = h_own
+        X[mp_.recv_ids] = h1[mp_.recv_ids]
+        return X
+
+    hits = []
+    real = ops.spmm3_middles
+    with monkeypatch.context() as mpc:
+        mpc.setattr(shard, "_exchange_rows", fake_exchange)
+        mpc.setattr(ops, "spmm3_middles", lambda *a, **k: hits.append(1) or real(*a, **k))
+        lp, emb = shard.middle_forward(m, mp, xd)
+    assert calls[0] == len(m.convs) - 1 and own_ok and all(own_ok)
+    assert len(hits) == len(m.convs)  # every layer on the middle-tile kernel
+    rows = mp.global_rows
+    assert torch.equal(lp, lp_ref[rows]) and torch.equal(emb, emb_ref[rows])
+    return mp
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("rank", [0, 7])
+def test_config4_5gram_middle_partition_bitexact(pkg, cuda, five_gram, rank, monkeypatch):
+    """The middle partition (bench.py --gpus N's default multi-GPU forward) at 5-gram, ranks 0 and 7 of P = 8."""
+    f = five_gram
+    mp = _middle_rank_check(pkg, f["m"], f["g"], f["xd"], f["lp"], f["emb"], rank, 8, monkeypatch)
+    assert mp.n_own == f["N"] // 8
+    assert mp.recv_ids.numel() < 0.35 * f["N"]  # ghost rows: about a third of N at P = 8
+
+
+@pytest.mark.timeout(600)
+def test_middle_partition_4gram_every_rank_bitexact(pkg, cuda, monkeypatch):
+    """The same for every rank of P = 8 at 4-gram (the bench graph); together the ranks' rows tile the graph."""
+    n, F = 4, 128
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    m = _model(pkg, [F, F, F], N, n).to(cuda).eval()
+    xd = torch.randn(N, F, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    with torch.no_grad():
+        lp, emb = m(pkg.Data(x=xd, graph=g))
+    seen = torch.zeros(N, dtype=torch.int64, device=cuda)
+    for rank in range(8):
+        mp = _middle_rank_check(pkg, m, g, xd, lp, emb, rank, 8, monkeypatch)
+        seen[mp.own] += 1
+    assert bool((seen == 1).all())
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # config 5
 # ---------------------------------------------------------------------------------------------------------------

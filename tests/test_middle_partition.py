@@ -1,0 +1,125 @@
+"""The middle partition with its ghost-row exchange (shard.middle_partition / middle_forward), on the CPU:
+  * structure: the ranks' owned rows tile the graph; what rank q sends rank p is exactly what p receives from q, in
+    the same order; a rank's own rows plus the ghost rows it receives are exactly the rows its middles read;
+  * the forward at world sizes 2 and 3 with gloo (the product's all_to_all_single) against the single-process
+    oracle, with CPU stand-ins for the HIP kernels (the product has no CPU path)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _graph(pkg, n):
+    from oracle import graph_cpu as og
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    m = og.build_matrices(N, s, d, c)
+    return N, m, pkg.graph.csr_from_coo(N, *m["in"], *m["out"], *m["und"], cache=False)
+
+
+@pytest.mark.parametrize("n,world", [(3, 1), (3, 2), (3, 3), (3, 8), (4, 8)])
+def test_middle_partition_structure(pkg, n, world):
+    from protgram_directgcn_amd import shard
+    N, _, g = _graph(pkg, n)
+    parts = [shard.middle_partition(g, r, world) for r in range(world)]
+    owned = torch.cat([p.own for p in parts])
+    assert torch.equal(torch.sort(owned).values, torch.arange(N))
+    K = 20
+    for p in parts:
+        assert p.n_own == (p.m1 - p.m0) * K * K
+        assert p.send_counts[p.rank] == 0 and p.recv_counts[p.rank] == 0
+        assert sum(p.send_counts) == p.send_pos.numel() and sum(p.recv_counts) == p.recv_ids.numel()
+        reads = shard._middle_reads(K, n, p.m0, p.m1, torch.device("cpu"))
+        got = torch.sort(torch.cat([p.own, p.recv_ids])).values
+        assert torch.equal(got, reads)  # own rows + ghosts == the rows its middles read, each once
+        cols = torch.unique(p.own_csr.edges3[:, 0].long())
+        assert bool(torch.isin(cols, reads).all())
+    for q in parts:  # q -> p: q's send list (as global ids) == p's receive list from q
+        off_s = [0]
+        for c in q.send_counts:
+            off_s.append(off_s[-1] + c)
+        for p in parts:
+            if p.rank == q.rank:
+                continue
+            sent = q.own[q.send_pos[off_s[p.rank]:off_s[p.rank + 1]]]
+            off_r = sum(p.recv_counts[:q.rank])
+            assert torch.equal(sent, p.recv_ids[off_r:off_r + p.recv_counts[q.rank]]), (q.rank, p.rank)
+    if world == 8 and n == 4:  # ghost rows received per rank: well below the (P-1)/P N of a node-range all-gather
+        assert max(p.recv_ids.numel() for p in parts) < 0.5 * N
+
+
+def test_middle_partition_rejects_other_graphs(pkg):
+    from protgram_directgcn_amd import shard
+    _, _, g2 = _graph(pkg, 2)
+    with pytest.raises(NotImplementedError):
+        shard.middle_partition(g2, 0, 2)  # a single middle
+    from oracle import graph_cpu as og
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    s, d = s.copy(), d.copy()
+    d[0] = (s[0] + 4210) % N  # 0 -> 4210 = 10.10.10: not a row that middles 0..9 (rank 0) read
+    m = og.build_matrices(N, s, d, c)
+    g = pkg.graph.csr_from_coo(N, *m["in"], *m["out"], *m["und"], cache=False)
+    with pytest.raises(ValueError):
+        shard.middle_partition(g, 0, 2)
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard
+    from oracle import directgcn_cpu as oc
+    from test_shard_gloo import _cpu_layer_dense, _cpu_spmm3
+    ops.spmm3 = _cpu_spmm3
+    ops.layer_dense = _cpu_layer_dense
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, m, g = _graph(pkg, 3)
+        dims = [16, 16, 12, 12]
+        torch.manual_seed(0)
+        model = pkg.ProtGramDirectGCN(dims, N, 5, 3, 0, 512, 0.5, True).eval()
+        with torch.no_grad():
+            for name, p in model.named_parameters():
+                if name.split(".")[-1].startswith("C_"):
+                    p.uniform_(0.5, 1.5)
+        x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
+        mp_ = shard.middle_partition(g, rank, world)
+        p = {k: v.detach() for k, v in model.state_dict().items()}
+        lp_r, emb_r = oc.model_forward(p, dims, x, *m["in"], *m["out"], *m["und"], n_gram_len=3)
+        lp, emb = shard.middle_forward(model, mp_, x)
+        rows = mp_.global_rows
+        ok = (torch.allclose(lp, lp_r[rows], rtol=1e-5, atol=1e-5)
+              and torch.allclose(emb, emb_r[rows], rtol=1e-5, atol=1e-5))
+        out_q.put((rank, int(rows.numel()), bool(ok), float((lp - lp_r[rows]).abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_middle_forward_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=280) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert sum(r[1] for r in res) == 8000
+    assert all(r[2] for r in res), res

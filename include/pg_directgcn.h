@@ -80,6 +80,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */
 #define PG_FLAG_NGRAM_BLOCK4 (1u << 21)   /* host-side: the 4x4-block n-gram forward (pg_spmm3_ngram_f32) instead of the
                                              middle-tile kernel (pg_spmm3_ngram_mid_f32) */
+#define PG_FLAG_MID_NO_PAIRS (1u << 22)   /* middle-tile kernel: no workgroup pairs on odd / even feature chunks
+                                             (each workgroup walks all chunks of its middles) */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes

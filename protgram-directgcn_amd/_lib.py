@@ -21,6 +21,7 @@ PG_FLAG_DENSE_TILED = 1 << 15
 PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_NO_NGRAM = 1 << 20
 PG_FLAG_NGRAM_BLOCK4 = 1 << 21
+PG_FLAG_MID_NO_PAIRS = 1 << 22
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 

@@ -75,7 +75,8 @@ struct XP {
     int64_t ldz;
     int F;
     int nch;               // F / 16
-    int chunks;            // K^(n-2) * nch: the (middle, chunk) stream, middle-major
+    int chunks;            // length of the (middle, chunk) stream a workgroup pair / workgroup walks, middle-major
+    int cstride;           // 2: workgroup pairs split each middle's chunks odd / even (see the kernel); 1: no pairs
     int remap;
     int exp;               // diagnostics build only: timing experiments (bit 0: no Z stores, 1: no out/self DMA, 2: no in DMA)
     unsigned long long* stamps;  // diagnostics build only (PG_MID_STAMPS): s_memtime per block, chunk and point
@@ -118,15 +119,22 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     XSTAMP(XSTAMP_LAST, 5);  // kernel entry
-    // This workgroup's share of the chunk stream: the contiguous range [g0, g1) of (middle, chunk) pairs in
-    // middle-major order (ranges differ by at most one chunk: no tail of whole middles; the weights reload only where
-    // the middle changes; neighbouring ranges, which share a middle, sit on the same XCD)
+    // This workgroup's share of the chunk stream: a contiguous range [g0, g1) of it in middle-major order (ranges
+    // differ by at most one step: no tail of whole middles; the weights reload only where the middle changes;
+    // neighbouring ranges, which share a middle, sit on the same XCD). With cstride 2, the two workgroups of a pair
+    // (logical blocks 2i, 2i + 1: same XCD) walk the same range, one the even and one the odd 16-feature chunks of
+    // each middle, in step: a 64-B row piece is half of a 128-B line, and the partner's read of the other half,
+    // issued at about the same time, hits in L2 (alone, each half-line read fetched the whole line from HBM: 2x the
+    // X bytes), and the partners' 64-B stores of one line merge in L2 before it is written back.
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
-    const int g0 = (int)(lb * p.chunks / gridDim.x), g1 = (int)((lb + 1) * p.chunks / gridDim.x);
+    const int half = p.cstride == 2 ? (int)(lb & 1) : 0;
+    const int64_t lu = p.cstride == 2 ? lb >> 1 : lb, nu = p.cstride == 2 ? gridDim.x >> 1 : gridDim.x;
+    const int g0 = (int)(lu * p.chunks / nu), g1 = (int)((lu + 1) * p.chunks / nu);
+    const int nchu = p.nch / p.cstride;  // chunks of one middle in a workgroup's stream
     auto chunk_at = [&](int g) -> Chunk {
-        const int Mr = g / p.nch;
-        const int ch = g - Mr * p.nch;
-        return Chunk{(int)p.m0 + Mr, ch, g == g0 || ch == 0};
+        const int Mr = g / nchu;
+        const int j = g - Mr * nchu;
+        return Chunk{(int)p.m0 + Mr, j * p.cstride + half, g == g0 || j == 0};
     };
 
     if (wave >= XCW) {  // ---------------- loader waves: LDS-DMA only (same barrier sequence as the compute waves)
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     for (int g = g0; g < g1; ++g) {
         const Chunk cu = chunk_at(g);
         XSTAMP(ci, 0);
-        const bool next_mid = g + 1 < g1 && cu.ch + 1 == p.nch;  // the next chunk starts another middle
+        const bool next_mid = g + 1 < g1 && (g + 1) % nchu == 0;  // the next chunk starts another middle
         // ---- out-phase: tiles (b = 2 j + wb, m = mw); hand-over of row (k, a) to the in-phase row k K + b of a.
         // Software-pipelined over tile pairs: the B fragments of pair j + 2 are read while pair j's MFMAs run.
         auto rd_out = [&](int j, float (&x)[2][XS]) {
@@ -510,12 +518,17 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     p.ldz = ldz;
     p.F = (int)F;
     p.nch = (int)(F / XFC);
-    p.chunks = (int)((m_end - m_begin) * p.nch);
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    const int64_t cap = grid_cap();
+    const int64_t total = (m_end - m_begin) * p.nch;
+    // workgroup pairs on odd / even chunks (even chunk count, an even grid, and the XCD-contiguous block order that
+    // keeps a pair on one XCD)
+    p.cstride = (p.nch % 2 == 0 && p.remap && total >= 2 && !(flags & PG_FLAG_MID_NO_PAIRS)) ? 2 : 1;
+    p.chunks = (int)(total / p.cstride);
     p.stamps = stamps;
     p.exp = stamps ? (int)((flags >> 24) & 15u) : 0;
-    const int64_t cap = grid_cap();
-    const unsigned grid = (unsigned)(p.chunks < cap ? p.chunks : cap);
+    unsigned grid = (unsigned)(total < cap ? total : cap);
+    if (p.cstride == 2) grid &= ~1u;
     hipStream_t s = (hipStream_t)stream;
     static bool attr_set = false;  // the kernel's dynamic LDS exceeds the 64 KiB default (set once; idempotent)
     if (!attr_set) {

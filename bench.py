@@ -65,6 +65,8 @@ def parse():
                     "(default; falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the "
                     "(L-1)-hop halo of its rows (no collective on the data path); 'exchange' = node-range rows + RCCL "
                     "all-gather of all rows per layer")
+    ap.add_argument("--no-graphs", action="store_true", help="N>1 middle partition: eager launches instead of the "
+                    "per-segment HIP graphs")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     ap.add_argument("--launch-check", action="store_true", help="N>1 plumbing check without a GPU: start the ranks, "
@@ -174,6 +176,7 @@ def main():
     if world > 1 and partition == "middle":
         mp = shard.middle_partition(g, rank, world)
         mid_in = shard.middle_inputs(model, mp)
+        mid_run = shard.MiddleRunner(model, mp, x, mid_in, graphs=not args.no_graphs)  # setup: HIP graphs captured
         log(f"[bench] middle partition: rank {rank} owns middles [{mp.m0}, {mp.m1}) = {mp.n_own} rows, receives "
             f"{int(mp.recv_ids.numel())} ghost rows per layer boundary (N={N})")
     elif world > 1 and partition == "halo":
@@ -186,7 +189,7 @@ def main():
     def step():
         with torch.no_grad():
             if mp is not None:
-                return shard.middle_forward(model, mp, x, mid_in)
+                return mid_run()
             if hp is not None:
                 return shard.halo_forward(model, hp, halo_in)
             if part is None:
@@ -218,6 +221,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
+    if not events and mp is not None:  # graph replays record no per-launch events: time eager forwards (untimed)
+        ops.SPMM_EVENTS = []
+        for _ in range(10):
+            with torch.no_grad():
+                shard.middle_forward(model, mp, x, mid_in)
+        torch.cuda.synchronize()
+        events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
     spmm_ms = [e0.elapsed_time(e1) for e0, e1 in events]
     t_local = torch.tensor([elapsed, sum(spmm_ms) / max(1, len(spmm_ms))], dtype=torch.float64, device=dev)
     if world > 1:
@@ -502,17 +512,23 @@ def extra_measurements(pkg, ops, g, model, x, data, log):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
 
-    from protgram_directgcn_amd._lib import PG_FLAG_NO_NGRAM, PG_FLAG_UNROLL4
+    from protgram_directgcn_amd._lib import (PG_FLAG_MID_NO_PAIRS, PG_FLAG_NGRAM_BLOCK4, PG_FLAG_NO_NGRAM,
+                                             PG_FLAG_UNROLL4)
     Fd = x.size(1)
     comp = g.compulsory_bytes(Fd)
     conv0 = model.convs[0]
     prm0 = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv0._dense_params())))
-    for fl, name in ((0, "ngram" if g.ngram is not None else "csr"), (PG_FLAG_NO_NGRAM, "csr_window_u4"),
-                     (PG_FLAG_NO_NGRAM | PG_FLAG_UNROLL4, "csr_window_u8")):
+    df = ops.default_flags()
+    variants = [(df, "ngram" if g.ngram is not None else "csr")]
+    if g.ngram is not None:
+        variants += [(df | PG_FLAG_MID_NO_PAIRS, "ngram_mid_no_pairs"), (df | PG_FLAG_NGRAM_BLOCK4, "ngram_block4")]
+    variants += [(df | PG_FLAG_NO_NGRAM, "csr_window_u4"), (df | PG_FLAG_NO_NGRAM | PG_FLAG_UNROLL4, "csr_window_u8")]
+    for fl, name in variants:
         ms = timeit(lambda: ops.spmm3(g, x, flags=fl))
         res[f"spmm3_{name}_ms"] = round(ms, 4)
         res[f"spmm3_{name}_compulsory_GBs"] = round(comp / ms / 1e6, 1)
-        res[f"spmm3_gated_{name}_ms"] = round(timeit(lambda: ops.spmm3_gated(g, x, prm0, 0, flags=fl)), 4)
+        if ops.spmm3_gated(g, x, prm0, 0, flags=fl) is not None:  # kernels with a gated store (not the middle one)
+            res[f"spmm3_gated_{name}_ms"] = round(timeit(lambda: ops.spmm3_gated(g, x, prm0, 0, flags=fl)), 4)
         if g.raw is not None and fl:
             res[f"spmm3_fused_{name}_ms"] = round(timeit(lambda: ops.spmm3(g, x, fused=True, flags=fl)), 4)
     Z = ops.spmm3(g, x)

@@ -810,3 +810,106 @@ def middle_forward(model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None
             X = _exchange_rows(mp, h_own, group)
         res_x = h_own
     return model.head(h_own)
+
+
+class MiddleRunner:
+    """middle_forward for a fixed input, with each rank's local work between two exchanges captured once as a HIP
+    graph (torch.cuda.CUDAGraph): per forward, L graph launches and L - 1 all_to_all_single calls, instead of a
+    dozen eager launches and their Python. At P = 8 a rank's GPU work per forward (~tens of us at 4-gram) is shorter
+    than the host time to issue it eagerly, so the graphs are what make the per-rank step GPU-bound. The collective
+    stays outside the graphs (issued eagerly between them, on the current stream). `graphs=False` (or a CPU input)
+    runs the same segments eagerly. Rebuild the runner after the parameters or the input change."""
+
+    def __init__(self, model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None, group=None, graphs: bool = True):
+        self.model, self.mp, self.x, self.group = model, mp, x_full, group
+        self.layers = inputs if inputs is not None else middle_inputs(model, mp)
+        self.L = len(model.convs)
+        dt = torch.bfloat16 if model.compute_dtype == torch.bfloat16 else x_full.dtype
+        self.bufs = [torch.empty(mp.n, conv.in_channels, device=x_full.device, dtype=dt)
+                     for conv in model.convs[1:]]  # global-layout inputs of layers 2..L
+        self.recv = [torch.empty(int(mp.recv_ids.numel()), conv.in_channels, device=x_full.device, dtype=dt)
+                     for conv in model.convs[1:]]
+        self.state = {}
+        self.graphs = None
+        with torch.no_grad():
+            for _ in range(2):  # eager warm-up: kernel attributes, allocator pools, lazy library state
+                out = self._run_eager()
+        torch.cuda.synchronize() if x_full.is_cuda else None
+        self.out = out
+        if graphs and x_full.is_cuda:
+            self._capture()
+
+    def _segment(self, i: int):
+        """Layer i's local work: its input (layer 0: the replicated input; later: own + received rows scattered
+        into the global-layout buffer), propagation over the owned middles, dense layer; then the rows to send
+        (not the last layer) or the head (the last)."""
+        mp, model = self.mp, self.model
+        conv, res = model.convs[i], model.res_projs[i]
+        prm, const = self.layers[i]
+        if i == 0:
+            h = model._apply_pe(self.x)
+            if model.compute_dtype == torch.bfloat16:
+                h = h.to(torch.bfloat16)
+            X, res_x = h, take(h, mp.own)
+        else:
+            X = self.bufs[i - 1]
+            res_x = self.state["h"]
+            X.index_copy_(0, mp.own, res_x)
+            if mp.world > 1:
+                X.index_copy_(0, mp.recv_ids, self.recv[i - 1])
+        gate_mode = 0 if conv.use_vector_coeffs else 1
+        W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
+        Z = _owned_spmm3(mp, X)
+        h_own = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=res_x, W_res=W_res, b_res=b_res, act=True)
+        self.state["h"] = h_own
+        if i + 1 < self.L:
+            self.state["send"] = take(h_own, mp.send_pos) if mp.world > 1 else None
+            return None
+        return model.head(h_own)
+
+    def _exchange(self, i: int):
+        mp = self.mp
+        if mp.world == 1:
+            return
+        send, recv = self.state["send"], self.recv[i]
+        if send.is_cuda and dist.get_backend(self.group) == "gloo":  # CPU rehearsal backend: host buffers
+            r = recv.new_empty(recv.shape, device="cpu")
+            dist.all_to_all_single(r, send.cpu(), mp.recv_counts, mp.send_counts, group=self.group)
+            recv.copy_(r)
+        else:
+            dist.all_to_all_single(recv, send, mp.recv_counts, mp.send_counts, group=self.group)
+
+    def _run_eager(self):
+        out = None
+        for i in range(self.L):
+            out = self._segment(i)
+            if i + 1 < self.L:
+                self._exchange(i)
+        return out
+
+    def _capture(self):
+        self.graphs = []
+        outs = None
+        pool = torch.cuda.graph_pool_handle()
+        for i in range(self.L):
+            gph = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(gph, pool=pool):
+                outs = self._segment(i)
+            self.graphs.append(gph)
+            if i + 1 < self.L:
+                gph.replay()  # the send rows of this capture's buffers, for the next segment's capture inputs
+                self._exchange(i)
+        self.out = outs
+        torch.cuda.synchronize()
+
+    @torch.no_grad()
+    def __call__(self):
+        """(log_probs, emb) for mp.global_rows. With graphs, the returned tensors are the graph's static outputs:
+        overwritten by the next call."""
+        if self.graphs is None:
+            return self._run_eager()
+        for i, gph in enumerate(self.graphs):
+            gph.replay()
+            if i + 1 < self.L:
+                self._exchange(i)
+        return self.out

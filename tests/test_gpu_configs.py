@@ -400,6 +400,16 @@ def _middle_rank_check(pkg, m, g, xd, lp_ref, emb_ref, rank, world, monkeypatch)
     assert len(hits) == len(m.convs)  # every layer on the middle-tile kernel
     rows = mp.global_rows
     assert torch.equal(lp, lp_ref[rows]) and torch.equal(emb, emb_ref[rows])
+    # the same rank through MiddleRunner: its segments captured as HIP graphs, the exchange (outside the graphs)
+    # filling the receive buffers from the single-GPU layer-1 output
+    with monkeypatch.context() as mpc:
+        mpc.setattr(shard.MiddleRunner, "_exchange", lambda self, i: self.recv[i].copy_(h1[self.mp.recv_ids]))
+        run = shard.MiddleRunner(m, mp, xd)
+        assert run.graphs is not None and len(run.graphs) == len(m.convs)
+        for _ in range(2):
+            lp2, emb2 = run()
+            torch.cuda.synchronize()
+            assert torch.equal(lp2, lp) and torch.equal(emb2, emb)
     return mp
 
 

@@ -103,6 +103,9 @@ def _worker(rank, world, port, out_q):
         rows = mp_.global_rows
         ok = (torch.allclose(lp, lp_r[rows], rtol=1e-5, atol=1e-5)
               and torch.allclose(emb, emb_r[rows], rtol=1e-5, atol=1e-5))
+        run = shard.MiddleRunner(model, mp_, x)  # CPU input: its segments run eagerly
+        lp2, emb2 = run()
+        ok = ok and torch.equal(lp2, lp) and torch.equal(emb2, emb)
         out_q.put((rank, int(rows.numel()), bool(ok), float((lp - lp_r[rows]).abs().max())))
     finally:
         dist.destroy_process_group()

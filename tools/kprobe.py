@@ -62,9 +62,10 @@ W1, b1 = torch.randn(64, 128, device=dev) * 0.1, torch.zeros(64, device=dev)
 W2, b2 = torch.randn(20, 64, device=dev) * 0.1, torch.zeros(20, device=dev)
 dY = torch.randn(N, 128, device=dev)
 for _ in range(reps):
-    Zg = ops.spmm3_gated(g, x, prm, 0)  # the inference (bench) propagation
-    ops.layer_dense(Zg, prm, 0, constant=layer.constant.detach(), res_x=x, act=True, pregated=True)
-    Z = ops.spmm3(g, x)                 # the training propagation
+    Zg = ops.spmm3_gated(g, x, prm, 0)  # the 4x4-block kernel's gated store (None: the middle-tile default gates later)
+    if Zg is not None:
+        ops.layer_dense(Zg, prm, 0, constant=layer.constant.detach(), res_x=x, act=True, pregated=True)
+    Z = ops.spmm3(g, x)                 # the propagation (inference and training: middle-tile kernel)
     ops.spmm3_t(g, Z)                   # transposed propagation (backward)
     Y = ops.layer_dense(Z, prm, 0, constant=layer.constant.detach(), res_x=x, act=True)
     ops.layer_dense_backward(dY, Z, Y, prm, 0, res_x=x, act=True)  # dgrad / wgrad / reduce

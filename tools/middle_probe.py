@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-rank cost of the middle partition (shard.middle_partition / middle_forward), measured on one GPU: for P in
-2, 4, 8 every rank's forward is timed in turn with HIP events, its ghost-row all_to_all replaced by the local part of
-the exchange (the index copy into the global-layout buffer; the received rows are taken from a precomputed layer-1
-output). The exchange itself is priced from the measured byte counts: per rank pair one xGMI link, so the
+2, 4, 8 every rank's forward is timed in turn with HIP events -- as the bench runs it (shard.MiddleRunner: per-segment
+HIP graphs) and eagerly (shard.middle_forward) -- its ghost-row all_to_all replaced by the local part of the exchange
+(the received rows are taken from a precomputed layer-1 output, once: the timed runner forward is the rank's local
+work only). The exchange itself is priced from the measured byte counts: per rank pair one xGMI link, so the
 all_to_all takes max over (sender, receiver) pairs of bytes / link rate; it is printed for the stated link rates,
 without and with overlap (max(compute, exchange) vs compute + exchange).
 usage: python tools/middle_probe.py [ngram] [F] [reps] [--out FILE]"""
@@ -18,6 +19,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 from protgram_directgcn_amd import ops, shard  # noqa: E402
+from protgram_directgcn_amd.graph import take  # noqa: E402
 import bench  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -61,7 +63,7 @@ with torch.no_grad():
 print(f"B(20,{n}) F={F}: single GPU {t1:.4f} ms/step", flush=True)
 report = {"ngram": n, "F": F, "N": N, "single_gpu_ms": round(t1, 4), "link_gbs_assumed": LINK_GBS, "P": {}}
 for P in (2, 4, 8):
-    ts, ghosts, link = [], [], 0
+    ts, te, ghosts, link = [], [], [], 0
     for r in range(P):
         mp = shard.middle_partition(g, r, P)
         inp = shard.middle_inputs(model, mp)
@@ -74,9 +76,24 @@ for P in (2, 4, 8):
         shard_exchange = shard._exchange_rows
         shard._exchange_rows = local_exchange
         try:
-            ts.append(timeit(lambda: shard.middle_forward(model, mp, x, inp)))
+            te.append(timeit(lambda: shard.middle_forward(model, mp, x, inp)))
         finally:
             shard._exchange_rows = shard_exchange
+        # the bench's path: MiddleRunner (per-segment HIP graphs), the exchange's receive side filled locally
+        runner_exchange = shard.MiddleRunner._exchange
+        def fill_once(self, i):  # layer-1 rows stand in for every boundary's received rows (timing only)
+            done = self.__dict__.setdefault("_filled", set())
+            if i not in done:
+                self.recv[i].copy_(take(h1, self.mp.recv_ids))
+                done.add(i)
+
+        shard.MiddleRunner._exchange = fill_once
+        try:
+            run = shard.MiddleRunner(model, mp, x, inp)
+            ts.append(timeit(run))
+        finally:
+            shard.MiddleRunner._exchange = runner_exchange
+        del run
         ghosts.append(int(mp.recv_ids.numel()))
         link = max(link, max(mp.recv_counts))
         del mp, inp, buf
@@ -87,10 +104,12 @@ for P in (2, 4, 8):
                "speedup_serial": round(t1 / (m + v), 2), "speedup_overlapped": round(t1 / max(m, v), 2)}
            for k, v in xch.items()}
     report["P"][P] = {"rank_ms": [round(t, 4) for t in ts], "max_rank_ms": round(m, 4),
+                      "eager_rank_ms": [round(t, 4) for t in te], "eager_max_rank_ms": round(max(te), 4),
                       "compute_speedup": round(t1 / m, 2), "ghost_rows_max": max(ghosts),
                       "ghost_MB_max": round(max(ghosts) * row_b / 1e6, 2), "max_rows_per_link": link,
                       "exchange_ms_per_link_rate": xch, "estimate": est}
-    print(f"P={P}: per-rank ms {' '.join(f'{t:.4f}' for t in ts)}  max {m:.4f}  compute speedup {t1 / m:.2f}x  "
+    print(f"P={P}: per-rank ms (graphs) {' '.join(f'{t:.4f}' for t in ts)}  max {m:.4f} (eager {max(te):.4f})  "
+          f"compute speedup {t1 / m:.2f}x  "
           f"ghost rows/rank <= {max(ghosts)} ({max(ghosts) * row_b / 1e6:.1f} MB), busiest link {link} rows; "
           + "; ".join(f"@{k} GB/s/link: exchange {v:.4f} ms -> {t1 / (m + v):.2f}x serial, {t1 / max(m, v):.2f}x "
                       f"overlapped" for k, v in xch.items()), flush=True)

@@ -58,8 +58,8 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 FETCH_SIZE/WRITE_SIZE passes that "
                     "measure roofline.traffic (N=1 only)")
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
-    ap.add_argument("--chunks", type=int, default=4, help="N>1: layer-boundary all-gather in this many pieces, "
-                    "overlapped with the compute (1 = one exchange after the layer)")
+    ap.add_argument("--chunks", type=int, default=0, help="N>1: layer-boundary exchange in this many pieces, "
+                    "overlapped with the compute (1 = one exchange after the layer; 0 = by the rank's share)")
     ap.add_argument("--partition", choices=("middle", "halo", "exchange"), default="middle",
                     help="N>1: 'middle' = middle (n-2)-gram ranges + RCCL ghost-row all_to_all per layer boundary "
                     "(default; falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the "
@@ -174,7 +174,12 @@ def main():
     if world > 1 and partition == "middle" and (shard.ngram_shape(g) is None or shard.ngram_shape(g)[1] < 3):
         partition = "halo"
     if world > 1 and partition == "middle":
-        mp = shard.middle_partition(g, rank, world)
+        # sub-ranges for the overlapped exchange only where a rank's share is large enough that a sub-range still
+        # fills the GPU (a middle-tile launch has a fixed ~10 us start; at 4-gram, 8 ranks, 20k rows each, one
+        # range is faster; at 5-gram, 400k rows each, four)
+        n_own = N // world
+        chunks = args.chunks if args.chunks > 0 else max(1, min(4, n_own // 100_000))
+        mp = shard.middle_partition(g, rank, world, chunks=chunks)
         mid_in = shard.middle_inputs(model, mp)
         mid_run = shard.MiddleRunner(model, mp, x, mid_in, graphs=not args.no_graphs)  # setup: HIP graphs captured
         log(f"[bench] middle partition: rank {rank} owns middles [{mp.m0}, {mp.m1}) = {mp.n_own} rows, receives "
@@ -194,7 +199,7 @@ def main():
                 return shard.halo_forward(model, hp, halo_in)
             if part is None:
                 return model(data)
-            return shard.sharded_forward(model, part, x, chunks=args.chunks)
+            return shard.sharded_forward(model, part, x, chunks=args.chunks or 4)
 
     # untimed clock ramp: the GPU's clocks take ~100 ms of load to settle (5 warm-up steps measured 0.915 ms/step,
     # 50 or 200 gave 0.62): run steps for args.clock_warmup_s seconds before the W counted warm-up steps, so a short
@@ -317,7 +322,7 @@ def main():
                        "parallelism": ("single" if world == 1 else f"middle_ghost_a2a_x{world}" if mp is not None
                                        else f"halo_recompute_x{world}" if hp is not None else f"node_range_x{world}"),
                        "ghost_rows_rank0": int(mp.recv_ids.numel()) if mp is not None else None,
-                       "exchange_chunks": args.chunks if part is not None else None,
+                       "exchange_chunks": (mp.chunks if mp is not None else (args.chunks or 4) if part is not None else None),
                        "halo_rows_rank0": hp.layer_rows if hp is not None else None},
             "nodes_per_sec": round(N * L * args.steps / elapsed, 1),
             "roofline": roofline,

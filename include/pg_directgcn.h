@@ -241,6 +241,15 @@ int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, cons
 int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                                 int64_t m_begin, int64_t m_end, float* Z, int64_t ldz, uint32_t flags, void* stream);
 
+/* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
+ * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).
+ * Byte-generic rows of row_bytes (a multiple of 4; 16-B pieces when rows, strides and pointers allow); strides in
+ * bytes. pg_rows_gather: dst[i] = src[idx[i]]; pg_rows_scatter: dst[idx[i]] = src[i] (indices must be distinct). */
+int pg_rows_gather(const void* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t row_bytes, void* dst,
+                   int64_t ld_dst, void* stream);
+int pg_rows_scatter(const void* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t row_bytes, void* dst,
+                    int64_t ld_dst, void* stream);
+
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output
  * (read for leaky_relu' when act != 0); `packed` the forward's packed operand. Outputs:

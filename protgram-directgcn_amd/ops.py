@@ -186,6 +186,37 @@ def spmm3_middles(g: CSRGraph, x: torch.Tensor, m_begin: int, m_end: int, flags:
     return Z
 
 
+def rows_gather(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[i] = src[idx[i]] (pg_rows_gather; rows of any dtype, unit column stride)."""
+    lib = load_library()
+    _require_gpu(src)
+    if src.dim() != 2 or src.stride(1) != 1:
+        raise ValueError("rows_gather needs a 2-D source with unit column stride")
+    idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+    out = out if out is not None else torch.empty(idx.numel(), src.size(1), device=src.device, dtype=src.dtype)
+    if out.shape != (idx.numel(), src.size(1)) or out.dtype != src.dtype or out.stride(1) != 1:
+        raise ValueError("rows_gather: out must be [len(idx), src.size(1)] of src's dtype")
+    es = src.element_size()
+    check(lib.pg_rows_gather(_p(src), src.stride(0) * es, _p(idx), idx.numel(), src.size(1) * es, _p(out),
+                             out.stride(0) * es, _stream(src)), "pg_rows_gather")
+    return out
+
+
+def rows_scatter(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """dst[idx[i]] = src[i] (pg_rows_scatter; distinct indices; rows of any dtype, unit column stride)."""
+    lib = load_library()
+    _require_gpu(src)
+    if src.dim() != 2 or dst.dim() != 2 or src.size(1) != dst.size(1) or src.dtype != dst.dtype:
+        raise ValueError("rows_scatter: src and dst must be 2-D of the same width and dtype")
+    if src.stride(1) != 1 or dst.stride(1) != 1 or idx.numel() != src.size(0):
+        raise ValueError("rows_scatter: unit column strides and one index per source row")
+    idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+    es = src.element_size()
+    check(lib.pg_rows_scatter(_p(src), src.stride(0) * es, _p(idx), idx.numel(), src.size(1) * es, _p(dst),
+                              dst.stride(0) * es, _stream(src)), "pg_rows_scatter")
+    return dst
+
+
 def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
     x = _bf16c(x)
     _require_gpu(x)

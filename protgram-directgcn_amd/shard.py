@@ -635,11 +635,15 @@ class MiddlePartition:
     m1: int
     own: torch.Tensor           # int64 [n_own]: global ids of the owned rows, middle-major ((M - m0) K^2 + a K + b)
     own_csr: CSRGraph           # the global CSR's rows `own` (global column ids): the CSR-kernel path
-    send_pos: torch.Tensor      # int64: positions (in the owned-row order) of the rows sent, grouped by destination
-    send_counts: List[int]
-    recv_ids: torch.Tensor      # int64: global ids of the rows received, grouped by source rank (ascending ids)
-    recv_counts: List[int]
+    send_pos: torch.Tensor      # int64: positions (owned-row order) of the rows sent, by (chunk, destination)
+    send_counts: List[int]      # rows sent to each rank (all chunks)
+    recv_ids: torch.Tensor      # int64: global ids of the rows received, by (chunk, source), ascending ids within
+    recv_counts: List[int]      # rows received from each rank (all chunks)
     graph: CSRGraph             # the global graph (its middle plan)
+    chunks: int = 1             # the owned middles in `chunks` sub-ranges: a layer's exchange per sub-range
+    chunk_bounds: List[tuple] = field(default_factory=list)   # owned middle sub-ranges
+    chunk_send: List[List[int]] = field(default_factory=list)  # [chunk][destination] rows sent
+    chunk_recv: List[List[int]] = field(default_factory=list)  # [chunk][source] rows received
     cache: dict = field(default_factory=dict)
 
     @property
@@ -687,10 +691,12 @@ def _middle_reads(K: int, n: int, m0: int, m1: int, dev) -> torch.Tensor:
     return torch.unique(torch.cat([out_src, in_src, _middle_rows(K, n, m0, m1, dev)]))
 
 
-def middle_partition(g: CSRGraph, rank: int, world: int) -> MiddlePartition:
+def middle_partition(g: CSRGraph, rank: int, world: int, chunks: int = 1) -> MiddlePartition:
     """This rank's middle partition of a complete n-gram graph (see the section comment). Setup work, once per
     graph: the exchange lists of every rank pair are built from the closed-form read sets (and checked against
-    the CSR's own columns), so both ends of each pair agree without communication."""
+    the CSR's own columns), so both ends of each pair agree without communication. With chunks > 1 every rank's
+    middles are cut into `chunks` sub-ranges and the lists are grouped by the sender's sub-range, so each sub-range's
+    rows can be exchanged as soon as they are computed (MiddleRunner overlaps that exchange with the next one)."""
     shape = ngram_shape(g)
     if shape is None or not g.shared:
         raise NotImplementedError("middle partition needs a shared-pattern graph over all K^n n-grams")
@@ -702,31 +708,53 @@ def middle_partition(g: CSRGraph, rank: int, world: int) -> MiddlePartition:
         raise ValueError(f"{world} ranks but only {Kn2} middles")
     dev = g.rowptr.device
     bounds = middle_bounds(Kn2, world)
+    chunks = max(1, min(chunks, min(b - a for a, b in bounds)))
     starts = torch.tensor([b[0] for b in bounds], dtype=torch.int64, device=dev)
     m0, m1 = bounds[rank]
 
-    def owner_and_pos(x):
+    chunk_of = torch.empty(Kn2, dtype=torch.int64)  # middle -> sub-range of its owner's range
+    for a, b in bounds:
+        for cc in range(chunks):
+            chunk_of[a + cc * (b - a) // chunks:a + (cc + 1) * (b - a) // chunks] = cc
+    chunk_of = chunk_of.to(dev)
+
+    def owner_pos_chunk(x):
         Mx = (x % Kn1) // K
         q = torch.searchsorted(starts, Mx, right=True) - 1
         pos = (Mx - starts[q]) * (K * K) + (x // Kn1) * K + x % K
-        return q, pos
+        return q, pos, chunk_of[Mx]
 
     own = _middle_rows(K, n, m0, m1, dev)
-    send_pos, send_counts, recv_ids, recv_counts = [], [0] * world, None, [0] * world
+    sends = [[None] * world for _ in range(chunks)]
+    chunk_send = [[0] * world for _ in range(chunks)]
+    chunk_recv = [[0] * world for _ in range(chunks)]
+    recv_ids = None
     for p in range(world):
         reads = _middle_reads(K, n, *bounds[p], dev)
-        q, pos = owner_and_pos(reads)
+        q, pos, c = owner_pos_chunk(reads)
         if p == rank:
             ghost = q != rank
-            gq, gid = q[ghost], reads[ghost]
-            order = torch.sort(gq, stable=True).indices  # by source rank, ascending ids within
+            gq, gc, gid = q[ghost], c[ghost], reads[ghost]
+            order = torch.sort(gc * world + gq, stable=True).indices  # by (chunk, source), ascending ids within
             recv_ids = gid[order]
-            recv_counts = torch.bincount(gq, minlength=world).tolist()
+            cnt = torch.bincount(gc * world + gq, minlength=chunks * world).view(chunks, world).tolist()
+            chunk_recv = cnt
         else:
             mine = q == rank
-            send_pos.append(pos[mine])
-            send_counts[p] = int(mine.sum())
-    send_pos = torch.cat(send_pos) if send_pos else torch.zeros(0, dtype=torch.int64, device=dev)
+            pm, cm = pos[mine], c[mine]
+            for cc in range(chunks):
+                sel = pm[cm == cc]
+                sends[cc][p] = sel
+                chunk_send[cc][p] = int(sel.numel())
+    empty = torch.zeros(0, dtype=torch.int64, device=dev)
+    send_pos = torch.cat([sends[cc][p] if sends[cc][p] is not None else empty
+                          for cc in range(chunks) for p in range(world)]) if world > 1 else empty
+    send_counts = [sum(chunk_send[cc][p] for cc in range(chunks)) for p in range(world)]
+    recv_counts = [sum(chunk_recv[cc][p] for cc in range(chunks)) for p in range(world)]
+    if recv_ids is None:
+        recv_ids = empty
+    L = m1 - m0
+    chunk_bounds = [(m0 + cc * L // chunks, m0 + (cc + 1) * L // chunks) for cc in range(chunks)]
     # the owned rows' CSR (global column ids), and the check that it reads nothing outside the closed-form set
     rp = g.rowptr
     cnt = rp[own + 1] - rp[own]
@@ -742,7 +770,7 @@ def middle_partition(g: CSRGraph, rank: int, world: int) -> MiddlePartition:
     own_csr = CSRGraph(n_rows=own.numel(), shared=True, rowptr=lrp, edges3=e, symmetric=False, nnz=tot,
                        row_order=None, n_cols=g.n_rows)
     return MiddlePartition(rank, world, g.n_rows, K, n, m0, m1, own, own_csr, send_pos, send_counts, recv_ids,
-                           recv_counts, g)
+                           recv_counts, g, chunks, chunk_bounds, chunk_send, chunk_recv)
 
 
 @torch.no_grad()
@@ -774,18 +802,18 @@ def _owned_spmm3(mp: MiddlePartition, X: torch.Tensor) -> torch.Tensor:
 def _exchange_rows(mp: MiddlePartition, h_own: torch.Tensor, group=None) -> torch.Tensor:
     """The next layer's input in the global row layout: this rank's rows plus the ghost rows it reads, received
     from their owners by one all_to_all_single (the same tensor collective on RCCL and on gloo). Rows nobody
-    reads stay unwritten."""
+    reads stay unwritten. (MiddleRunner does the same per chunk, overlapped.)"""
     F_ = h_own.size(1)
     X = h_own.new_empty(mp.n, F_)
-    X.index_copy_(0, mp.own, h_own)
+    ops.rows_scatter(h_own, mp.own, X)
     if mp.world > 1:
-        send = take(h_own, mp.send_pos)
+        send = ops.rows_gather(h_own, mp.send_pos)
         stage = h_own.is_cuda and dist.get_backend(group) == "gloo"  # gloo (CPU rehearsal backend): host buffers
         if stage:
             send = send.cpu()
         recv = send.new_empty(int(mp.recv_ids.numel()), F_)
         dist.all_to_all_single(recv, send, mp.recv_counts, mp.send_counts, group=group)
-        X.index_copy_(0, mp.recv_ids, recv.to(X.device) if stage else recv)
+        ops.rows_scatter(recv.to(X.device) if stage else recv, mp.recv_ids, X)
     return X
 
 
@@ -799,7 +827,7 @@ def middle_forward(model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None
     h = model._apply_pe(x_full)
     if model.compute_dtype == torch.bfloat16:
         h = h.to(torch.bfloat16)
-    X, res_x = h, take(h, mp.own)
+    X, res_x = h, ops.rows_gather(h, mp.own)
     L = len(model.convs)
     for i, (conv, res, (prm, const)) in enumerate(zip(model.convs, model.res_projs, layers)):
         gate_mode = 0 if conv.use_vector_coeffs else 1
@@ -813,93 +841,163 @@ def middle_forward(model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None
 
 
 class MiddleRunner:
-    """middle_forward for a fixed input, with each rank's local work between two exchanges captured once as a HIP
-    graph (torch.cuda.CUDAGraph): per forward, L graph launches and L - 1 all_to_all_single calls, instead of a
-    dozen eager launches and their Python. At P = 8 a rank's GPU work per forward (~tens of us at 4-gram) is shorter
-    than the host time to issue it eagerly, so the graphs are what make the per-rank step GPU-bound. The collective
-    stays outside the graphs (issued eagerly between them, on the current stream). `graphs=False` (or a CPU input)
-    runs the same segments eagerly. Rebuild the runner after the parameters or the input change."""
+    """The bench's multi-GPU forward on the middle partition, for a fixed input.
 
-    def __init__(self, model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None, group=None, graphs: bool = True):
+    Every layer but the last runs in the partition's `chunks` middle sub-ranges: sub-range c's rows are propagated
+    (middle-tile kernel over its middles), transformed (dense kernel on its rows), and the rows other ranks read
+    are gathered and handed to an asynchronous all_to_all_single, which runs on the collective's own stream while
+    sub-range c + 1 computes. The next layer waits for all of them, scatters its own and the received rows into its
+    global-layout input, and so on; the last layer runs whole and ends in the head. Each compute segment is
+    captured once as a HIP graph (torch.cuda.CUDAGraph) and replayed, so a rank issues L-1 x chunks + 1 graph
+    launches and the collectives per forward; the collectives stay outside the graphs. `graphs=False` (or a CPU
+    input) runs the segments eagerly; gloo (the CPU rehearsal backend) exchanges synchronously through host
+    buffers. Rebuild the runner after the parameters or the input change. The rows it returns are bit-identical
+    to middle_forward's (and to the single-GPU forward's)."""
+
+    def __init__(self, model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None, group=None,
+                 graphs: bool = True):
         self.model, self.mp, self.x, self.group = model, mp, x_full, group
         self.layers = inputs if inputs is not None else middle_inputs(model, mp)
         self.L = len(model.convs)
-        dt = torch.bfloat16 if model.compute_dtype == torch.bfloat16 else x_full.dtype
-        self.bufs = [torch.empty(mp.n, conv.in_channels, device=x_full.device, dtype=dt)
-                     for conv in model.convs[1:]]  # global-layout inputs of layers 2..L
-        self.recv = [torch.empty(int(mp.recv_ids.numel()), conv.in_channels, device=x_full.device, dtype=dt)
+        dev = x_full.device
+        self.dt = torch.bfloat16 if model.compute_dtype == torch.bfloat16 else x_full.dtype
+        self.bufs = [torch.empty(mp.n, conv.in_channels, device=dev, dtype=self.dt) for conv in model.convs[1:]]
+        self.recv = [torch.empty(int(mp.recv_ids.numel()), conv.in_channels, device=dev, dtype=self.dt)
                      for conv in model.convs[1:]]
+        self.hout = [torch.empty(mp.n_own, conv.out_channels, device=dev, dtype=self.dt) for conv in model.convs[:-1]]
+        K2 = mp.K * mp.K
+        self.row_bounds = [((a - mp.m0) * K2, (b - mp.m0) * K2) for a, b in mp.chunk_bounds]
+        off, self.send_slices = 0, []
+        for c in range(mp.chunks):
+            k = sum(mp.chunk_send[c])
+            self.send_slices.append((off, off + k))
+            off += k
+        off, self.recv_slices = 0, []
+        for c in range(mp.chunks):
+            k = sum(mp.chunk_recv[c])
+            self.recv_slices.append((off, off + k))
+            off += k
+        # the CSR path's row blocks (bf16 / no middle plan), cut before any capture (slicing reads rowptr on the host)
+        self.csr_chunks = [_rows_slice(mp.own_csr, r0, r1, None) for r0, r1 in self.row_bounds]
+        backend = dist.get_backend(group) if (mp.world > 1 and dist.is_initialized()) else None
+        self.sync = (not x_full.is_cuda) or backend == "gloo"
         self.state = {}
+        self.works = []
         self.graphs = None
         with torch.no_grad():
             for _ in range(2):  # eager warm-up: kernel attributes, allocator pools, lazy library state
                 out = self._run_eager()
-        torch.cuda.synchronize() if x_full.is_cuda else None
+        if x_full.is_cuda:
+            torch.cuda.synchronize()
         self.out = out
         if graphs and x_full.is_cuda:
             self._capture()
 
-    def _segment(self, i: int):
-        """Layer i's local work: its input (layer 0: the replicated input; later: own + received rows scattered
-        into the global-layout buffer), propagation over the owned middles, dense layer; then the rows to send
-        (not the last layer) or the head (the last)."""
+    # ---- segments (graph bodies)
+    def _prepare(self, i: int):
+        """Layer i's global-layout input and its residual rows (owned-row order)."""
         mp, model = self.mp, self.model
-        conv, res = model.convs[i], model.res_projs[i]
-        prm, const = self.layers[i]
         if i == 0:
             h = model._apply_pe(self.x)
             if model.compute_dtype == torch.bfloat16:
                 h = h.to(torch.bfloat16)
-            X, res_x = h, take(h, mp.own)
+            self.state["X"], self.state["res"] = h, ops.rows_gather(h, mp.own)
         else:
-            X = self.bufs[i - 1]
-            res_x = self.state["h"]
-            X.index_copy_(0, mp.own, res_x)
-            if mp.world > 1:
-                X.index_copy_(0, mp.recv_ids, self.recv[i - 1])
+            X, h_prev = self.bufs[i - 1], self.hout[i - 1]
+            ops.rows_scatter(h_prev, mp.own, X)
+            if mp.world > 1 and self.recv[i - 1].size(0):
+                ops.rows_scatter(self.recv[i - 1], mp.recv_ids, X)
+            self.state["X"], self.state["res"] = X, h_prev
+
+    def _compute(self, i: int, c: Optional[int]):
+        """Layer i over chunk c's middles (c None: all owned middles); returns the layer output rows."""
+        mp, model = self.mp, self.model
+        conv, res = model.convs[i], model.res_projs[i]
+        prm, const = self.layers[i]
+        if c is None:
+            (a, b), (r0, r1) = (mp.m0, mp.m1), (0, mp.n_own)
+        else:
+            (a, b), (r0, r1) = mp.chunk_bounds[c], self.row_bounds[c]
+        X, res_x = self.state["X"], self.state["res"][r0:r1]
+        if mp.graph.ngram is not None and ops._mid_ok(mp.graph, X, ops.default_flags()):
+            Z = ops.spmm3_middles(mp.graph, X, a, b)
+        else:
+            Z = ops.spmm3(mp.own_csr if c is None else self.csr_chunks[c], X)
+        if conv.use_vector_coeffs:
+            prm = dict(prm)
+            for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+                prm[k] = prm[k][r0:r1]
+            const = const[r0:r1] if const is not None else None
         gate_mode = 0 if conv.use_vector_coeffs else 1
         W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
-        Z = _owned_spmm3(mp, X)
-        h_own = ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=res_x, W_res=W_res, b_res=b_res, act=True)
-        self.state["h"] = h_own
-        if i + 1 < self.L:
-            self.state["send"] = take(h_own, mp.send_pos) if mp.world > 1 else None
-            return None
-        return model.head(h_own)
+        out = self.hout[i][r0:r1] if i + 1 < self.L else None
+        return ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=res_x, W_res=W_res, b_res=b_res, act=True,
+                               out=out)
 
-    def _exchange(self, i: int):
+    def _segment(self, i: int, c: Optional[int]):
+        """One graph body: [layer input (first chunk)], chunk c of layer i, the rows it sends (or the head)."""
+        if c is None or c == 0:
+            self._prepare(i)
+        h = self._compute(i, c)
+        if i + 1 < self.L:
+            if self.mp.world > 1:
+                s0, s1 = self.send_slices[c]
+                self.state[("send", i, c)] = ops.rows_gather(self.hout[i], self.mp.send_pos[s0:s1])
+            return None
+        return self.model.head(h)
+
+    # ---- exchange (outside the graphs)
+    def _exchange(self, i: int, c: int):
         mp = self.mp
         if mp.world == 1:
             return
-        send, recv = self.state["send"], self.recv[i]
-        if send.is_cuda and dist.get_backend(self.group) == "gloo":  # CPU rehearsal backend: host buffers
+        send = self.state[("send", i, c)]
+        r0, r1 = self.recv_slices[c]
+        recv = self.recv[i][r0:r1]
+        if self.sync:  # gloo / CPU: synchronous, through host buffers for device tensors
             r = recv.new_empty(recv.shape, device="cpu")
-            dist.all_to_all_single(r, send.cpu(), mp.recv_counts, mp.send_counts, group=self.group)
+            dist.all_to_all_single(r, send.cpu(), mp.chunk_recv[c], mp.chunk_send[c], group=self.group)
             recv.copy_(r)
         else:
-            dist.all_to_all_single(recv, send, mp.recv_counts, mp.send_counts, group=self.group)
+            self.works.append(dist.all_to_all_single(recv, send, mp.chunk_recv[c], mp.chunk_send[c],
+                                                     group=self.group, async_op=True))
+
+    def _wait(self):
+        for w in self.works:
+            w.wait()  # RCCL: the current stream waits for the collective's stream (no host block)
+        self.works = []
+
+    def _plan(self):
+        """The segment sequence: (layer, chunk) pairs; the last layer whole (chunk None)."""
+        seq = [(i, c) for i in range(self.L - 1) for c in range(self.mp.chunks)]
+        return seq + [(self.L - 1, None)]
 
     def _run_eager(self):
         out = None
-        for i in range(self.L):
-            out = self._segment(i)
-            if i + 1 < self.L:
-                self._exchange(i)
+        for i, c in self._plan():
+            if c is None or c == 0:
+                self._wait()
+            out = self._segment(i, c)
+            if c is not None:
+                self._exchange(i, c)
+        self._wait()
         return out
 
     def _capture(self):
         self.graphs = []
-        outs = None
         pool = torch.cuda.graph_pool_handle()
-        for i in range(self.L):
+        for i, c in self._plan():
+            if c is None or c == 0:
+                self._wait()
             gph = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(gph, pool=pool):
-                outs = self._segment(i)
+                out = self._segment(i, c)
+            gph.replay()  # this segment's outputs for the next capture's inputs
+            if c is not None:
+                self._exchange(i, c)
             self.graphs.append(gph)
-            if i + 1 < self.L:
-                gph.replay()  # the send rows of this capture's buffers, for the next segment's capture inputs
-                self._exchange(i)
-        self.out = outs
+        self._wait()
+        self.out = out
         torch.cuda.synchronize()
 
     @torch.no_grad()
@@ -908,8 +1006,11 @@ class MiddleRunner:
         overwritten by the next call."""
         if self.graphs is None:
             return self._run_eager()
-        for i, gph in enumerate(self.graphs):
+        for gph, (i, c) in zip(self.graphs, self._plan()):
+            if c is None or c == 0:
+                self._wait()
             gph.replay()
-            if i + 1 < self.L:
-                self._exchange(i)
+            if c is not None:
+                self._exchange(i, c)
+        self._wait()
         return self.out

@@ -400,12 +400,18 @@ def _middle_rank_check(pkg, m, g, xd, lp_ref, emb_ref, rank, world, monkeypatch)
     assert len(hits) == len(m.convs)  # every layer on the middle-tile kernel
     rows = mp.global_rows
     assert torch.equal(lp, lp_ref[rows]) and torch.equal(emb, emb_ref[rows])
-    # the same rank through MiddleRunner: its segments captured as HIP graphs, the exchange (outside the graphs)
-    # filling the receive buffers from the single-GPU layer-1 output
+    # the same rank through MiddleRunner (the bench's path): layer 1 in 3 middle sub-ranges, each compute segment
+    # captured as a HIP graph; the per-sub-range exchange (outside the graphs) fills the receive slices from the
+    # single-GPU layer-1 output
+    def fill(self, i, c):
+        r0, r1 = self.recv_slices[c]
+        self.recv[i][r0:r1] = h1[self.mp.recv_ids[r0:r1]]
+
+    mpc_ = shard.middle_partition(g, rank, world, chunks=3)
     with monkeypatch.context() as mpc:
-        mpc.setattr(shard.MiddleRunner, "_exchange", lambda self, i: self.recv[i].copy_(h1[self.mp.recv_ids]))
-        run = shard.MiddleRunner(m, mp, xd)
-        assert run.graphs is not None and len(run.graphs) == len(m.convs)
+        mpc.setattr(shard.MiddleRunner, "_exchange", fill)
+        run = shard.MiddleRunner(m, mpc_, xd)
+        assert run.graphs is not None and len(run.graphs) == 3 * (len(m.convs) - 1) + 1
         for _ in range(2):
             lp2, emb2 = run()
             torch.cuda.synchronize()

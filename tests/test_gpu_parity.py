@@ -1090,3 +1090,22 @@ def test_take_large_wide_rows(pkg, cuda):
     got = pkg.graph.take(t.to(cuda), idx.to(cuda))
     assert got.shape == (rows, 128)
     assert torch.equal(got.cpu(), t[idx])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,F", [(torch.float32, 128), (torch.bfloat16, 128), (torch.float32, 5), (torch.bfloat16, 6)])
+def test_rows_gather_scatter(pkg, cuda, dtype, F):
+    """pg_rows_gather / pg_rows_scatter (the middle partition's exchange data movement) == torch indexing, bit for
+    bit, on 16-B-vector rows and on rows of 4-B words only, with a strided source."""
+    from protgram_directgcn_amd import ops
+    gen = torch.Generator().manual_seed(F)
+    src = torch.randn(5000, F + 4, generator=gen).to(dtype).to(cuda)[:, :F]  # row stride != row width
+    idx = torch.randperm(5000, generator=gen)[:3001].to(cuda)
+    got = ops.rows_gather(src, idx)
+    assert torch.equal(got, src[idx])
+    dst = torch.zeros(5000, F, dtype=dtype, device=cuda)
+    ops.rows_scatter(got, idx, dst)
+    ref = torch.zeros_like(dst)
+    ref[idx] = src[idx]
+    assert torch.equal(dst, ref)
+    assert ops.rows_gather(src, idx[:0]).shape == (0, F)

@@ -60,6 +60,38 @@ def test_middle_partition_structure(pkg, n, world):
         assert max(p.recv_ids.numel() for p in parts) < 0.5 * N
 
 
+@pytest.mark.parametrize("n,world,chunks", [(3, 2, 2), (3, 3, 3), (4, 8, 4)])
+def test_middle_partition_chunked_lists(pkg, n, world, chunks):
+    """With the owned middles in sub-ranges, sub-range c of rank q sends p exactly what p receives from q in c (same
+    order), the sub-ranges tile the owned middles, and the per-pair totals equal the unchunked partition's."""
+    from protgram_directgcn_amd import shard
+    N, _, g = _graph(pkg, n)
+    parts = [shard.middle_partition(g, r, world, chunks=chunks) for r in range(world)]
+    flat = [shard.middle_partition(g, r, world) for r in range(world)]
+    for p, f in zip(parts, flat):
+        assert p.chunks == chunks and p.chunk_bounds[0][0] == p.m0 and p.chunk_bounds[-1][1] == p.m1
+        assert all(a[1] == b[0] for a, b in zip(p.chunk_bounds, p.chunk_bounds[1:]))
+        assert p.send_counts == f.send_counts and p.recv_counts == f.recv_counts
+        assert torch.equal(torch.sort(p.recv_ids).values, torch.sort(f.recv_ids).values)
+
+    def seg(counts, c, r):  # offset of (chunk c, rank r) in a chunk-major, rank-minor list
+        off = sum(sum(counts[cc]) for cc in range(c)) + sum(counts[c][:r])
+        return off, off + counts[c][r]
+
+    for q in parts:
+        for p in parts:
+            if p.rank == q.rank:
+                continue
+            for c in range(chunks):
+                a, b = seg(q.chunk_send, c, p.rank)
+                sent = q.own[q.send_pos[a:b]]
+                a2, b2 = seg(p.chunk_recv, c, q.rank)
+                assert torch.equal(sent, p.recv_ids[a2:b2]), (q.rank, p.rank, c)
+                lo, hi = q.chunk_bounds[c]  # every row q sends in sub-range c comes from one of its middles
+                mids = (sent % 20 ** (n - 1)) // 20
+                assert bool(((mids >= lo) & (mids < hi)).all())
+
+
 def test_middle_partition_rejects_other_graphs(pkg):
     from protgram_directgcn_amd import shard
     _, _, g2 = _graph(pkg, 2)
@@ -85,6 +117,8 @@ def _worker(rank, world, port, out_q):
     from test_shard_gloo import _cpu_layer_dense, _cpu_spmm3
     ops.spmm3 = _cpu_spmm3
     ops.layer_dense = _cpu_layer_dense
+    ops.rows_gather = lambda src, idx, out=None: src[idx] if out is None else out.copy_(src[idx])
+    ops.rows_scatter = lambda src, idx, dst: dst.index_copy_(0, idx, src)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         N, m, g = _graph(pkg, 3)
@@ -106,6 +140,9 @@ def _worker(rank, world, port, out_q):
         run = shard.MiddleRunner(model, mp_, x)  # CPU input: its segments run eagerly
         lp2, emb2 = run()
         ok = ok and torch.equal(lp2, lp) and torch.equal(emb2, emb)
+        mpc = shard.middle_partition(g, rank, world, chunks=2)  # layer 1 in two sub-ranges, exchanged per sub-range
+        lp3, emb3 = shard.MiddleRunner(model, mpc, x)()
+        ok = ok and torch.equal(lp3, lp) and torch.equal(emb3, emb)
         out_q.put((rank, int(rows.numel()), bool(ok), float((lp - lp_r[rows]).abs().max())))
     finally:
         dist.destroy_process_group()

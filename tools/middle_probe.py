@@ -29,6 +29,7 @@ if out in args:
 n = int(args[0]) if args else 4
 F = int(args[1]) if len(args) > 1 else 128
 reps = int(args[2]) if len(args) > 2 else 30
+CHUNKS = 4  # bench.py --chunks default: layer 1 in 4 middle sub-ranges, each exchanged as soon as it is computed
 LINK_GBS = (50.0, 100.0)  # assumed achieved all_to_all rate per xGMI peer link and direction (GB/s)
 dev = torch.device("cuda:0")
 N, s, d, c = pkg.synth.de_bruijn_edges(n)
@@ -65,7 +66,7 @@ report = {"ngram": n, "F": F, "N": N, "single_gpu_ms": round(t1, 4), "link_gbs_a
 for P in (2, 4, 8):
     ts, te, ghosts, link = [], [], [], 0
     for r in range(P):
-        mp = shard.middle_partition(g, r, P)
+        mp = shard.middle_partition(g, r, P, chunks=CHUNKS)
         inp = shard.middle_inputs(model, mp)
         buf = h1.clone()
 
@@ -81,11 +82,12 @@ for P in (2, 4, 8):
             shard._exchange_rows = shard_exchange
         # the bench's path: MiddleRunner (per-segment HIP graphs), the exchange's receive side filled locally
         runner_exchange = shard.MiddleRunner._exchange
-        def fill_once(self, i):  # layer-1 rows stand in for every boundary's received rows (timing only)
+        def fill_once(self, i, c):  # layer-1 rows stand in for every boundary's received rows (timing only)
             done = self.__dict__.setdefault("_filled", set())
-            if i not in done:
-                self.recv[i].copy_(take(h1, self.mp.recv_ids))
-                done.add(i)
+            if (i, c) not in done:
+                r0, r1 = self.recv_slices[c]
+                self.recv[i][r0:r1] = take(h1, self.mp.recv_ids[r0:r1])
+                done.add((i, c))
 
         shard.MiddleRunner._exchange = fill_once
         try:

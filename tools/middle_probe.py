@@ -62,11 +62,21 @@ with torch.no_grad():
     h1 = ops.layer_dense(ops.spmm3(g, h0), prm, 0 if conv.use_vector_coeffs else 1,
                          constant=conv.constant.detach() if conv.use_vector_coeffs else None, res_x=h0, act=True)
 print(f"B(20,{n}) F={F}: single GPU {t1:.4f} ms/step", flush=True)
+
+
+def fill_once(self, i, c):  # layer-1 rows stand in for every boundary's received rows (timing only)
+    done = self.__dict__.setdefault("_filled", set())
+    if (i, c) not in done:
+        r0, r1 = self.recv_slices[c]
+        self.recv[i][r0:r1] = take(h1, self.mp.recv_ids[r0:r1])
+        done.add((i, c))
+
+
 report = {"ngram": n, "F": F, "N": N, "single_gpu_ms": round(t1, 4), "link_gbs_assumed": LINK_GBS, "P": {}}
 for P in (2, 4, 8):
-    ts, te, ghosts, link = [], [], [], 0
+    ts, tc, te, ghosts, link = [], [], [], [], 0
     for r in range(P):
-        mp = shard.middle_partition(g, r, P, chunks=CHUNKS)
+        mp = shard.middle_partition(g, r, P)
         inp = shard.middle_inputs(model, mp)
         buf = h1.clone()
 
@@ -80,41 +90,42 @@ for P in (2, 4, 8):
             te.append(timeit(lambda: shard.middle_forward(model, mp, x, inp)))
         finally:
             shard._exchange_rows = shard_exchange
-        # the bench's path: MiddleRunner (per-segment HIP graphs), the exchange's receive side filled locally
+        # the bench's path: MiddleRunner (per-segment HIP graphs), the exchange's receive side filled locally; one
+        # exchange after layer 1, and layer 1 in CHUNKS sub-ranges (each exchanged as soon as it is computed)
         runner_exchange = shard.MiddleRunner._exchange
-        def fill_once(self, i, c):  # layer-1 rows stand in for every boundary's received rows (timing only)
-            done = self.__dict__.setdefault("_filled", set())
-            if (i, c) not in done:
-                r0, r1 = self.recv_slices[c]
-                self.recv[i][r0:r1] = take(h1, self.mp.recv_ids[r0:r1])
-                done.add((i, c))
-
         shard.MiddleRunner._exchange = fill_once
         try:
             run = shard.MiddleRunner(model, mp, x, inp)
             ts.append(timeit(run))
+            del run
+            mpc = shard.middle_partition(g, r, P, chunks=CHUNKS)
+            run = shard.MiddleRunner(model, mpc, x, inp)
+            tc.append(timeit(run))
+            del run, mpc
         finally:
             shard.MiddleRunner._exchange = runner_exchange
-        del run
         ghosts.append(int(mp.recv_ids.numel()))
         link = max(link, max(mp.recv_counts))
         del mp, inp, buf
-    m = max(ts)
+    m, mc = max(ts), max(tc)
     row_b = F * 4
     xch = {f"{gb:g}": round(link * row_b / (gb * 1e9) * 1e3, 4) for gb in LINK_GBS}  # ms per layer boundary
-    est = {k: {"serial_ms": round(m + v, 4), "overlapped_ms": round(max(m, v), 4),
-               "speedup_serial": round(t1 / (m + v), 2), "speedup_overlapped": round(t1 / max(m, v), 2)}
+    # serial: one exchange after layer 1 (chunks = 1); overlapped bound: layer 1 in sub-ranges, the exchange hidden
+    # behind the compute as far as it goes (max of the two)
+    est = {k: {"serial_ms": round(m + v, 4), "overlapped_bound_ms": round(max(mc, v), 4),
+               "speedup_serial": round(t1 / (m + v), 2), "speedup_overlapped_bound": round(t1 / max(mc, v), 2)}
            for k, v in xch.items()}
-    report["P"][P] = {"rank_ms": [round(t, 4) for t in ts], "max_rank_ms": round(m, 4),
+    report["P"][P] = {"rank_ms_graphs": [round(t, 4) for t in ts], "max_rank_ms": round(m, 4),
+                      f"rank_ms_graphs_chunks{CHUNKS}": [round(t, 4) for t in tc], "max_rank_ms_chunked": round(mc, 4),
                       "eager_rank_ms": [round(t, 4) for t in te], "eager_max_rank_ms": round(max(te), 4),
                       "compute_speedup": round(t1 / m, 2), "ghost_rows_max": max(ghosts),
                       "ghost_MB_max": round(max(ghosts) * row_b / 1e6, 2), "max_rows_per_link": link,
                       "exchange_ms_per_link_rate": xch, "estimate": est}
-    print(f"P={P}: per-rank ms (graphs) {' '.join(f'{t:.4f}' for t in ts)}  max {m:.4f} (eager {max(te):.4f})  "
-          f"compute speedup {t1 / m:.2f}x  "
-          f"ghost rows/rank <= {max(ghosts)} ({max(ghosts) * row_b / 1e6:.1f} MB), busiest link {link} rows; "
-          + "; ".join(f"@{k} GB/s/link: exchange {v:.4f} ms -> {t1 / (m + v):.2f}x serial, {t1 / max(m, v):.2f}x "
-                      f"overlapped" for k, v in xch.items()), flush=True)
+    print(f"P={P}: max per-rank ms: graphs {m:.4f}, graphs + {CHUNKS} sub-ranges {mc:.4f}, eager {max(te):.4f}; "
+          f"compute speedup {t1 / m:.2f}x; ghost rows/rank <= {max(ghosts)} ({max(ghosts) * row_b / 1e6:.1f} MB), "
+          f"busiest link {link} rows; "
+          + "; ".join(f"@{k} GB/s/link: exchange {v:.4f} ms -> {t1 / (m + v):.2f}x serial, "
+                      f"<= {t1 / max(mc, v):.2f}x overlapped" for k, v in xch.items()), flush=True)
 if out:
     with open(out, "w") as f:
         json.dump(report, f, indent=1)

@@ -446,6 +446,42 @@ def test_middle_partition_4gram_every_rank_bitexact(pkg, cuda, monkeypatch):
     assert bool((seen == 1).all())
 
 
+@pytest.mark.timeout(600)
+def test_middle_partition_bf16_rank_bitexact(pkg, cuda, monkeypatch):
+    """bf16 mode through the middle partition (the CSR bf16 kernels over the rank's rows -- the middle-tile kernel is
+    fp32 -- and bf16 ghost rows): ranks 0 and 3 of P = 4 at 4-gram match the single-GPU bf16 forward. The
+    propagation rows are bit-identical; the bf16 dense kernel's accumulation order depends on the row count, so
+    its outputs agree to bf16 rounding (1 ulp), not bit for bit: |d| <= 2e-2 + 2e-2|ref| on the log-probs and
+    embeddings."""
+    from protgram_directgcn_amd import ops, shard
+    n, F = 4, 128
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    m = _model(pkg, [F, F, F], N, n).to(cuda).eval()
+    m.compute_dtype = torch.bfloat16
+    xd = torch.randn(N, F, generator=torch.Generator().manual_seed(1234)).to(cuda).to(torch.bfloat16)
+    conv = m.convs[0]
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    with torch.no_grad():
+        lp, emb = m(pkg.Data(x=xd, graph=g))
+        h1 = ops.layer_dense(ops.spmm3(g, xd), prm, 0, constant=conv.constant.detach(), res_x=xd, act=True)
+    assert h1.dtype == torch.bfloat16
+
+    def fill(self, i, c):
+        r0, r1 = self.recv_slices[c]
+        assert self.recv[i].dtype == torch.bfloat16  # bf16 rows on the wire in bf16 mode
+        self.recv[i][r0:r1] = h1[self.mp.recv_ids[r0:r1]]
+
+    monkeypatch.setattr(shard.MiddleRunner, "_exchange", fill)
+    for rank in (0, 3):
+        mp = shard.middle_partition(g, rank, 4, chunks=2)
+        lp2, emb2 = shard.MiddleRunner(m, mp, xd)()
+        torch.cuda.synchronize()
+        assert torch.equal(ops.spmm3(mp.own_csr, xd), ops.spmm3(g, xd)[mp.own])  # propagation: bit-identical
+        for got, ref in ((lp2, lp[mp.global_rows]), (emb2, emb[mp.global_rows])):
+            assert bool(((got.float() - ref.float()).abs() <= 2e-2 + 2e-2 * ref.float().abs()).all()), rank
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # config 5
 # ---------------------------------------------------------------------------------------------------------------

@@ -8,12 +8,13 @@ identity residuals), C=20 classes, eval mode, fp32. One step = one full model fo
 decoder, log_softmax, L2-normalised embeddings), inputs resident in HBM.
   edges/s = 3 * nnz * L / t_step   (each adjacency entry counted once per layer)
 
---gpus N (torchrun, one process per GPU; "scaling": "strong": total work fixed). Default --partition middle (complete
+--gpus N (torchrun, one process per GPU; "scaling": "strong": total work fixed). --partition middle (complete
 n-gram graphs, n >= 3): rank p owns the nodes a.M.b of a contiguous range of middle (n-2)-grams M and runs the
 middle-tile kernel over them; between the layers each rank receives exactly the ghost rows its middles read from
-their owners (one RCCL all_to_all_single; shard.middle_partition / middle_forward). --partition halo: each rank
+their owners (one RCCL all_to_all_single; shard.middle_partition / MiddleRunner). --partition halo: each rank
 recomputes the 1-hop halo of its rows in layer 1 on the CSR kernels, no collective (shard.halo_partition).
 --partition exchange: node-range rows and an RCCL all-gather of all layer-1 rows (shard.sharded_forward).
+Default (auto): halo up to 4 ranks, middle from 5.
 Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
 over ranks is reported. Rank 0 prints one JSON line.
 
@@ -60,11 +61,13 @@ def parse():
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
     ap.add_argument("--chunks", type=int, default=0, help="N>1: layer-boundary exchange in this many pieces, "
                     "overlapped with the compute (1 = one exchange after the layer; 0 = by the rank's share)")
-    ap.add_argument("--partition", choices=("middle", "halo", "exchange"), default="middle",
+    ap.add_argument("--partition", choices=("auto", "middle", "halo", "exchange"), default="auto",
                     help="N>1: 'middle' = middle (n-2)-gram ranges + RCCL ghost-row all_to_all per layer boundary "
-                    "(default; falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the "
-                    "(L-1)-hop halo of its rows (no collective on the data path); 'exchange' = node-range rows + RCCL "
-                    "all-gather of all rows per layer")
+                    "(falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the (L-1)-hop "
+                    "halo of its rows (no collective on the data path); 'exchange' = node-range rows + RCCL "
+                    "all-gather of all rows per layer; 'auto' (default) = halo up to 4 ranks, middle from 5 (at 4 ranks "
+                    "and fewer a rank's ghost rows go over one or three links: the exchange costs more than the halo's "
+                    "recompute, DESIGN.md 5c)")
     ap.add_argument("--no-graphs", action="store_true", help="N>1 middle partition: eager launches instead of the "
                     "per-segment HIP graphs")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
@@ -171,6 +174,8 @@ def main():
 
     part = hp = mp = None
     partition = args.partition
+    if partition == "auto":
+        partition = "halo" if world <= 4 else "middle"
     if world > 1 and partition == "middle" and (shard.ngram_shape(g) is None or shard.ngram_shape(g)[1] < 3):
         partition = "halo"
     if world > 1 and partition == "middle":

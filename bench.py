@@ -14,7 +14,9 @@ middle-tile kernel over them; between the layers each rank receives exactly the 
 their owners (one RCCL all_to_all_single; shard.middle_partition / MiddleRunner). --partition halo: each rank
 recomputes the 1-hop halo of its rows in layer 1 on the CSR kernels, no collective (shard.halo_partition).
 --partition exchange: node-range rows and an RCCL all-gather of all layer-1 rows (shard.sharded_forward).
-Default (auto): halo up to 4 ranks, middle from 5.
+--partition replicate: every rank runs the layers before the last over all rows (the single-GPU kernels) and the
+last layer over its middles only; no collective (MiddleRunner(replicate=True)).
+Default (auto): AUTO_PARTITION below (by rank count, from the round-3 per-rank measurements).
 Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
 over ranks is reported. Rank 0 prints one JSON line.
 
@@ -34,6 +36,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# --partition auto by rank count (absent: middle). Per-rank 4-gram times measured on one MI355X
+AUTO_PARTITION = {2: "replicate", 3: "replicate", 4: "halo"}
 
 
 def parse():
@@ -61,13 +65,14 @@ def parse():
     ap.add_argument("--extra", action="store_true", help="also time kernel variants / training step (stderr)")
     ap.add_argument("--chunks", type=int, default=0, help="N>1: layer-boundary exchange in this many pieces, "
                     "overlapped with the compute (1 = one exchange after the layer; 0 = by the rank's share)")
-    ap.add_argument("--partition", choices=("auto", "middle", "halo", "exchange"), default="auto",
+    ap.add_argument("--partition", choices=("auto", "middle", "replicate", "halo", "exchange"), default="auto",
                     help="N>1: 'middle' = middle (n-2)-gram ranges + RCCL ghost-row all_to_all per layer boundary "
                     "(falls back to 'halo' on graphs it does not take); 'halo' = each rank recomputes the (L-1)-hop "
                     "halo of its rows (no collective on the data path); 'exchange' = node-range rows + RCCL "
-                    "all-gather of all rows per layer; 'auto' (default) = halo up to 4 ranks, middle from 5 (at 4 ranks "
-                    "and fewer a rank's ghost rows go over one or three links: the exchange costs more than the halo's "
-                    "recompute, DESIGN.md 5c)")
+                    "all-gather of all rows per layer; 'replicate' = layers before the last over all rows on every "
+                    "rank, the last over the rank's middles (no collective); 'auto' (default) = AUTO_PARTITION by rank "
+                    "count (at few ranks a rank's ghost rows go over few links: the exchange costs more than "
+                    "recomputing, DESIGN.md 5c)")
     ap.add_argument("--no-graphs", action="store_true", help="N>1 middle partition: eager launches instead of the "
                     "per-segment HIP graphs")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
@@ -175,10 +180,17 @@ def main():
     part = hp = mp = None
     partition = args.partition
     if partition == "auto":
-        partition = "halo" if world <= 4 else "middle"
-    if world > 1 and partition == "middle" and (shard.ngram_shape(g) is None or shard.ngram_shape(g)[1] < 3):
+        partition = AUTO_PARTITION.get(world, "middle")
+    if (world > 1 and partition in ("middle", "replicate")
+            and (shard.ngram_shape(g) is None or shard.ngram_shape(g)[1] < 3)):
         partition = "halo"
-    if world > 1 and partition == "middle":
+    if world > 1 and partition == "replicate":
+        mp = shard.middle_partition(g, rank, world)
+        mid_in = shard.middle_inputs(model, mp)
+        mid_run = shard.MiddleRunner(model, mp, x, mid_in, graphs=not args.no_graphs, replicate=True)
+        log(f"[bench] replicate: every rank runs layers 1..{L - 1} over all {N} rows, rank {rank} the last layer "
+            f"over middles [{mp.m0}, {mp.m1}) = {mp.n_own} rows")
+    elif world > 1 and partition == "middle":
         # sub-ranges for the overlapped exchange only where a rank's share is large enough that a sub-range still
         # fills the GPU (a middle-tile launch has a fixed ~10 us start; at 4-gram, 8 ranks, 20k rows each, one
         # range is faster; at 5-gram, 400k rows each, four)
@@ -235,7 +247,7 @@ def main():
         ops.SPMM_EVENTS = []
         for _ in range(10):
             with torch.no_grad():
-                shard.middle_forward(model, mp, x, mid_in)
+                mid_run._run_eager()
         torch.cuda.synchronize()
         events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
     spmm_ms = [e0.elapsed_time(e1) for e0, e1 in events]
@@ -279,6 +291,9 @@ def main():
             reads = shard._middle_reads(mp.K, mp.ngram, mp.m0, mp.m1, mp.own.device).numel()
             comp = (g.ngram.mplan.numel() * 4 * (mp.m1 - mp.m0) // (N // mp.K ** 2) + reads * Fd * el
                     + mp.n_own * 3 * Fd * el)
+            if mid_run.replicate:  # L-1 whole-graph launches, then one over the rank's middles: their mean
+                kname = f"pg_spmm3_ngram_mid_f32 x{L - 1} + pg_spmm3_ngram_mid_rows_f32"
+                comp = ((L - 1) * g.compulsory_bytes(Fd, elem=el, gated=False) + comp) // L
         else:
             kname = "pg_spmm3_bf16" if args.bf16 else "pg_spmm3_f32"
             comp = mp.own_csr.compulsory_bytes(Fd, elem=el, gated=False)
@@ -324,10 +339,14 @@ def main():
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
                        "entry": ("trainer COO (edge_index_*/edge_weight_* -> csr_from_coo)" if entry == "coo"
                                  else "prebuilt Data.graph (build_propagation_csr)"),
-                       "parallelism": ("single" if world == 1 else f"middle_ghost_a2a_x{world}" if mp is not None
+                       "parallelism": ("single" if world == 1
+                                       else f"replicate_then_middle_x{world}" if mp is not None and mid_run.replicate
+                                       else f"middle_ghost_a2a_x{world}" if mp is not None
                                        else f"halo_recompute_x{world}" if hp is not None else f"node_range_x{world}"),
-                       "ghost_rows_rank0": int(mp.recv_ids.numel()) if mp is not None else None,
-                       "exchange_chunks": (mp.chunks if mp is not None else (args.chunks or 4) if part is not None else None),
+                       "ghost_rows_rank0": (int(mp.recv_ids.numel()) if mp is not None and not mid_run.replicate
+                                            else None),
+                       "exchange_chunks": (mp.chunks if mp is not None and not mid_run.replicate
+                                           else (args.chunks or 4) if part is not None else None),
                        "halo_rows_rank0": hp.layer_rows if hp is not None else None},
             "nodes_per_sec": round(N * L * args.steps / elapsed, 1),
             "roofline": roofline,

@@ -791,6 +791,13 @@ def middle_inputs(model, mp: MiddlePartition):
     return layers
 
 
+@torch.no_grad()
+def _full_inputs(conv):
+    """A layer's dense parameters and constant over every row (MiddleRunner's replicated layers)."""
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    return prm, (conv.constant.detach() if conv.use_vector_coeffs else None)
+
+
 def _owned_spmm3(mp: MiddlePartition, X: torch.Tensor) -> torch.Tensor:
     """Aggregates of the owned rows (owned-row order) from X in the global row layout: the middle-tile kernel over
     the owned middles where it takes the call (fp32, F % 16 == 0), else the CSR kernels over the owned rows' CSR."""
@@ -855,15 +862,18 @@ class MiddleRunner:
     to middle_forward's (and to the single-GPU forward's)."""
 
     def __init__(self, model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None, group=None,
-                 graphs: bool = True):
+                 graphs: bool = True, replicate: bool = False):
         self.model, self.mp, self.x, self.group = model, mp, x_full, group
         self.layers = inputs if inputs is not None else middle_inputs(model, mp)
         self.L = len(model.convs)
+        self.replicate = replicate
         dev = x_full.device
         self.dt = torch.bfloat16 if model.compute_dtype == torch.bfloat16 else x_full.dtype
         self.bufs = [torch.empty(mp.n, conv.in_channels, device=dev, dtype=self.dt) for conv in model.convs[1:]]
-        self.recv = [torch.empty(int(mp.recv_ids.numel()), conv.in_channels, device=dev, dtype=self.dt)
-                     for conv in model.convs[1:]]
+        nrecv = 0 if replicate else int(mp.recv_ids.numel())
+        self.recv = [torch.empty(nrecv, conv.in_channels, device=dev, dtype=self.dt) for conv in model.convs[1:]]
+        # replicate: every layer but the last over all rows, on every rank (the full parameters), into self.bufs
+        self.full = [_full_inputs(conv) for conv in model.convs[:-1]] if replicate else None
         self.hout = [torch.empty(mp.n_own, conv.out_channels, device=dev, dtype=self.dt) for conv in model.convs[:-1]]
         K2 = mp.K * mp.K
         self.row_bounds = [((a - mp.m0) * K2, (b - mp.m0) * K2) for a, b in mp.chunk_bounds]
@@ -895,19 +905,33 @@ class MiddleRunner:
 
     # ---- segments (graph bodies)
     def _prepare(self, i: int):
-        """Layer i's global-layout input and its residual rows (owned-row order)."""
+        """Layer i's global-layout input and its residual rows (owned-row order; replicated layers: all rows)."""
         mp, model = self.mp, self.model
         if i == 0:
             h = model._apply_pe(self.x)
             if model.compute_dtype == torch.bfloat16:
                 h = h.to(torch.bfloat16)
-            self.state["X"], self.state["res"] = h, ops.rows_gather(h, mp.own)
+            self.state["X"] = h
+            self.state["res"] = h if self.replicate and self.L > 1 else ops.rows_gather(h, mp.own)
+        elif self.replicate:
+            X = self.bufs[i - 1]  # the replicated layer's output, every row
+            self.state["X"] = X
+            self.state["res"] = X if i + 1 < self.L else ops.rows_gather(X, mp.own)
         else:
             X, h_prev = self.bufs[i - 1], self.hout[i - 1]
             ops.rows_scatter(h_prev, mp.own, X)
             if mp.world > 1 and self.recv[i - 1].size(0):
                 ops.rows_scatter(self.recv[i - 1], mp.recv_ids, X)
             self.state["X"], self.state["res"] = X, h_prev
+
+    def _compute_full(self, i: int):
+        """A replicated layer: the single-GPU layer over every row, into the next layer's global-layout input."""
+        conv, res = self.model.convs[i], self.model.res_projs[i]
+        prm, const = self.full[i]
+        W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
+        X = self.state["X"]
+        return ops.layer_dense(ops.spmm3(self.mp.graph, X), prm, 0 if conv.use_vector_coeffs else 1, constant=const,
+                               res_x=self.state["res"], W_res=W_res, b_res=b_res, act=True, out=self.bufs[i])
 
     def _compute(self, i: int, c: Optional[int]):
         """Layer i over chunk c's middles (c None: all owned middles); returns the layer output rows."""
@@ -936,8 +960,11 @@ class MiddleRunner:
 
     def _segment(self, i: int, c: Optional[int]):
         """One graph body: [layer input (first chunk)], chunk c of layer i, the rows it sends (or the head)."""
-        if c is None or c == 0:
+        if c is None or c <= 0:
             self._prepare(i)
+        if c == -1:
+            self._compute_full(i)
+            return None
         h = self._compute(i, c)
         if i + 1 < self.L:
             if self.mp.world > 1:
@@ -968,7 +995,9 @@ class MiddleRunner:
         self.works = []
 
     def _plan(self):
-        """The segment sequence: (layer, chunk) pairs; the last layer whole (chunk None)."""
+        """The segment sequence: (layer, chunk) pairs; the last layer whole (chunk None); replicated layers -1."""
+        if self.replicate:
+            return [(i, -1) for i in range(self.L - 1)] + [(self.L - 1, None)]
         seq = [(i, c) for i in range(self.L - 1) for c in range(self.mp.chunks)]
         return seq + [(self.L - 1, None)]
 
@@ -978,7 +1007,7 @@ class MiddleRunner:
             if c is None or c == 0:
                 self._wait()
             out = self._segment(i, c)
-            if c is not None:
+            if c is not None and c >= 0:
                 self._exchange(i, c)
         self._wait()
         return out
@@ -993,7 +1022,7 @@ class MiddleRunner:
             with torch.no_grad(), torch.cuda.graph(gph, pool=pool):
                 out = self._segment(i, c)
             gph.replay()  # this segment's outputs for the next capture's inputs
-            if c is not None:
+            if c is not None and c >= 0:
                 self._exchange(i, c)
             self.graphs.append(gph)
         self._wait()
@@ -1010,7 +1039,7 @@ class MiddleRunner:
             if c is None or c == 0:
                 self._wait()
             gph.replay()
-            if c is not None:
+            if c is not None and c >= 0:
                 self._exchange(i, c)
         self._wait()
         return self.out

@@ -416,6 +416,16 @@ def _middle_rank_check(pkg, m, g, xd, lp_ref, emb_ref, rank, world, monkeypatch)
             lp2, emb2 = run()
             torch.cuda.synchronize()
             assert torch.equal(lp2, lp) and torch.equal(emb2, emb)
+    # replicated first layer (the bench's partition at 2 ranks): layer 1 over every row on this rank, the last layer
+    # over its middles; no exchange at all
+    with monkeypatch.context() as mpc:
+        mpc.setattr(shard.MiddleRunner, "_exchange", lambda *a: pytest.fail("replicate must not exchange"))
+        run = shard.MiddleRunner(m, mp, xd, replicate=True)
+        assert len(run.graphs) == len(m.convs)
+        lp3, emb3 = run()
+        torch.cuda.synchronize()
+        assert torch.equal(run.bufs[0], h1)
+        assert torch.equal(lp3, lp) and torch.equal(emb3, emb)
     return mp
 
 

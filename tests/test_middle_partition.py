@@ -143,6 +143,8 @@ def _worker(rank, world, port, out_q):
         mpc = shard.middle_partition(g, rank, world, chunks=2)  # layer 1 in two sub-ranges, exchanged per sub-range
         lp3, emb3 = shard.MiddleRunner(model, mpc, x)()
         ok = ok and torch.equal(lp3, lp) and torch.equal(emb3, emb)
+        lp4, emb4 = shard.MiddleRunner(model, mp_, x, replicate=True)()  # layer 1 on every row, no exchange
+        ok = ok and torch.allclose(lp4, lp, rtol=1e-5, atol=1e-6) and torch.allclose(emb4, emb, rtol=1e-5, atol=1e-6)
         out_q.put((rank, int(rows.numel()), bool(ok), float((lp - lp_r[rows]).abs().max())))
     finally:
         dist.destroy_process_group()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-rank cost of the halo-recompute partition, measured on one GPU: for P in 1,2,4,8 every rank's forward
+"""Per-rank cost of the halo-recompute partition, measured on one GPU: for P in 1,2,3,4,8 every rank's forward
 (shard.halo_forward, exactly the work that rank does on its own GPU: the path has no collective) is timed
 in turn with HIP events; the max over ranks is the P-GPU step time up to launch skew.
 usage: python tools/halo_probe.py [ngram] [F] [reps]"""
@@ -43,7 +43,7 @@ def timeit(fn):
 
 t1 = timeit(lambda: model(data))
 print(f"single GPU: {t1:.4f} ms/step")
-for P in (2, 4, 8):
+for P in (2, 3, 4, 8):
     ts, rows = [], []
     for r in range(P):
         hp = shard.halo_partition(g, r, P, 2)

@@ -5,7 +5,8 @@ HIP graphs) and eagerly (shard.middle_forward) -- its ghost-row all_to_all repla
 (the received rows are taken from a precomputed layer-1 output, once: the timed runner forward is the rank's local
 work only). The exchange itself is priced from the measured byte counts: per rank pair one xGMI link, so the
 all_to_all takes max over (sender, receiver) pairs of bytes / link rate; it is printed for the stated link rates,
-without and with overlap (max(compute, exchange) vs compute + exchange).
+without and with overlap (max(compute, exchange) vs compute + exchange). The replicate mode (layers before the last
+over all rows, no exchange) is timed as is: its per-rank time is the step's.
 usage: python tools/middle_probe.py [ngram] [F] [reps] [--out FILE]"""
 import json
 import os
@@ -73,8 +74,8 @@ def fill_once(self, i, c):  # layer-1 rows stand in for every boundary's receive
 
 
 report = {"ngram": n, "F": F, "N": N, "single_gpu_ms": round(t1, 4), "link_gbs_assumed": LINK_GBS, "P": {}}
-for P in (2, 4, 8):
-    ts, tc, te, ghosts, link = [], [], [], [], 0
+for P in (2, 3, 4, 8):
+    ts, tc, te, tr, ghosts, link = [], [], [], [], [], 0
     for r in range(P):
         mp = shard.middle_partition(g, r, P)
         inp = shard.middle_inputs(model, mp)
@@ -102,6 +103,9 @@ for P in (2, 4, 8):
             run = shard.MiddleRunner(model, mpc, x, inp)
             tc.append(timeit(run))
             del run, mpc
+            run = shard.MiddleRunner(model, mp, x, inp, replicate=True)  # no exchange: its time is the step's
+            tr.append(timeit(run))
+            del run
         finally:
             shard.MiddleRunner._exchange = runner_exchange
         ghosts.append(int(mp.recv_ids.numel()))
@@ -118,10 +122,13 @@ for P in (2, 4, 8):
     report["P"][P] = {"rank_ms_graphs": [round(t, 4) for t in ts], "max_rank_ms": round(m, 4),
                       f"rank_ms_graphs_chunks{CHUNKS}": [round(t, 4) for t in tc], "max_rank_ms_chunked": round(mc, 4),
                       "eager_rank_ms": [round(t, 4) for t in te], "eager_max_rank_ms": round(max(te), 4),
+                      "replicate_rank_ms": [round(t, 4) for t in tr], "replicate_max_rank_ms": round(max(tr), 4),
+                      "replicate_speedup": round(t1 / max(tr), 2),
                       "compute_speedup": round(t1 / m, 2), "ghost_rows_max": max(ghosts),
                       "ghost_MB_max": round(max(ghosts) * row_b / 1e6, 2), "max_rows_per_link": link,
                       "exchange_ms_per_link_rate": xch, "estimate": est}
-    print(f"P={P}: max per-rank ms: graphs {m:.4f}, graphs + {CHUNKS} sub-ranges {mc:.4f}, eager {max(te):.4f}; "
+    print(f"P={P}: replicate-first-layers {max(tr):.4f} ms = {t1 / max(tr):.2f}x (no exchange); "
+          f"max per-rank ms: graphs {m:.4f}, graphs + {CHUNKS} sub-ranges {mc:.4f}, eager {max(te):.4f}; "
           f"compute speedup {t1 / m:.2f}x; ghost rows/rank <= {max(ghosts)} ({max(ghosts) * row_b / 1e6:.1f} MB), "
           f"busiest link {link} rows; "
           + "; ".join(f"@{k} GB/s/link: exchange {v:.4f} ms -> {t1 / (m + v):.2f}x serial, "

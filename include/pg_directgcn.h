@@ -176,6 +176,18 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* args, float* packed, void* stre
  * any other case returns PG_ERR_UNSUPPORTED without launching (callers then pack and call again). */
 int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uint32_t flags, void* stream);
 
+/* pg_directgcn_dense_f32 over the rows of a middle range in middle-major order (the rows
+ * pg_spmm3_ngram_mid_rows_f32 writes: row m = 400 (M - m0) + 20 a + b for the middles m0, m0 + 1, ..., K = 20),
+ * with the residual rows read (map_res != 0) and / or the output rows written (map_y != 0) at the global n-gram
+ * row a.M.b = a Kn1 + 20 M + b (Kn1 = K^(n-1)) of res_x / Y instead of at row m: a rank of the multi-GPU middle
+ * partition reads its layer input and writes its layer output in the global row layout directly (no row gather /
+ * scatter around the launch). Same arithmetic as pg_directgcn_dense_f32 (bit-identical rows). Only the pipelined
+ * split-bf16 kernel's shape (F_in = F_out = 128, no W_res, no rows, 16-B aligned): PG_ERR_UNSUPPORTED otherwise.
+ * Requires args->M a multiple of 400 and m0 + M / 400 <= Kn1 / 20. (Replaces, for a middle range, the same
+ * protgram_directgcn.py:100-133 + :213-215 as pg_directgcn_dense_f32.) */
+int pg_directgcn_dense_ngram_rows_f32(const pg_layer_args_t* args, const float* packed, int64_t Kn1, int64_t m0,
+                                      int32_t map_res, int32_t map_y, uint32_t flags, void* stream);
+
 /* pg_spmm3_f32 with the DirectGCN gates applied at the store: Z_q[i] = s_q(i) * (A_q X)[i], s_in = c_all*c_dir*c_in,
  * s_out = c_all*c_dir*c_out, s_und = c_all*c_und (protgram_directgcn.py:116-133), from the C_* / gate_mode fields
  * of `gates` (rows must be NULL). The inference producer for pg_directgcn_dense_f32 with

@@ -91,6 +91,8 @@ SIGNATURES = {
     "pg_directgcn_packed_floats": (c_i64, [c_i64, c_i64, ctypes.c_int]),
     "pg_directgcn_pack_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_vp]),
     "pg_directgcn_dense_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_u32, c_vp]),
+    "pg_directgcn_dense_ngram_rows_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, c_i64, c_i64, c_i32, c_i32,
+                                                         c_u32, c_vp]),
     "pg_directgcn_dense_bwd_workspace": (c_i64, [ctypes.POINTER(LayerArgs)]),
     "pg_directgcn_dense_bwd_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
                                                   c_u32, c_vp]),

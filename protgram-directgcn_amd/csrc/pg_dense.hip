@@ -62,7 +62,20 @@ struct DenseP {
     int rawW;
     const float *Wq0, *Wq1, *Wq2, *Wsh;
     const float *bm0, *bs0, *bm1, *bs1, *bm2, *bs2;
+    // n-gram row map (pg_directgcn_dense_ngram_rows_f32; pipelined split-bf16 kernel only): row m of Z (middle-major
+    // rows of the middles map_m0, map_m0 + 1, ...: m = 400 (M - map_m0) + 20 a + b) reads its residual row (map_res)
+    // and / or writes its output row (map_y) at the global n-gram row a.M.b = a K^(n-1) + 20 M + b
+    int64_t map_kn1, map_m0;
+    int map_res, map_y;
 };
+
+// global n-gram row of middle-major row m (K = 20: 400 rows per middle); see DenseP::map_*
+__device__ __forceinline__ int64_t ngram_row(const DenseP& p, int64_t m) {
+    const int r = (int)m;  // rows of one launch < 2^31 (checked on the host)
+    const int q = r / 400, w = r - 400 * q;
+    const int a = w / 20, b = w - 20 * a;
+    return (int64_t)a * p.map_kn1 + (p.map_m0 + q) * 20 + b;
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float4 scale4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.z * s, a.w * s); }
@@ -835,7 +848,9 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         asm volatile("" : "+v"(ln));
         const int rr = min(2 * wave + (ln >> 5), rmax);
         const float* cb = has_const ? p.constant + m0 * p.ld_const + (rr * (int)p.ld_const) : p.Z + m0 * p.ldz;
-        const float* rb = id_res ? p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res) : p.Z + m0 * p.ldz;
+        const float* rb = !id_res    ? p.Z + m0 * p.ldz
+                          : p.map_res ? p.res_x + ngram_row(p, m0 + rr) * p.ld_res
+                                      : p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res);
         glds16(cb + 4 * (ln & 31), Cs + wave * 256);
         glds16(rb + 4 * (ln & 31), Rs + wave * 256);
     };
@@ -971,7 +986,8 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                     y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
                 }
                 {
-                    *reinterpret_cast<float4*>(p.Y + (m0 + er) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
+                    const int64_t yr = p.map_y ? ngram_row(p, m0 + er) : m0 + er;
+                    *reinterpret_cast<float4*>(p.Y + yr * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
                     y_pending = true;
                 }
             }
@@ -1034,7 +1050,8 @@ int pg_directgcn_pack_f32(const pg_layer_args_t* a, float* packed, void* stream)
     return pg::check_launch("pg_directgcn_pack_f32");
 }
 
-int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32_t flags, void* stream) {
+static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t flags, const int64_t* ngmap,
+                        void* stream) {
     PG_REQUIRE(a != nullptr, "null args");
     PG_REQUIRE(a->M >= 0 && a->F_in > 0 && a->F_out > 0 && a->F_in < (1 << 20) && a->F_out < (1 << 20),
                "bad shape M=%lld F_in=%lld F_out=%lld", (long long)a->M, (long long)a->F_in, (long long)a->F_out);
@@ -1091,6 +1108,12 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
+    if (ngmap) {  // {Kn1, m0, map_res, map_y}
+        p.map_kn1 = ngmap[0];
+        p.map_m0 = ngmap[1];
+        p.map_res = ngmap[2] ? 1 : 0;
+        p.map_y = ngmap[3] ? 1 : 0;
+    }
     p.vec_out = (a->F_out % 4 == 0) && (a->ldy % 4 == 0) && pg::aligned16(a->Y) &&
                 (!a->constant || (a->ld_const % 4 == 0 && pg::aligned16(a->constant))) &&
                 (!a->res_x || a->W_res || (a->ld_res % 4 == 0 && pg::aligned16(a->res_x)));
@@ -1110,6 +1133,8 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
     if (!(flags & PG_FLAG_DENSE_TILED) && ws_shape_ok && a->ldz < (1 << 24) && a->rows == nullptr &&
         (!a->res_x || a->ld_res < (1 << 24)) &&
         ((a->F_in == 128 && !a->W_res) || (a->F_in == 64 && a->W_res))) {
+        if (ngmap && a->F_in != 128)
+            return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_ngram_rows_f32: F_in = F_out = 128 only");
         int dev = 0, ncu = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
@@ -1133,6 +1158,9 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         }
         return pg::check_launch("pg_directgcn_dense_f32");
     }
+    if (ngmap)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_ngram_rows_f32: needs the pipelined split-bf16 "
+                                                 "kernel's shape (F_in = F_out = 128, no W_res, no row map, aligned)");
     if (p.rawW)
         return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights need the pipelined "
                                                  "split-bf16 kernel (F_in = F_out = 128, no row map)");
@@ -1145,6 +1173,23 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
         else hipLaunchKernelGGL((dense_kernel<128, 64, 8, false>), dim3((unsigned)nb), dim3(512), 0, s, p);
     }
     return pg::check_launch("pg_directgcn_dense_f32");
+}
+
+int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32_t flags, void* stream) {
+    return dense_launch(a, packed, flags, nullptr, stream);
+}
+
+int pg_directgcn_dense_ngram_rows_f32(const pg_layer_args_t* a, const float* packed, int64_t Kn1, int64_t m0,
+                                      int32_t map_res, int32_t map_y, uint32_t flags, void* stream) {
+    PG_REQUIRE(a != nullptr, "null args");
+    PG_REQUIRE(Kn1 >= 20 && Kn1 % 20 == 0 && m0 >= 0 && m0 < Kn1, "bad n-gram map (Kn1 = %lld, m0 = %lld)",
+               (long long)Kn1, (long long)m0);
+    PG_REQUIRE(a->M % 400 == 0 && a->M < (int64_t(1) << 31), "rows must be whole middles (M = %lld)", (long long)a->M);
+    PG_REQUIRE(!map_res || a->res_x, "map_res needs res_x");
+    PG_REQUIRE(m0 + a->M / 400 <= Kn1 / 20, "middles [%lld, %lld) past the graph's %lld", (long long)m0,
+               (long long)(m0 + a->M / 400), (long long)(Kn1 / 20));
+    const int64_t map[4] = {Kn1, m0, map_res, map_y};
+    return dense_launch(a, packed, flags, map, stream);
 }
 
 }  // extern "C"

@@ -483,6 +483,47 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
     return Y
 
 
+def layer_dense_ngram_rows(Z, prm: dict, gate_mode: int, Kn1: int, m0: int, constant=None, res_x=None,
+                           map_res: bool = False, out: Optional[torch.Tensor] = None, map_out: bool = False,
+                           act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None):
+    """pg_directgcn_dense_ngram_rows_f32: layer_dense over the middle-major rows of the middles m0, m0 + 1, ...
+    (spmm3_middles' rows), with the residual rows read (map_res) and / or the output rows written (map_out) at their
+    global n-gram rows of res_x / out (Kn1 = K^(n-1)). Returns the output tensor (out when map_out), or None when
+    the shape is not the pipelined split-bf16 kernel's (fp32, F_in = F_out = 128, identity residual): the caller
+    then runs layer_dense on gathered rows."""
+    lib = load_library()
+    _require_gpu(Z)
+    if _is_bf16(Z) or Z.dtype != torch.float32:
+        return None
+    M = Z.size(0)
+    F_out = prm["W_main_in"].size(0)
+    if map_out:
+        if out is None or out.dtype != torch.float32 or out.stride(1) != 1 or out.size(1) != F_out:
+            raise ValueError("map_out needs a row-major fp32 out [n_rows, F_out] in the global row layout")
+        Y = out
+    elif out is not None:
+        if out.shape != (M, F_out) or out.dtype != torch.float32 or out.stride(1) != 1 or out.device != Z.device:
+            raise ValueError("out must be a row-major fp32 [M, F_out] tensor on Z's device")
+        Y = out
+    else:
+        Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
+    if map_res and (res_x is None or res_x.dtype != torch.float32):
+        return None
+    a, keep = _layer_args(Z, prm, gate_mode, None, constant, res_x, None, act, slope)
+    a.Y, a.ldy = _p(Y), Y.stride(0)
+    raw = [_f32c(prm[k].detach()) for k in _PACK_KEYS]
+    (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
+     a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared) = [_p(t) for t in raw]
+    fl = default_flags() if flags is None else flags
+    rc = lib.pg_directgcn_dense_ngram_rows_f32(ctypes.byref(a), None, int(Kn1), int(m0), int(bool(map_res)),
+                                               int(bool(map_out)), fl, _stream(Z))
+    del keep, raw
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_directgcn_dense_ngram_rows_f32")
+    return Y
+
+
 def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags):
     lib = load_library()
     packed, p16 = pack_weights_bf16(prm, W_res, b_res)

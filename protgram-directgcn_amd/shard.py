@@ -889,6 +889,15 @@ class MiddleRunner:
             off += k
         # the CSR path's row blocks (bf16 / no middle plan), cut before any capture (slicing reads rowptr on the host)
         self.csr_chunks = [_rows_slice(mp.own_csr, r0, r1, None) for r0, r1 in self.row_bounds]
+        # mapped: the dense kernel reads the residual rows and writes the output rows of this rank's middles in the
+        # global row layout itself (pg_directgcn_dense_ngram_rows_f32): no residual gather, no scatter of the own
+        # rows; only the received rows are scattered. fp32 on the GPU, every layer 128 -> 128 with an identity
+        # residual (the pipelined split-bf16 kernel's shape); otherwise rows_gather / rows_scatter around the launch
+        self.mapped = (x_full.is_cuda and self.dt == torch.float32 and mp.K == 20
+                       and all(cv.in_channels == 128 and cv.out_channels == 128 for cv in model.convs)
+                       and not any(isinstance(r, nn.Linear) for r in model.res_projs))
+        self.Kn1 = mp.K ** (mp.ngram - 1)
+        self.send_glob = mp.own[mp.send_pos] if mp.world > 1 else None  # the sent rows' global ids
         backend = dist.get_backend(group) if (mp.world > 1 and dist.is_initialized()) else None
         self.sync = (not x_full.is_cuda) or backend == "gloo"
         self.state = {}
@@ -912,17 +921,24 @@ class MiddleRunner:
             if model.compute_dtype == torch.bfloat16:
                 h = h.to(torch.bfloat16)
             self.state["X"] = h
-            self.state["res"] = h if self.replicate and self.L > 1 else ops.rows_gather(h, mp.own)
+            if self.replicate and self.L > 1:
+                self.state["res"] = h
+            else:  # mapped: the dense kernel reads the residual rows from h itself
+                self.state["res"] = None if self.mapped else ops.rows_gather(h, mp.own)
         elif self.replicate:
             X = self.bufs[i - 1]  # the replicated layer's output, every row
             self.state["X"] = X
-            self.state["res"] = X if i + 1 < self.L else ops.rows_gather(X, mp.own)
+            if i + 1 < self.L:
+                self.state["res"] = X
+            else:
+                self.state["res"] = None if self.mapped else ops.rows_gather(X, mp.own)
         else:
             X, h_prev = self.bufs[i - 1], self.hout[i - 1]
-            ops.rows_scatter(h_prev, mp.own, X)
+            if not self.mapped:  # mapped: layer i - 1's dense kernel wrote the own rows into X
+                ops.rows_scatter(h_prev, mp.own, X)
             if mp.world > 1 and self.recv[i - 1].size(0):
                 ops.rows_scatter(self.recv[i - 1], mp.recv_ids, X)
-            self.state["X"], self.state["res"] = X, h_prev
+            self.state["X"], self.state["res"] = X, None if self.mapped else h_prev
 
     def _compute_full(self, i: int):
         """A replicated layer: the single-GPU layer over every row, into the next layer's global-layout input."""
@@ -942,7 +958,7 @@ class MiddleRunner:
             (a, b), (r0, r1) = (mp.m0, mp.m1), (0, mp.n_own)
         else:
             (a, b), (r0, r1) = mp.chunk_bounds[c], self.row_bounds[c]
-        X, res_x = self.state["X"], self.state["res"][r0:r1]
+        X = self.state["X"]
         if mp.graph.ngram is not None and ops._mid_ok(mp.graph, X, ops.default_flags()):
             Z = ops.spmm3_middles(mp.graph, X, a, b)
         else:
@@ -953,6 +969,14 @@ class MiddleRunner:
                 prm[k] = prm[k][r0:r1]
             const = const[r0:r1] if const is not None else None
         gate_mode = 0 if conv.use_vector_coeffs else 1
+        if self.mapped:  # residual rows from X, output rows into the next layer's input (global layout)
+            last = i + 1 == self.L
+            y = ops.layer_dense_ngram_rows(Z, prm, gate_mode, self.Kn1, a, constant=const, res_x=X, map_res=True,
+                                           out=None if last else self.bufs[i], map_out=not last, act=True)
+            if y is None:
+                raise RuntimeError("pg_directgcn_dense_ngram_rows_f32 did not take the layer's shape")
+            return y
+        res_x = self.state["res"][r0:r1]
         W_res, b_res = ((res.weight.detach(), res.bias.detach()) if isinstance(res, nn.Linear) else (None, None))
         out = self.hout[i][r0:r1] if i + 1 < self.L else None
         return ops.layer_dense(Z, prm, gate_mode, constant=const, res_x=res_x, W_res=W_res, b_res=b_res, act=True,
@@ -969,7 +993,10 @@ class MiddleRunner:
         if i + 1 < self.L:
             if self.mp.world > 1:
                 s0, s1 = self.send_slices[c]
-                self.state[("send", i, c)] = ops.rows_gather(self.hout[i], self.mp.send_pos[s0:s1])
+                if self.mapped:
+                    self.state[("send", i, c)] = ops.rows_gather(self.bufs[i], self.send_glob[s0:s1])
+                else:
+                    self.state[("send", i, c)] = ops.rows_gather(self.hout[i], self.mp.send_pos[s0:s1])
             return None
         return self.model.head(h)
 

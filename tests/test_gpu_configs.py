@@ -412,6 +412,7 @@ def _middle_rank_check(pkg, m, g, xd, lp_ref, emb_ref, rank, world, monkeypatch)
         mpc.setattr(shard.MiddleRunner, "_exchange", fill)
         run = shard.MiddleRunner(m, mpc_, xd)
         assert run.graphs is not None and len(run.graphs) == 3 * (len(m.convs) - 1) + 1
+        assert run.mapped == (xd.size(1) == 128)  # 128-wide fp32 layers: the dense kernel maps its rows itself
         for _ in range(2):
             lp2, emb2 = run()
             torch.cuda.synchronize()

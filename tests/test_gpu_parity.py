@@ -1109,3 +1109,43 @@ def test_rows_gather_scatter(pkg, cuda, dtype, F):
     ref[idx] = src[idx]
     assert torch.equal(dst, ref)
     assert ops.rows_gather(src, idx[:0]).shape == (0, F)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m0,nm", [(4, 37, 13), (3, 0, 20)])
+def test_dense_ngram_rows_map(pkg, cuda, n, m0, nm):
+    """pg_directgcn_dense_ngram_rows_f32 (the middle partition's dense launch): over the middle-major rows of the
+    middles [m0, m0 + nm), reading the residual and writing the output at the global n-gram rows a.M.b, it equals
+    layer_dense on the gathered residual rows bit for bit, and writes no other row."""
+    from protgram_directgcn_amd import ops
+    K, F = 20, 128
+    N, Kn1 = K ** n, K ** (n - 1)
+    gen = torch.Generator().manual_seed(n)
+    M_ = torch.arange(m0, m0 + nm).view(-1, 1, 1)
+    a = torch.arange(K).view(1, -1, 1)
+    b = torch.arange(K).view(1, 1, -1)
+    rows = (a * Kn1 + M_ * K + b).reshape(-1).to(cuda)  # middle-major order
+    R = rows.numel()
+    Z = torch.randn(R, 3 * F, generator=gen).to(cuda)
+    X = torch.randn(N, F, generator=gen).to(cuda)
+    prm = {k: torch.randn(F, F, generator=gen).mul_(0.05).to(cuda)
+           for k in ("W_main_in", "W_main_out", "W_undirected", "W_shared")}
+    for k in ("b_main_in", "b_dir_shared_in", "b_main_out", "b_dir_shared_out", "b_undirected", "b_undirected_shared"):
+        prm[k] = torch.randn(F, generator=gen).mul_(0.1).to(cuda)
+    for k in ("C_in", "C_out", "C_directed", "C_undirected", "C_all"):
+        prm[k] = (torch.rand(R, 1, generator=gen) + 0.5).to(cuda)
+    const = torch.randn(R, F, generator=gen).to(cuda)
+    ref = ops.layer_dense(Z, prm, 0, constant=const, res_x=X[rows], act=True)
+    Y = torch.full((N, F), float("nan"), device=cuda)
+    got = ops.layer_dense_ngram_rows(Z, prm, 0, Kn1, m0, constant=const, res_x=X, map_res=True, out=Y, map_out=True,
+                                     act=True)
+    torch.cuda.synchronize()
+    assert got is Y
+    assert torch.equal(Y[rows], ref)
+    keep = torch.ones(N, dtype=torch.bool, device=cuda)
+    keep[rows] = False
+    assert bool(torch.isnan(Y[keep]).all())
+    compact = ops.layer_dense_ngram_rows(Z, prm, 0, Kn1, m0, constant=const, res_x=X, map_res=True, act=True)
+    assert torch.equal(compact, ref)  # residual mapped, output compact (the last layer)
+    with pytest.raises(Exception):  # a partial middle is refused on the host
+        ops.layer_dense_ngram_rows(Z[:399], prm, 0, Kn1, m0, res_x=X, map_res=True, act=True)

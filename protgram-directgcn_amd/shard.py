@@ -1040,21 +1040,33 @@ class MiddleRunner:
         return out
 
     def _capture(self):
+        """Capture every compute segment once (setup). No collective is in flight while a segment is captured:
+        each exchange is drained (host sync) before the next capture begins, and the capture mode is thread-local,
+        so the collective library's own threads (progress, watchdog) cannot invalidate it. If the capture fails
+        anyway, the runner stays eager (a warning on stderr), with the same results."""
         self.graphs = []
         pool = torch.cuda.graph_pool_handle()
-        for i, c in self._plan():
-            if c is None or c == 0:
+        try:
+            for i, c in self._plan():
+                gph = torch.cuda.CUDAGraph()
+                with torch.no_grad(), torch.cuda.graph(gph, pool=pool, capture_error_mode="thread_local"):
+                    out = self._segment(i, c)
+                gph.replay()  # this segment's outputs for the next capture's inputs
+                if c is not None and c >= 0:
+                    self._exchange(i, c)
                 self._wait()
-            gph = torch.cuda.CUDAGraph()
-            with torch.no_grad(), torch.cuda.graph(gph, pool=pool):
-                out = self._segment(i, c)
-            gph.replay()  # this segment's outputs for the next capture's inputs
-            if c is not None and c >= 0:
-                self._exchange(i, c)
-            self.graphs.append(gph)
-        self._wait()
+                torch.cuda.synchronize()
+                self.graphs.append(gph)
+        except RuntimeError as e:  # pragma: no cover - depends on the collective library
+            import sys
+            print(f"[MiddleRunner] HIP graph capture failed ({e}); running the segments eagerly", file=sys.stderr)
+            self.graphs = None
+            self.works = []
+            torch.cuda.synchronize()
+            with torch.no_grad():
+                out = self._run_eager()
+            torch.cuda.synchronize()
         self.out = out
-        torch.cuda.synchronize()
 
     @torch.no_grad()
     def __call__(self):

@@ -274,7 +274,8 @@ def main():
     ngram = (all(gi.ngram is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm
              and Fd in (64, 128, 256))
     if args.bf16:
-        kname = "pg_spmm3_bf16"
+        kname = ("pg_spmm3_ngram_mid_bf16" if all(gi.ngram is not None and gi.ngram.mplan is not None
+                                                  for gi in launch_graphs) and Fd % 16 == 0 else "pg_spmm3_bf16")
     elif args.fused_norm:
         kname = "pg_spmm3_fusednorm_f32"
     elif ngram:  # n-gram tile kernel; inference gates the aggregates at its store
@@ -285,14 +286,16 @@ def main():
         kname = "pg_spmm3_gated_f32" if gated else "pg_spmm3_f32"
     comp = sum(gi.compulsory_bytes(Fd, elem=el, gated=gated) for gi in launch_graphs) // len(launch_graphs)
     if mp is not None:  # a rank's launch: its middles' plan share, the rows they read once, its rows' aggregates
-        mid_launch = ngram and g.ngram.mplan is not None and Fd % 16 == 0 and not args.bf16
+        mid_launch = (g.ngram is not None and g.ngram.mplan is not None and Fd % 16 == 0 and not args.fused_norm
+                      and (args.bf16 or ngram))
         if mid_launch:
-            kname = "pg_spmm3_ngram_mid_rows_f32"
+            kname = "pg_spmm3_ngram_mid_rows_" + ("bf16" if args.bf16 else "f32")
             reads = shard._middle_reads(mp.K, mp.ngram, mp.m0, mp.m1, mp.own.device).numel()
             comp = (g.ngram.mplan.numel() * 4 * (mp.m1 - mp.m0) // (N // mp.K ** 2) + reads * Fd * el
                     + mp.n_own * 3 * Fd * el)
             if mid_run.replicate:  # L-1 whole-graph launches, then one over the rank's middles: their mean
-                kname = f"pg_spmm3_ngram_mid_f32 x{L - 1} + pg_spmm3_ngram_mid_rows_f32"
+                sfx = "bf16" if args.bf16 else "f32"
+                kname = f"pg_spmm3_ngram_mid_{sfx} x{L - 1} + pg_spmm3_ngram_mid_rows_{sfx}"
                 comp = ((L - 1) * g.compulsory_bytes(Fd, elem=el, gated=False) + comp) // L
         else:
             kname = "pg_spmm3_bf16" if args.bf16 else "pg_spmm3_f32"

@@ -252,6 +252,15 @@ int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, cons
  * and own rows), Z in MIDDLE-MAJOR order: row (M - m_begin) K^2 + a K + b holds node a.M.b. */
 int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                                 int64_t m_begin, int64_t m_end, float* Z, int64_t ldz, uint32_t flags, void* stream);
+/* bf16 mode (config 5): the same kernels on bf16 rows of X and Z (ldx, ldz in elements; X rows 16-B aligned, Z rows
+ * 8-B aligned), the weights, products and sums fp32, each aggregate rounded once to bf16 (RNE) at the store -- the
+ * bf16 model's contract (every sum fp32, one rounding), as pg_spmm3_bf16. Sources are staged as bf16 (half the LDS
+ * and HBM bytes of the fp32 kernel) and widened exactly when read. */
+int pg_spmm3_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx, int64_t F,
+                            uint16_t* Z, int64_t ldz, uint32_t flags, void* stream);
+int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx,
+                                 int64_t F, int64_t m_begin, int64_t m_end, uint16_t* Z, int64_t ldz, uint32_t flags,
+                                 void* stream);
 
 /* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
  * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).

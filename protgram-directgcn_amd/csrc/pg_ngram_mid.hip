@@ -32,6 +32,9 @@
 // MFMA sums in groups of 4 c: out-slots, then the diagonal by a VALU FMA, then in-slots) in another order than the
 // reference's scatter_add: within fp32 rounding of it (|d| <= 1e-5 + 1e-5|ref|), like pg_spmm3_ngram_f32. Zero
 // weights add 0 * x: X must be finite.
+#include <type_traits>
+
+#include "pg_bf16_util.h"
 #include "pg_common.h"
 
 namespace {
@@ -52,16 +55,28 @@ constexpr int XPO = 0;                              // out fragments
 constexpr int XPI = XK * 4 * XS * 64;               // in fragments (25,600 floats after the out ones)
 constexpr int XPD = 2 * XPI;                        // diagonal weights [a][b][k]
 constexpr int XMB = XPD + XR * 3;                   // floats per middle: 52,400
-// LDS image (bytes)
-constexpr int LOUT = 0;                             // out-sources [b][c][16 f]   400 rows x 64 B
 constexpr int XCB = XK + 1;                         // in-source c-block rows (one pad row: bank offset 16)
-constexpr int LIN = LOUT + XR * 64;                 // in-sources  [c][a (+pad)][16 f]
-constexpr int LINB = (XK * XCB * 64 + 1023) / 1024 * 1024;  // in-region bytes: whole LDS-DMA wave-instructions
-constexpr int LSELF = LIN + LINB;                   // self rows   [a][b][16 f]
-constexpr int LPART = LSELF + XR * 64;              // partial     [a][row k K + b (3K)][16 f] fp32
-constexpr int LDIAG = LPART + XK * 3 * XK * 64;     // diagonal weights [a][b][k]
-constexpr int LBYTES = LDIAG + XR * 3 * 4;          // 160,448 B
-static_assert(LBYTES <= 163840, "LDS image exceeds 160 KiB");
+// LDS image (bytes) of the fp32 kernel (BF = false: X and Z fp32) and of the bf16 one (BF = true: X and Z bf16 rows,
+// the same fp32 weights, partial buffer and sums; Z rounded once at the store). Source regions hold one 16-feature
+// row chunk per row (64 B fp32, 32 B bf16), rounded up to whole LDS-DMA wave-instructions (1 KiB).
+template <bool BF>
+struct ML {
+    static constexpr int ES = BF ? 2 : 4;                           // bytes per source element
+    static constexpr int RB = XFC * ES;                             // bytes per source row chunk
+    static constexpr int PPR = RB / 16;                             // 16-B LDS-DMA pieces per row chunk
+    static constexpr int EPP = 16 / ES;                             // elements per piece
+    static constexpr int OUTB = (XR * RB + 1023) / 1024 * 1024;      // out / self region bytes
+    static constexpr int LOUT = 0;                                  // out-sources [b][c][16 f]
+    static constexpr int LIN = LOUT + OUTB;                         // in-sources  [c][a (+pad)][16 f]
+    static constexpr int LINB = (XK * XCB * RB + 1023) / 1024 * 1024;
+    static constexpr int LSELF = LIN + LINB;                        // self rows   [a][b][16 f]
+    static constexpr int LPART = LSELF + OUTB;                      // partial     [a][row k K + b (3K)][16 f] fp32
+    static constexpr int LDIAG = LPART + XK * 3 * XK * 64;          // diagonal weights [a][b][k]
+    static constexpr int LBYTES = LDIAG + XR * 3 * 4;               // 160,448 B fp32; 122,560 B bf16
+    static constexpr int NOI = OUTB / 1024, NII = LINB / 1024;      // wave-instructions per region
+};
+static_assert(ML<false>::LBYTES == 160448 && ML<false>::OUTB == XR * 64, "fp32 LDS image");
+static_assert(ML<true>::LBYTES <= 163840 && ML<false>::LBYTES <= 163840, "LDS image exceeds 160 KiB");
 static_assert(XTILES % XCW == 0 && XTPW % 2 == 0, "tiles per wave");
 
 struct XP {
@@ -69,10 +84,10 @@ struct XP {
     int64_t m0;            // first middle of the launch (the chunk stream covers middles m0 .. m0 + chunks / nch - 1)
     int64_t zsa, zsm;      // Z row of a.M.b = a zsa + (M - m0) zsm + b: (K^(n-1), K) global, (K, K^2) middle-major
     const float* plan;
-    const float* X;
-    int64_t ldx;
-    float* Z;
-    int64_t ldz;
+    const void* X;         // fp32 or (bf16 kernel) bf16 rows
+    int64_t ldx;           // elements
+    void* Z;               // fp32 or (bf16 kernel) bf16 rows
+    int64_t ldz;           // elements
     int F;
     int nch;               // F / 16
     int chunks;            // length of the (middle, chunk) stream a workgroup pair / workgroup walks, middle-major
@@ -106,15 +121,27 @@ __device__ __forceinline__ int opaque(int v) {
     return v;
 }
 
-__device__ __forceinline__ void glds16(const float* src, const void* lds_base) {
+__device__ __forceinline__ void glds16(const void* src, const void* lds_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// one source element from the LDS image as fp32 (bf16: exact widening)
+template <bool BF>
+__device__ __forceinline__ float lds_src(const char* q) {
+    if constexpr (BF) return __uint_as_float((uint32_t)(*reinterpret_cast<const uint16_t*>(q)) << 16);
+    else return *reinterpret_cast<const float*>(q);
 }
 
 struct Chunk {
     int M, ch, first;  // middle, chunk index, first chunk of this middle in the workgroup's range
 };
 
+template <bool BF>
 __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
+    using C = ML<BF>;
+    using ET = std::conditional_t<BF, uint16_t, float>;
+    constexpr int LOUT = C::LOUT, LIN = C::LIN, LSELF = C::LSELF, LPART = C::LPART, LDIAG = C::LDIAG;
+    constexpr int RB = C::RB, ES = C::ES;
     extern __shared__ __attribute__((aligned(16))) char L[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -139,45 +166,52 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
 
     if (wave >= XCW) {  // ---------------- loader waves: LDS-DMA only (same barrier sequence as the compute waves)
         const int lw = wave - XCW;
-        // One region = 400 rows x 64 B = 25 wave-instructions (in-sources: 420 rows with the pad rows, 27), split over
-        // the loader waves; piece order = LDS order; the in-sources are fetched c-major (one wave-instruction: rows
-        // c.a.M of one c, within 4 MB). The per-lane part of every piece's element offset does not depend on the
-        // middle or the chunk: computed once here (64-bit, in registers), so a DMA costs one add per instruction.
-        constexpr int NO = (XR * 4 / 64 + XLW - 1) / XLW, NI = (LINB / 1024 + XLW - 1) / XLW;
+        // One region = 400 rows x 64 B = 25 wave-instructions fp32, 400 x 32 B = 12.5 -> 13 bf16 (in-sources: 420 rows
+        // with the pad rows, 27 / 14), split over the loader waves; piece order = LDS order; the in-sources are fetched
+        // c-major (one wave-instruction: rows c.a.M of one c, within 4 MB). The per-lane part of every piece's element
+        // offset does not depend on the middle or the chunk: computed once here (64-bit, in registers), so a DMA costs
+        // one add per instruction. Pieces past the last row of a region (bf16: rows 400..415) fetch row 0 of the
+        // middle (a valid address) into the region's padding.
+        constexpr int NO = (C::NOI + XLW - 1) / XLW, NI = (C::NII + XLW - 1) / XLW;
+        constexpr int PPR = C::PPR, EPP = C::EPP;
         int64_t off_o[NO], off_i[NI], off_s[NO];
         const int64_t ldx = p.ldx;
 #pragma unroll
         for (int t = 0; t < NO; ++t) {
             const int it = lw + t * XLW;
-            const int rl = (it * 64 + lane) >> 2, q = lane & 3;
-            off_o[t] = (int64_t)rl * ldx + q * 4;                                    // out: row M.b.c = 400 M + rl
+            int rl = (int)((unsigned)(it * 64 + lane) / PPR);
+            const int q = lane & (PPR - 1);  // 64 % PPR == 0
+            if constexpr (C::OUTB != XR * C::RB) {  // bf16: the region's padding rows
+                if (rl >= XR) rl = 0;
+            }
+            off_o[t] = (int64_t)rl * ldx + q * EPP;                                  // out: row M.b.c = 400 M + rl
             const int a = rl / XK, b = rl - a * XK;
-            off_s[t] = (a * p.Kn1 + b) * ldx + q * 4;                                 // self: a.M.b = a K^(n-1) + 20 M + b
+            off_s[t] = (a * p.Kn1 + b) * ldx + q * EPP;                               // self: a.M.b = a K^(n-1) + 20 M + b
         }
 #pragma unroll
         for (int t = 0; t < NI; ++t) {
             const int it = lw + t * XLW;
-            const int rl = (it * 64 + lane) >> 2, q = lane & 3;
+            const int rl = (int)((unsigned)(it * 64 + lane) / PPR), q = lane & (PPR - 1);
             const int c = rl / XCB, a = rl - c * XCB;
-            off_i[t] = (a >= XK || c >= XK) ? q * 4 : (c * p.Kn1 + a * p.Kn2) * ldx + q * 4;  // in: c.a.M (+ M); pad: row M
+            off_i[t] = (a >= XK || c >= XK) ? q * EPP : (c * p.Kn1 + a * p.Kn2) * ldx + q * EPP;  // in: c.a.M; pad: row M
         }
         auto dma_rows = [&](int region, int kind, int M, int ch) {
-            const float* xc = p.X + ch * XFC;
+            const ET* xc = reinterpret_cast<const ET*>(p.X) + ch * XFC;
             if (kind == 0) {
-                const float* base = xc + (int64_t)M * XR * ldx;
+                const ET* base = xc + (int64_t)M * XR * ldx;
 #pragma unroll
                 for (int t = 0; t < NO; ++t)
-                    if (lw + t * XLW < XR * 4 / 64) glds16(base + off_o[t], L + region + (lw + t * XLW) * 1024);
+                    if (lw + t * XLW < C::NOI) glds16(base + off_o[t], L + region + (lw + t * XLW) * 1024);
             } else if (kind == 1) {
-                const float* base = xc + (int64_t)M * ldx;
+                const ET* base = xc + (int64_t)M * ldx;
 #pragma unroll
                 for (int t = 0; t < NI; ++t)
-                    if (lw + t * XLW < LINB / 1024) glds16(base + off_i[t], L + region + (lw + t * XLW) * 1024);
+                    if (lw + t * XLW < C::NII) glds16(base + off_i[t], L + region + (lw + t * XLW) * 1024);
             } else {
-                const float* base = xc + (int64_t)M * XK * ldx;
+                const ET* base = xc + (int64_t)M * XK * ldx;
 #pragma unroll
                 for (int t = 0; t < NO; ++t)
-                    if (lw + t * XLW < XR * 4 / 64) glds16(base + off_s[t], L + region + (lw + t * XLW) * 1024);
+                    if (lw + t * XLW < C::NOI) glds16(base + off_s[t], L + region + (lw + t * XLW) * 1024);
             }
         };
         auto dma_diag = [&](int M) {  // 4,800 B = 300 pieces: wave-instructions 0..4 (the last one partial)
@@ -258,15 +292,15 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         rk[r] = i / XK;
         rv[r] = i - rk[r] * XK;
     }
-    // LDS byte offsets: sources [row][16 f] (64 B rows); partial [a][row k K + b][16 f]
-    const int src_lane = (q4 * 16 + fl) * 4;                 // out: + (b * K + 4 s) * 64
-    const int in_lane = (q4 * XCB * 16 + fl) * 4;            // in:  + (4 s * XCB + a) * 64
+    // LDS byte offsets: sources [row][16 f] (RB-byte rows: 64 fp32, 32 bf16); partial [a][row k K + b][16 f] fp32
+    const int src_lane = (q4 * XFC + fl) * ES;               // out: + (b * K + 4 s) * RB
+    const int in_lane = (q4 * XCB * XFC + fl) * ES;          // in:  + (4 s * XCB + a) * RB
     int part_w[4], part_r[4], self_r[4], diag_r[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         part_w[r] = LPART + ((rv[r] * 3 * XK + rk[r] * XK + wb) * 16 + fl) * 4;  // out: a = rv, row k K + b; + 2 j * 64
         part_r[r] = LPART + ((wb * 3 * XK + rk[r] * XK + rv[r]) * 16 + fl) * 4;   // in: + 2 j * 60 * 64
-        self_r[r] = LSELF + ((rv[r] * XK + wb) * 16 + fl) * 4;                     // out: (a = rv, b); + 2 j * 64
+        self_r[r] = LSELF + ((rv[r] * XK + wb) * XFC + fl) * ES;                  // out: (a = rv, b); + 2 j * RB
         diag_r[r] = LDIAG + ((rv[r] * XK + wb) * 3 + rk[r]) * 4;                   // + 2 j * 12
         part_w[r] = opaque(part_w[r]);
         part_r[r] = opaque(part_r[r]);
@@ -295,8 +329,8 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         auto rd_out = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
-                x[0][s] = *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
-                x[1][s] = *reinterpret_cast<const float*>(L + LOUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
+                x[0][s] = lds_src<BF>(L + LOUT + src_lane + ((2 * j + wb) * XK + 4 * s) * RB);
+                x[1][s] = lds_src<BF>(L + LOUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * RB);
             }
         };
         float xo[2][2][XS];
@@ -310,8 +344,8 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             for (int r = 0; r < 4; ++r) {
                 w0[r] = *reinterpret_cast<const float*>(L + diag_r[r] + 2 * j * 12);
                 w1[r] = *reinterpret_cast<const float*>(L + diag_r[r] + (2 * j + 2) * 12);
-                s0[r] = *reinterpret_cast<const float*>(L + self_r[r] + 2 * j * 64);
-                s1[r] = *reinterpret_cast<const float*>(L + self_r[r] + (2 * j + 2) * 64);
+                s0[r] = lds_src<BF>(L + self_r[r] + 2 * j * RB);
+                s1[r] = lds_src<BF>(L + self_r[r] + (2 * j + 2) * RB);
             }
             asm volatile("" ::: "memory");  // the reads above are issued before the MFMAs below
             f4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -334,13 +368,13 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
         // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
-        float* zso = p.Z + ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz + (int64_t)so_k * p.F +
-                     cu.ch * XFC + 4 * (lane & 3);
+        ET* zso = reinterpret_cast<ET*>(p.Z) + ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz +
+                  (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
         auto rd_in = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
-                x[0][s] = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
-                x[1][s] = *reinterpret_cast<const float*>(L + LIN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
+                x[0][s] = lds_src<BF>(L + LIN + in_lane + (4 * s * XCB + 2 * j + wb) * RB);
+                x[1][s] = lds_src<BF>(L + LIN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * RB);
             }
         };
         float xi[2][2][XS];
@@ -379,8 +413,15 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
             const f4_t v1 = *reinterpret_cast<const f4_t*>(L + so_lds + (2 * j + 2) * 3 * XK * 64);
             if (!XEXP(0)) {
-                *reinterpret_cast<f4_t*>(zso + (int64_t)j * zstep) = v0;
-                *reinterpret_cast<f4_t*>(zso + (int64_t)(j + 1) * zstep) = v1;
+                if constexpr (BF) {  // one rounding to bf16 (RNE), 8-B stores
+                    *reinterpret_cast<uint2*>(zso + (int64_t)j * zstep) =
+                        make_uint2(pgbf::pack2(v0[0], v0[1]), pgbf::pack2(v0[2], v0[3]));
+                    *reinterpret_cast<uint2*>(zso + (int64_t)(j + 1) * zstep) =
+                        make_uint2(pgbf::pack2(v1[0], v1[1]), pgbf::pack2(v1[2], v1[3]));
+                } else {
+                    *reinterpret_cast<f4_t*>(zso + (int64_t)j * zstep) = v0;
+                    *reinterpret_cast<f4_t*>(zso + (int64_t)(j + 1) * zstep) = v1;
+                }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // W(t)
@@ -461,6 +502,19 @@ int grid_cap() {  // one persistent workgroup per CU (device-properties cache: i
     return cus[dev];
 }
 
+template <bool BF>
+int mid_go(unsigned grid, hipStream_t s, const XP& p, const char* name) {
+    static bool attr_set = false;  // the kernel's dynamic LDS exceeds the 64 KiB default (set once; idempotent)
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_mid_kernel<BF>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, ML<BF>::LBYTES) != hipSuccess)
+            return pg::set_error(PG_ERR_HIP, "%s: cannot raise the LDS limit", name);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(ngram_mid_kernel<BF>, dim3(grid), dim3(XTHREADS), ML<BF>::LBYTES, s, p);
+    return pg::check_launch(name);
+}
+
 }  // namespace
 
 extern "C" {
@@ -487,9 +541,11 @@ int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, cons
     return pg::check_launch("pg_ngram_mplan_f32");
 }
 
-static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
-                      int64_t m_begin, int64_t m_end, bool middle_major, const pg_layer_args_t* gates, float* Z,
-                      int64_t ldz, uint32_t flags, unsigned long long* stamps, void* stream) {
+// bf: X and Z are bf16 rows (the bf16 kernel); ldx / ldz in elements
+static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const void* X, int64_t ldx, int64_t F,
+                      int64_t m_begin, int64_t m_end, bool middle_major, const pg_layer_args_t* gates, void* Z,
+                      int64_t ldz, uint32_t flags, unsigned long long* stamps, bool bf, void* stream) {
+    const char* name = bf ? "pg_spmm3_ngram_mid_bf16" : "pg_spmm3_ngram_mid_f32";
     int64_t Kn1 = 0, Kn2 = 0;
     PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
     if (m_end < 0) m_end = Kn2;
@@ -498,13 +554,16 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     if (m_begin == m_end) return PG_OK;
     PG_REQUIRE(plan && X && Z, "null pointer");
     PG_REQUIRE(ldz >= 3 * F && ldx >= F, "leading dimensions too small");
-    if (gates)
-        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: no gated store (the dense kernel gates)");
-    if (F <= 0 || F % XFC)
-        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: F must be a multiple of %d", XFC);
-    if (!pg::aligned16(X) || !pg::aligned16(plan) || !pg::aligned16(Z) || (ldx * 4) % 16 || (ldz * 4) % 16)
-        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_ngram_mid_f32: needs 16-B aligned X and Z rows");
+    if (gates) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: no gated store (the dense kernel gates)", name);
+    if (F <= 0 || F % XFC) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be a multiple of %d", name, XFC);
+    const int64_t es = bf ? 2 : 4;
+    // LDS-DMA pieces of 16 B from every X row; Z stores of 16 B (fp32) / 8 B (bf16)
+    const bool z_ok = bf ? ((reinterpret_cast<uintptr_t>(Z) & 7) == 0 && (ldz * es) % 8 == 0)
+                         : (pg::aligned16(Z) && (ldz * es) % 16 == 0);
+    if (!pg::aligned16(X) || !pg::aligned16(plan) || (ldx * es) % 16 || !z_ok)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned X rows and aligned Z rows", name);
     PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 30), "too many column chunks");
+    PG_REQUIRE(!(bf && stamps), "time stamps: fp32 kernel only");
     XP p{};
     p.Kn1 = Kn1;
     p.Kn2 = Kn2;
@@ -530,32 +589,37 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const flo
     unsigned grid = (unsigned)(total < cap ? total : cap);
     if (p.cstride == 2) grid &= ~1u;
     hipStream_t s = (hipStream_t)stream;
-    static bool attr_set = false;  // the kernel's dynamic LDS exceeds the 64 KiB default (set once; idempotent)
-    if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_mid_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                LBYTES) != hipSuccess)
-            return pg::set_error(PG_ERR_HIP, "pg_spmm3_ngram_mid_f32: cannot raise the LDS limit");
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(ngram_mid_kernel, dim3(grid), dim3(XTHREADS), LBYTES, s, p);
-    return pg::check_launch("pg_spmm3_ngram_mid_f32");
+    return bf ? mid_go<true>(grid, s, p, name) : mid_go<false>(grid, s, p, name);
 }
 
 int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                            const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream) {
-    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, gates, Z, ldz, flags, nullptr, stream);
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, gates, Z, ldz, flags, nullptr, false, stream);
 }
 
 int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                                 int64_t m_begin, int64_t m_end, float* Z, int64_t ldz, uint32_t flags, void* stream) {
-    return mid_launch(K, n, n_rows, plan, X, ldx, F, m_begin, m_end, true, nullptr, Z, ldz, flags, nullptr, stream);
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, m_begin, m_end, true, nullptr, Z, ldz, flags, nullptr, false,
+                      stream);
+}
+
+int pg_spmm3_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx, int64_t F,
+                            uint16_t* Z, int64_t ldz, uint32_t flags, void* stream) {
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, nullptr, true, stream);
+}
+
+int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx,
+                                 int64_t F, int64_t m_begin, int64_t m_end, uint16_t* Z, int64_t ldz, uint32_t flags,
+                                 void* stream) {
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, m_begin, m_end, true, nullptr, Z, ldz, flags, nullptr, true,
+                      stream);
 }
 
 #ifdef PG_MID_STAMPS
 // diagnostics library only (tools/mid_stamps.py): the same launch with per-block time stamps
 int pg_mid_stamped(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F, float* Z,
                    int64_t ldz, uint32_t flags, unsigned long long* stamps, void* stream) {
-    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, stamps, stream);
+    return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, stamps, false, stream);
 }
 #endif
 }  // extern "C"

@@ -121,12 +121,13 @@ class CSRGraph:
     def compulsory_bytes(self, F: int, elem: int = 4, gated: bool = False) -> int:
         """SURVEY §8d's compulsory model: rowptr + records once, every X row read ONCE (the rows of X the
         graph references: n_cols, or n_rows), 3 output rows; gated launches also read 5 fp32 gates per row.
-        With an n-gram plan (the tile kernel runs, F = 64 / 128 fp32) the plan's weights replace rowptr + records.
+        With an n-gram plan (the tile kernels run: middle-tile fp32 / bf16 for F % 16 == 0, else 4x4-block fp32 at
+        F = 64 / 128 / 256) the plan's weights replace rowptr + records.
         The byte floor a propagation launch cannot go below; the roofline fraction is priced on it."""
         n = self.n_rows
         nx = self.n_cols if self.n_cols is not None else n
         g = 20 * n if gated else 0
-        if self.ngram is not None and self.ngram.mplan is not None and F % 16 == 0 and elem == 4:
+        if self.ngram is not None and self.ngram.mplan is not None and F % 16 == 0 and elem in (2, 4):
             return 4 * self.ngram.mplan.numel() + nx * F * elem + 3 * n * F * elem + g  # middle-tile kernel: its plan
         if self.ngram is not None and F in (64, 128, 256) and elem == 4:  # the n-gram tile kernel reads its plan instead
             return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g

@@ -94,10 +94,10 @@ def _ngram_ok(g: CSRGraph, x: torch.Tensor, fl: int, widths=(64, 128), dtype=tor
 
 
 def _mid_ok(g: CSRGraph, x: torch.Tensor, fl: int) -> bool:
-    """The middle-tile forward (pg_spmm3_ngram_mid_f32) takes this call: fp32 x with the graph's rows, F a multiple
-    of 16, a middle plan, and neither PG_FLAG_NO_NGRAM nor PG_FLAG_NGRAM_BLOCK4."""
+    """The middle-tile forward (pg_spmm3_ngram_mid_f32 / _bf16) takes this call: fp32 or bf16 x with the graph's rows,
+    F a multiple of 16, a middle plan, and neither PG_FLAG_NO_NGRAM nor PG_FLAG_NGRAM_BLOCK4."""
     return (g.ngram is not None and g.ngram.mplan is not None and not (fl & (PG_FLAG_NO_NGRAM | PG_FLAG_NGRAM_BLOCK4))
-            and x.dtype == torch.float32 and x.size(0) == g.n_rows and x.size(1) % 16 == 0)
+            and x.dtype in (torch.float32, torch.bfloat16) and x.size(0) == g.n_rows and x.size(1) % 16 == 0)
 
 
 def _ngram_fwd(lib, g, x, a, Z, fl, s):
@@ -165,9 +165,11 @@ def spmm3_middles(g: CSRGraph, x: torch.Tensor, m_begin: int, m_end: int, flags:
     """pg_spmm3_ngram_mid_rows_f32: Z = [A_in x | A_out x | A_und x] for the nodes a.M.b of the middles
     M in [m_begin, m_end) only, in middle-major order (row (M - m_begin) K^2 + a K + b), x in the global row layout
     (only the rows those middles read need be valid). The middle partition's per-rank propagation (shard.py).
-    Needs g.ngram with a middle plan and fp32 x with F % 16 == 0: raises otherwise (callers check `_mid_ok`)."""
+    Needs g.ngram with a middle plan and fp32 or bf16 x (bf16 Z: pg_spmm3_ngram_mid_rows_bf16) with F % 16 == 0:
+    raises otherwise (callers check `_mid_ok`)."""
     lib = load_library()
-    x = _f32c(x)
+    bf = _is_bf16(x)
+    x = _bf16c(x) if bf else _f32c(x)
     _require_gpu(x)
     _require_graph_on(g, x)
     fl = default_flags() if flags is None else flags
@@ -176,12 +178,13 @@ def spmm3_middles(g: CSRGraph, x: torch.Tensor, m_begin: int, m_end: int, flags:
     ng, N, F = g.ngram, g.n_rows, x.size(1)
     K2 = ng.K * ng.K
     rows = (m_end - m_begin) * K2
-    Z = out if out is not None else torch.empty(rows, 3 * F, device=x.device, dtype=torch.float32)
-    if Z.shape != (rows, 3 * F) or Z.stride(1) != 1:
-        raise ValueError("out must be [(m_end - m_begin) K^2, 3F] with unit column stride")
+    Z = out if out is not None else torch.empty(rows, 3 * F, device=x.device, dtype=x.dtype)
+    if Z.shape != (rows, 3 * F) or Z.stride(1) != 1 or Z.dtype != x.dtype:
+        raise ValueError("out must be [(m_end - m_begin) K^2, 3F] of x's dtype with unit column stride")
     ev = _ev_start(x)
-    check(lib.pg_spmm3_ngram_mid_rows_f32(ng.K, ng.n, N, _p(ng.mplan), _p(x), x.stride(0), F, m_begin, m_end, _p(Z),
-                                          Z.stride(0), fl, _stream(x)), "pg_spmm3_ngram_mid_rows_f32")
+    fn = lib.pg_spmm3_ngram_mid_rows_bf16 if bf else lib.pg_spmm3_ngram_mid_rows_f32
+    check(fn(ng.K, ng.n, N, _p(ng.mplan), _p(x), x.stride(0), F, m_begin, m_end, _p(Z), Z.stride(0), fl, _stream(x)),
+          "pg_spmm3_ngram_mid_rows_" + ("bf16" if bf else "f32"))
     _ev_end(x, ev)
     return Z
 
@@ -228,6 +231,14 @@ def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
         Z = out if out is not None else torch.empty(N, 3 * F, device=x.device, dtype=torch.bfloat16)
         fl = default_flags() if flags is None else flags
         ev = _ev_start(x)
+        if _mid_ok(g, x, fl):  # complete n-gram graphs: the middle-tile kernel on bf16 rows
+            ng = g.ngram
+            rc = lib.pg_spmm3_ngram_mid_bf16(ng.K, ng.n, N, _p(ng.mplan), _p(x), x.stride(0), F, _p(Z), Z.stride(0),
+                                             fl, _stream(x))
+            if rc != _lib.PG_ERR_UNSUPPORTED:
+                check(rc, "pg_spmm3_ngram_mid_bf16")
+                _ev_end(x, ev)
+                return Z
         rc = lib.pg_spmm3_bf16(N, _p(g.rowptr), _p(g.row_order), _p(g.edges3), _p(x), x.stride(0), F, _p(Z),
                                Z.stride(0), fl, _stream(x))
         if rc != _lib.PG_ERR_UNSUPPORTED:

@@ -35,3 +35,22 @@ def test_bench_json_line_is_self_consistent():
     assert 0.0 < rf["frac"] < 1.0  # compulsory bytes: physically below peak
     # the propagation is one of the step's kernels: its launches take less than the whole step
     assert rf["avg_launch_ms"] < out["ms_per_step"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("gpus,partition,label", [(2, "auto", "replicate_then_middle_x2"),
+                                                   (2, "middle", "middle_ghost_a2a_x2"),
+                                                   (3, "halo", "halo_recompute_x3"),
+                                                   (4, "middle", "middle_ghost_a2a_x4")])
+def test_bench_multi_rank_rehearsal(gpus, partition, label):
+    """bench.py --gpus N with N gloo ranks sharing this GPU (the driver's N > 1 launch shape, RCCL replaced by gloo):
+    each partition runs its timed loop and rank 0 prints one JSON line with the whole job's numbers."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--dist-backend", "gloo",
+                        "--one-device", "--steps", "3", "--warmup", "1", "--no-pmc", "--clock-warmup-s", "0",
+                        "--partition", partition], cwd=REPO, capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == gpus and out["config"]["parallelism"] == label and out["value"] > 0

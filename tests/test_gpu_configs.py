@@ -459,9 +459,9 @@ def test_middle_partition_4gram_every_rank_bitexact(pkg, cuda, monkeypatch):
 
 @pytest.mark.timeout(600)
 def test_middle_partition_bf16_rank_bitexact(pkg, cuda, monkeypatch):
-    """bf16 mode through the middle partition (the CSR bf16 kernels over the rank's rows -- the middle-tile kernel is
-    fp32 -- and bf16 ghost rows): ranks 0 and 3 of P = 4 at 4-gram match the single-GPU bf16 forward. The
-    propagation rows are bit-identical; the bf16 dense kernel's accumulation order depends on the row count, so
+    """bf16 mode through the middle partition (the bf16 middle-tile kernel over the rank's middles, bf16 ghost
+    rows): ranks 0 and 3 of P = 4 at 4-gram match the single-GPU bf16 forward. The propagation rows are
+    bit-identical (the same kernel, the same per-row sums, over the rank's middle range); the bf16 dense kernel's accumulation order depends on the row count, so
     its outputs agree to bf16 rounding (1 ulp), not bit for bit: |d| <= 2e-2 + 2e-2|ref| on the log-probs and
     embeddings."""
     from protgram_directgcn_amd import ops, shard
@@ -488,7 +488,7 @@ def test_middle_partition_bf16_rank_bitexact(pkg, cuda, monkeypatch):
         mp = shard.middle_partition(g, rank, 4, chunks=2)
         lp2, emb2 = shard.MiddleRunner(m, mp, xd)()
         torch.cuda.synchronize()
-        assert torch.equal(ops.spmm3(mp.own_csr, xd), ops.spmm3(g, xd)[mp.own])  # propagation: bit-identical
+        assert torch.equal(ops.spmm3_middles(g, xd, mp.m0, mp.m1), ops.spmm3(g, xd)[mp.own])  # bit-identical
         for got, ref in ((lp2, lp[mp.global_rows]), (emb2, emb[mp.global_rows])):
             assert bool(((got.float() - ref.float()).abs() <= 2e-2 + 2e-2 * ref.float().abs()).all()), rank
 

@@ -338,6 +338,50 @@ def test_ngram_mid_kernel_vs_csr(pkg, cuda, monkeypatch, n, F, drop):
                 ops.default_flags(), ops._stream(xp)) == _lib.PG_ERR_UNSUPPORTED
 
 
+@pytest.mark.parametrize("n,F,drop", [(2, 16, 0.0), (3, 64, 0.3), (3, 128, 0.0), (4, 32, 0.1), (4, 128, 0.0)])
+def test_ngram_mid_kernel_bf16(pkg, cuda, monkeypatch, n, F, drop):
+    """The bf16 middle-tile kernel (pg_spmm3_ngram_mid_bf16, bf16 mode's default on complete n-gram graphs) computes
+    the fp32 kernel's sums on the exactly widened bf16 rows and rounds each once: it equals bf16(fp32 middle-tile
+    kernel on x.float()) bit for bit, and the bf16 CSR kernel within one bf16 rounding; the middle-range variant
+    (pg_spmm3_ngram_mid_rows_bf16) gives the same rows in middle-major order; padded rows stay untouched."""
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    if drop:
+        keep = np.random.default_rng(n * 1000 + F).random(s.size) >= drop
+        s, d, c = s[keep], d[keep], c[keep]
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    xb = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(torch.bfloat16).to(cuda)
+    lib = ops.load_library()
+    hits = []
+    real = lib.pg_spmm3_ngram_mid_bf16
+    monkeypatch.setattr(lib, "pg_spmm3_ngram_mid_bf16", lambda *a: hits.append(1) or real(*a))
+    Zb = ops.spmm3(g, xb)
+    assert hits and Zb.dtype == torch.bfloat16, "the bf16 middle-tile kernel did not run"
+    Zf = ops.spmm3(g, xb.float())
+    assert torch.equal(Zb, Zf.to(torch.bfloat16))
+    Zc = ops.spmm3(g, xb, flags=_lib_csr())  # bf16 CSR kernel: fp32 sums in CSR order, one rounding
+    diff = (Zb.float() - Zc.float()).abs()
+    assert bool((diff <= 2.0 ** -7 * Zc.float().abs() + 1e-6).all()), float(diff.max())
+    ng = g.ngram
+    nm = N // (ng.K * ng.K)
+    m0, m1 = nm // 3, nm // 3 + max(1, nm // 4)
+    Zr = ops.spmm3_middles(g, xb, m0, m1)
+    M_ = torch.arange(m0, m1).view(-1, 1, 1)
+    a_ = torch.arange(ng.K).view(1, -1, 1)
+    b_ = torch.arange(ng.K).view(1, 1, -1)
+    rows = (a_ * (N // ng.K) + M_ * ng.K + b_).reshape(-1).to(cuda)
+    assert torch.equal(Zr, Zb[rows])
+    xp = torch.zeros(N, F + 8, dtype=torch.bfloat16, device=cuda)
+    xp[:, :F] = xb
+    Zp = torch.full((N, 3 * F + 4), 7.0, dtype=torch.bfloat16, device=cuda)
+    torch.cuda.synchronize()
+    rc = real(ng.K, ng.n, N, ops._p(ng.mplan), ops._p(xp), xp.stride(0), F, ops._p(Zp), Zp.stride(0),
+              ops.default_flags(), ops._stream(xp))
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    assert torch.equal(Zp[:, :3 * F], Zb) and bool((Zp[:, 3 * F:] == 7.0).all())
+
+
 @pytest.mark.parametrize("F,H,C", [(128, 64, 20), (128, 64, 32), (128, 64, 1), (32, 16, 5), (256, 128, 50), (16, 8, 400),
                                    (34, 17, 3), (12, 6, 1)])
 def test_head_kernel_vs_torch(pkg, cuda, F, H, C):

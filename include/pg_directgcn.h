@@ -82,6 +82,11 @@ typedef struct pg_edge1 {
                                              middle-tile kernel (pg_spmm3_ngram_mid_f32) */
 #define PG_FLAG_MID_NO_PAIRS (1u << 22)   /* middle-tile kernel: no workgroup pairs on odd / even feature chunks
                                              (each workgroup walks all chunks of its middles) */
+#define PG_FLAG_MID_LOADER_SYNC (1u << 19) /* middle-tile kernels: the loader waits for chunk t+1's out / self rows
+                                             before the in-phase barrier of chunk t (the round-3 protocol) instead of
+                                             before the store-out barrier */
+#define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernel
+                                             (pg_spmm3t_ngram_mid_f32) instead of the 4x4-block one */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -261,6 +266,14 @@ int pg_spmm3_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, con
 int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx,
                                  int64_t F, int64_t m_begin, int64_t m_end, uint16_t* Z, int64_t ldz, uint32_t flags,
                                  void* stream);
+/* Transposed middle-tile kernel: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k;
+ * the backward of the six propagates, protgram_directgcn.py:101-112, replacing pg_spmm3t_ngram_f32 / pg_spmm3t_f32
+ * on graphs over all K^n n-grams). Same middle plan, stream and loader as the forward; per chunk three sub-chunks
+ * (one per slice G_k) accumulate into one LDS partial, so dX is written once. K = 20, F a multiple of 16, 16-B
+ * aligned G and dX rows; PG_ERR_UNSUPPORTED otherwise. Numerics as the forward: within fp32 rounding of the CSR
+ * kernel; G must be finite. */
+int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
+                            float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
  * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).

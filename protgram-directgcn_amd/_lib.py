@@ -22,6 +22,8 @@ PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_NO_NGRAM = 1 << 20
 PG_FLAG_NGRAM_BLOCK4 = 1 << 21
 PG_FLAG_MID_NO_PAIRS = 1 << 22
+PG_FLAG_MID_LOADER_SYNC = 1 << 19
+PG_FLAG_MID_TRANSPOSED = 1 << 23
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
@@ -86,6 +88,8 @@ SIGNATURES = {
     "pg_rows_scatter": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                            ctypes.c_int, c_u32, c_vp]),
+    "pg_spmm3t_ngram_mid_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp,
+                                               c_i64, ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                             ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,

@@ -67,7 +67,16 @@ struct DenseP {
     // and / or writes its output row (map_y) at the global n-gram row a.M.b = a K^(n-1) + 20 M + b
     int64_t map_kn1, map_m0;
     int map_res, map_y;
+    int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
 };
+
+// Diagnostics build only: dense_x3p_kernel timing experiments, flag bits 24..28 (bit 0: no MFMAs, 1: no split,
+// 2: no Y stores, 3: no A DMA, 4: no constant / residual DMA). Results are garbage in those runs.
+#ifdef PG_DENSE_EXP
+#define DEXP(bit) ((p.exp >> (bit)) & 1)
+#else
+#define DEXP(bit) 0
+#endif
 
 // global n-gram row of middle-major row m (K = 20: 400 rows per middle); see DenseP::map_*
 __device__ __forceinline__ int64_t ngram_row(const DenseP& p, int64_t m) {
@@ -811,6 +820,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     auto tile_of = [&](int64_t kt) { return lo + max((int64_t)0, min(kt, ntl - 1)) * step; };
 
     auto issue_A = [&](int64_t tile, float* Ad) {
+        if (DEXP(3)) return;
         const int64_t m0 = tile * BM;
         const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
         const float* zb = p.Z + m0 * p.ldz;
@@ -842,6 +852,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         glds4(c4 + r, &Gi[slot][4][0]);
     };
     auto issue_CR = [&](int64_t tile) {  // wave w: rows 2w, 2w + 1
+        if (DEXP(4)) return;
         const int64_t m0 = tile * BM;
         const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
         int ln = lane;
@@ -865,6 +876,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     // fp32 tile -> three bf16 images; thread j converts units j and j + 512 (row j & 15, unit j >> 4): waves 0-3
     // two units, waves 4-7 one; all of a thread's fp32 reads in one LDS round trip
     auto split_tile = [&](const float* Af, int ab, int gslot) {
+        if (DEXP(1)) return;
         const int r = tid & 15;
         const bool two = tid + 512 < BM * NU;  // wave-uniform
         const int u0 = tid >> 4, u1 = u0 + 32;
@@ -902,6 +914,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         const uint4* a2 = &As[ab][2][a_unit16(0, lc, kg)];
         uint4 op[2][3];
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (DEXP(0)) return;
         op[0][0] = a0[0];
         op[0][1] = a1[0];
         op[0][2] = a2[0];
@@ -985,7 +998,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                     const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                     y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
                 }
-                {
+                if (!DEXP(2)) {
                     const int64_t yr = p.map_y ? ngram_row(p, m0 + er) : m0 + er;
                     *reinterpret_cast<float4*>(p.Y + yr * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
                     y_pending = true;
@@ -1108,6 +1121,9 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
+#ifdef PG_DENSE_EXP
+    p.exp = (int)((flags >> 24) & 31u);
+#endif
     if (ngmap) {  // {Kn1, m0, map_res, map_y}
         p.map_kn1 = ngmap[0];
         p.map_m0 = ngmap[1];

@@ -93,6 +93,7 @@ struct XP {
     int chunks;            // length of the (middle, chunk) stream a workgroup pair / workgroup walks, middle-major
     int cstride;           // 2: workgroup pairs split each middle's chunks odd / even (see the kernel); 1: no pairs
     int remap;
+    int early_in;          // loader: out / self DMA of chunk t + 1 waited for at W(t), not S(t) (PG_FLAG_MID_LOADER_SYNC clears)
     int exp;               // diagnostics build only: timing experiments (bit 0: no Z stores, 1: no out/self DMA, 2: no in DMA)
     unsigned long long* stamps;  // diagnostics build only (PG_MID_STAMPS): s_memtime per block, chunk and point
 };
@@ -123,6 +124,26 @@ __device__ __forceinline__ int opaque(int v) {
 
 __device__ __forceinline__ void glds16(const void* src, const void* lds_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// Loader wave lw after issuing the next chunk's in-source pieces: wait until everything it issued before them (the
+// out / self / diagonal pieces) has landed, leaving its own in-source pieces (the youngest vector-memory operations;
+// vmcnt counts in issue order) in flight. NII = in-source wave-instructions per region, dealt round-robin.
+template <int NII>
+__device__ __forceinline__ void wait_all_but_in(int lw) {
+    const int nin = (NII - lw + XLW - 1) / XLW;  // wave-uniform
+    static_assert((NII + XLW - 1) / XLW <= 8, "in pieces per loader wave");
+    switch (nin) {
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
 }
 
 // one source element from the LDS image as fp32 (bf16: exact widening)
@@ -245,11 +266,15 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
                 dma_rows(LSELF, 2, nx.M, nx.ch);
                 if (nx.first) dma_diag(nx.M);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // The out / self rows of chunk t + 1 are first read after W(t): with early_in they stay in flight across
+            // S(t) and the store-out, and only the in-source pieces issued after S(t) may still be in flight at W(t)
+            if (!p.early_in) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             XSTAMP(ci, 2);
             asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in-region free
             XSTAMP(ci, 3);
             if (more && !XEXP(2)) dma_rows(LIN, 1, nx.M, nx.ch);
+            if (XEXP(2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else wait_all_but_in<C::NII>(lw);
             asm volatile("s_barrier" ::: "memory");  // W(t): chunk t's results have left the partial buffer
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             XSTAMP(ci, 4);
@@ -432,6 +457,281 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     XSTAMP(XSTAMP_LAST, 7);
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Transposed middle-tile kernel: the backward of the forward above for the symmetric n-gram matrices (A_k^T = A_k;
+// the autograd of protgram_directgcn.py:101-112), with G_k = G[:, kF:(k+1)F]:
+//   dX[a.M.b, f] = sum_k ( sum_c Wout_k[a,b,c] G_k[M.b.c, f] + Wdiag_k[a,b] G_k[a.M.b, f] + sum_c Win_k[a,b,c] G_k[c.a.M, f] )
+// Same plan, same (middle, 16-feature chunk) stream and workgroup pairs, same LDS-DMA loader: each chunk runs three
+// sub-chunks k = 0, 1, 2, each an out-phase (per b) and an in-phase (per a) over the slice G_k, whose rows the loader
+// stages exactly as the forward stages X's. All six phases accumulate into ONE partial buffer P[a][b][16 f] in LDS
+// (each phase reads it as its MFMAs' initial accumulators and writes it back), which leaves for HBM once, after
+// k = 2: dX is written once per chunk, G_k's rows are read as out-sources, in-sources and own rows.
+// Sub-chunk k needs only the row tiles that hold rows (k, a) = 20 k .. 20 k + 19 of the plan's fragments (tiles
+// m = 20k / 16 and the next). The compute waves own fixed row tiles (their weights stay in registers per middle, as
+// in the forward): wave w owns tile m = (w & 1) + 2 (w >> 2) and the columns of parity (w >> 1) & 1, so the two waves
+// of every SIMD (w, w + 4) own tiles {0, 2} or {1, 3} and exactly one of them works in each phase. A lane row of an
+// active tile that belongs to another adjacency computes a value nobody reads: it reads and writes the pad dwords of
+// a P row (P rows are 20 dwords: 16 features + 4 pad, so both phases' lane patterns are bank-conflict free).
+constexpr int TPB = 20;                               // P row pitch (dwords)
+constexpr int TPA = XK * TPB + 4;                     // P a-block pitch (dwords)
+constexpr int TL_OUT = 0;                             // G_k out-sources [b][c][16 f]
+constexpr int TL_IN = TL_OUT + XR * 64;               // G_k in-sources  [c][a (+pad)][16 f]
+constexpr int TL_SELF = TL_IN + ML<false>::LINB;      // G_k own rows    [a][b][16 f]
+constexpr int TL_PART = TL_SELF + XR * 64;            // P [a][b][20]
+constexpr int TL_DIAG = TL_PART + XK * TPA * 4;       // diagonal weights [a][b][k]
+constexpr int TL_BYTES = TL_DIAG + XR * 3 * 4;        // 115,968 B
+static_assert(TL_BYTES <= 163840 && (TPB * 4) % 16 == 0 && (TPA * 4) % 16 == 0, "transposed LDS image");
+
+struct TChunk {
+    int M, ch, k, first;  // middle, chunk, adjacency (sub-chunk), first sub-chunk of this middle in the range
+};
+
+__global__ __launch_bounds__(XTHREADS) void ngram_midt_kernel(XP p, int accumulate) {
+    using C = ML<false>;
+    extern __shared__ __attribute__((aligned(16))) char L[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the forward's chunk ranges and pairs (see ngram_mid_kernel); sub-chunk t = 3 g + k
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int half = p.cstride == 2 ? (int)(lb & 1) : 0;
+    const int64_t lu = p.cstride == 2 ? lb >> 1 : lb, nu = p.cstride == 2 ? gridDim.x >> 1 : gridDim.x;
+    const int g0 = (int)(lu * p.chunks / nu), g1 = (int)((lu + 1) * p.chunks / nu);
+    const int nchu = p.nch / p.cstride;
+    const int t0 = 3 * g0, t1 = 3 * g1;
+    auto sub_at = [&](int t) -> TChunk {
+        const int g = t / 3, k = t - 3 * g;
+        const int Mr = g / nchu;
+        const int j = g - Mr * nchu;
+        return TChunk{(int)p.m0 + Mr, j * p.cstride + half, k, (g == g0 || j == 0) && k == 0};
+    };
+
+    if (wave >= XCW) {  // ---------------- loader waves (the forward's, on the columns of G_k)
+        const int lw = wave - XCW;
+        constexpr int NO = (C::NOI + XLW - 1) / XLW, NI = (C::NII + XLW - 1) / XLW;
+        int64_t off_o[NO], off_i[NI], off_s[NO];
+        const int64_t ldx = p.ldx;
+#pragma unroll
+        for (int t = 0; t < NO; ++t) {
+            const int it = lw + t * XLW;
+            const int rl = (int)((unsigned)(it * 64 + lane) / C::PPR), q = lane & (C::PPR - 1);
+            off_o[t] = (int64_t)rl * ldx + q * C::EPP;
+            const int a = rl / XK, b = rl - a * XK;
+            off_s[t] = (a * p.Kn1 + b) * ldx + q * C::EPP;
+        }
+#pragma unroll
+        for (int t = 0; t < NI; ++t) {
+            const int it = lw + t * XLW;
+            const int rl = (int)((unsigned)(it * 64 + lane) / C::PPR), q = lane & (C::PPR - 1);
+            const int c = rl / XCB, a = rl - c * XCB;
+            off_i[t] = (a >= XK || c >= XK) ? q * C::EPP : (c * p.Kn1 + a * p.Kn2) * ldx + q * C::EPP;
+        }
+        auto dma_rows = [&](int region, int kind, const TChunk& c) {
+            const float* xc = reinterpret_cast<const float*>(p.X) + (int64_t)c.k * p.F + c.ch * XFC;
+            if (kind == 0) {
+                const float* base = xc + (int64_t)c.M * XR * ldx;
+#pragma unroll
+                for (int t = 0; t < NO; ++t)
+                    if (lw + t * XLW < C::NOI) glds16(base + off_o[t], L + region + (lw + t * XLW) * 1024);
+            } else if (kind == 1) {
+                const float* base = xc + (int64_t)c.M * ldx;
+#pragma unroll
+                for (int t = 0; t < NI; ++t)
+                    if (lw + t * XLW < C::NII) glds16(base + off_i[t], L + region + (lw + t * XLW) * 1024);
+            } else {
+                const float* base = xc + (int64_t)c.M * XK * ldx;
+#pragma unroll
+                for (int t = 0; t < NO; ++t)
+                    if (lw + t * XLW < C::NOI) glds16(base + off_s[t], L + region + (lw + t * XLW) * 1024);
+            }
+        };
+        auto dma_diag = [&](int M) {
+            const float* d = p.plan + (int64_t)M * XMB + XPD;
+#pragma unroll 1
+            for (int it = lw; it < 5; it += XLW) {
+                const int P = it * 64 + lane;
+                if (P < XR * 3 / 4) glds16(d + P * 4, L + TL_DIAG + it * 1024);
+            }
+        };
+        if (t0 < t1) {
+            const TChunk c0 = sub_at(t0);
+            dma_rows(TL_OUT, 0, c0);
+            dma_rows(TL_IN, 1, c0);
+            dma_rows(TL_SELF, 2, c0);
+            dma_diag(c0.M);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");  // S(-1)
+#pragma unroll 1
+        for (int t = t0; t < t1; ++t) {
+            const bool more = t + 1 < t1;
+            const TChunk nx = more ? sub_at(t + 1) : TChunk{0, 0, 0, 0};
+            asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done; out / self / diag free
+            if (more) {
+                dma_rows(TL_OUT, 0, nx);
+                dma_rows(TL_SELF, 2, nx);
+                if (nx.first) dma_diag(nx.M);
+            }
+            if (!p.early_in) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in-region free
+            if (more) dma_rows(TL_IN, 1, nx);
+            wait_all_but_in<C::NII>(lw);             // out / self (+ diagonal) of t + 1 have landed
+            asm volatile("s_barrier" ::: "memory");  // W(t)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        return;
+    }
+
+    // ---------------- compute waves
+    const int q4 = lane >> 4, fl = lane & 15;
+    const int mw = (wave & 1) + 2 * (wave >> 2);  // row tile
+    const int wb = (wave >> 1) & 1;               // column parity: b (out) / a (in) = 2 j + wb
+    float Ao[XTPW][XS], Ai[XTPW][XS];
+    auto load_Ao = [&](int M) {
+        const float* pm = p.plan + (int64_t)M * XMB + XPO + lane;
+#pragma unroll
+        for (int j = 0; j < XTPW; ++j)
+#pragma unroll
+            for (int s = 0; s < XS; ++s) Ao[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+    };
+    auto load_Ai = [&](int M) {
+        const float* pm = p.plan + (int64_t)M * XMB + XPI + lane;
+#pragma unroll
+        for (int j = 0; j < XTPW; ++j)
+#pragma unroll
+            for (int s = 0; s < XS; ++s) Ai[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+    };
+    // this lane's accumulator rows i = 16 mw + 4 q4 + r, r = 0..3: (k, a) in the out-phase, (k, b) in the in-phase
+    // (padding rows 60..63 repeat 56..59, as in the forward). The four rows are consecutive and of one adjacency rk
+    // (20 and 40 are multiples of 4): rv + r. Per-row LDS offsets are the base's plus compile-time immediates.
+    const int i0 = 16 * mw + 4 * q4 - (16 * mw + 4 * q4 >= 3 * XK ? 4 : 0);
+    const int rk = i0 / XK, rv = i0 - rk * XK;
+    const int self_b = opaque(TL_SELF + ((rv * XK + wb) * XFC + fl) * 4);  // + r * K * 64 + 2 j * 64
+    const int col_v = fl * 4, col_j = (16 + (fl & 3)) * 4;  // a valid row's feature dword / a pad dword
+    const int src_lane = (q4 * XFC + fl) * 4;
+    const int in_lane = (q4 * XCB * XFC + fl) * 4;
+    if (t0 < t1) {
+        load_Ao(sub_at(t0).M);
+        load_Ai(sub_at(t0).M);
+    }
+    asm volatile("s_barrier" ::: "memory");  // S(-1)
+#pragma unroll 1
+    for (int t = t0; t < t1; ++t) {
+        const TChunk cu = sub_at(t);
+        const int k = cu.k;
+        const int mlo = (XK * k) >> 4;
+        const bool active = mw == mlo || mw == mlo + 1;  // wave-uniform
+        const bool next_mid = k == 2 && t + 1 < t1 && ((t + 1) / 3) % nchu == 0;
+        const int cv = rk == k ? col_v : col_j;
+        const int po = opaque(TL_PART + (rv * TPA + wb * TPB) * 4 + cv);  // out: P[a = rv + r][b = wb]; + r TPA 4 + 2 j TPB 4
+        const int dg = opaque(TL_DIAG + ((rv * XK + wb) * 3 + k) * 4);     // + r K 12 + 2 j 12
+        if (active) {
+            // ---- out-phase: tiles (b = 2 j + wb, m = mw); P[a][b] (+)= sum_c Wout_k G_k[M.b.c] + Wdiag_k G_k[a.M.b]
+            auto rd_out = [&](int j, float (&x)[2][XS]) {
+#pragma unroll
+                for (int s = 0; s < XS; ++s) {
+                    x[0][s] = *reinterpret_cast<const float*>(L + TL_OUT + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
+                    x[1][s] =
+                        *reinterpret_cast<const float*>(L + TL_OUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
+                }
+            };
+            float xo[2][2][XS];
+            rd_out(0, xo[0]);
+#pragma unroll
+            for (int j = 0; j < XTPW; j += 2) {
+                float(&xc)[2][XS] = xo[(j >> 1) & 1];
+                if (j + 2 < XTPW) rd_out(j + 2, xo[((j >> 1) + 1) & 1]);
+                float w0[4], w1[4], s0[4], s1[4];
+                f4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    w0[r] = *reinterpret_cast<const float*>(L + dg + r * XK * 12 + 2 * j * 12);
+                    w1[r] = *reinterpret_cast<const float*>(L + dg + r * XK * 12 + (2 * j + 2) * 12);
+                    s0[r] = *reinterpret_cast<const float*>(L + self_b + r * XK * 64 + 2 * j * 64);
+                    s1[r] = *reinterpret_cast<const float*>(L + self_b + r * XK * 64 + (2 * j + 2) * 64);
+                }
+                if (k) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        acc0[r] = *reinterpret_cast<const float*>(L + po + r * TPA * 4 + 2 * j * TPB * 4);
+                        acc1[r] = *reinterpret_cast<const float*>(L + po + r * TPA * 4 + (2 * j + 2) * TPB * 4);
+                    }
+                }
+                asm volatile("" ::: "memory");  // the reads above are issued before the MFMAs below
+#pragma unroll
+                for (int s = 0; s < XS; ++s) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j][s], xc[0][s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j + 1][s], xc[1][s], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    *reinterpret_cast<float*>(L + po + r * TPA * 4 + 2 * j * TPB * 4) = __builtin_fmaf(w0[r], s0[r], acc0[r]);
+                    *reinterpret_cast<float*>(L + po + r * TPA * 4 + (2 * j + 2) * TPB * 4) =
+                        __builtin_fmaf(w1[r], s1[r], acc1[r]);
+                }
+                asm volatile("" ::: "memory");
+            }
+        }
+        if (next_mid) load_Ao(cu.M + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // M(t)
+        if (active) {
+            // ---- in-phase: tiles (a = 2 j + wb, m = mw); P[a][b] += sum_c Win_k G_k[c.a.M]
+            const int pi = opaque(TL_PART + (wb * TPA + rv * TPB) * 4 + cv);  // P[a = wb][b = rv + r]; + r TPB 4 + 2 j TPA 4
+            auto rd_in = [&](int j, float (&x)[2][XS]) {
+#pragma unroll
+                for (int s = 0; s < XS; ++s) {
+                    x[0][s] = *reinterpret_cast<const float*>(L + TL_IN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
+                    x[1][s] = *reinterpret_cast<const float*>(L + TL_IN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
+                }
+            };
+            float xi[2][2][XS];
+            rd_in(0, xi[0]);
+#pragma unroll
+            for (int j = 0; j < XTPW; j += 2) {
+                float(&xc)[2][XS] = xi[(j >> 1) & 1];
+                f4_t acc0, acc1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc0[r] = *reinterpret_cast<const float*>(L + pi + r * TPB * 4 + 2 * j * TPA * 4);
+                    acc1[r] = *reinterpret_cast<const float*>(L + pi + r * TPB * 4 + (2 * j + 2) * TPA * 4);
+                }
+                if (j + 2 < XTPW) rd_in(j + 2, xi[((j >> 1) + 1) & 1]);
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int s = 0; s < XS; ++s) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j][s], xc[0][s], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j + 1][s], xc[1][s], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    *reinterpret_cast<float*>(L + pi + r * TPB * 4 + 2 * j * TPA * 4) = acc0[r];
+                    *reinterpret_cast<float*>(L + pi + r * TPB * 4 + (2 * j + 2) * TPA * 4) = acc1[r];
+                }
+                asm volatile("" ::: "memory");
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // S(t)
+        if (k == 2) {
+            // ---- store-out: the 400 rows of P as 16-B pieces (1,600 pieces over the 512 compute lanes)
+            const int64_t mrow = (int64_t)(cu.M - p.m0) * p.zsm;
+            float* dxc = reinterpret_cast<float*>(p.Z) + cu.ch * XFC;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const int pc = (int)threadIdx.x + 512 * tt;
+                if (pc < XR * 4) {  // tt < 3: every lane; tt = 3: wave 0
+                    const int row = pc >> 2, q = pc & 3;
+                    const int a = row / XK, b = row - a * XK;
+                    f4_t v = *reinterpret_cast<const f4_t*>(L + TL_PART + (a * TPA + b * TPB + 4 * q) * 4);
+                    f4_t* dst = reinterpret_cast<f4_t*>(dxc + ((int64_t)a * p.zsa + mrow + b) * p.ldz + 4 * q);
+                    if (accumulate) v += *dst;
+                    *dst = v;
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // W(t): P read out before the next out-phase
+        if (next_mid) load_Ai(cu.M + 1);
+    }
+}
+
 // Plan construction: one thread per CSR row scatters its entries into the fragment-ordered slots.
 __global__ __launch_bounds__(256) void ngram_mplan_kernel(int64_t Kn1, int64_t n_rows, const int64_t* rowptr,
                                                           const int4* edges, float* plan, int* bad) {
@@ -585,6 +885,7 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const voi
     p.cstride = (p.nch % 2 == 0 && p.remap && total >= 2 && !(flags & PG_FLAG_MID_NO_PAIRS)) ? 2 : 1;
     p.chunks = (int)(total / p.cstride);
     p.stamps = stamps;
+    p.early_in = (flags & PG_FLAG_MID_LOADER_SYNC) ? 0 : 1;
     p.exp = stamps ? (int)((flags >> 24) & 15u) : 0;
     unsigned grid = (unsigned)(total < cap ? total : cap);
     if (p.cstride == 2) grid &= ~1u;
@@ -613,6 +914,49 @@ int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan
                                  void* stream) {
     return mid_launch(K, n, n_rows, plan, X, ldx, F, m_begin, m_end, true, nullptr, Z, ldz, flags, nullptr, true,
                       stream);
+}
+
+int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
+                            float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+    const char* name = "pg_spmm3t_ngram_mid_f32";
+    int64_t Kn1 = 0, Kn2 = 0;
+    PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
+    PG_REQUIRE(plan && G && dX, "null pointer");
+    PG_REQUIRE(ldg >= 3 * F && lddx >= F, "leading dimensions too small");
+    if (F <= 0 || F % XFC) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be a multiple of %d", name, XFC);
+    if (!pg::aligned16(G) || !pg::aligned16(dX) || !pg::aligned16(plan) || (ldg * 4) % 16 || (lddx * 4) % 16)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned G and dX rows", name);
+    PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 29), "too many column chunks");
+    XP p{};
+    p.Kn1 = Kn1;
+    p.Kn2 = Kn2;
+    p.m0 = 0;
+    p.zsa = Kn1;
+    p.zsm = XK;
+    p.plan = plan;
+    p.X = G;
+    p.ldx = ldg;
+    p.Z = dX;
+    p.ldz = lddx;
+    p.F = (int)F;
+    p.nch = (int)(F / XFC);
+    p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    const int64_t total = Kn2 * p.nch;
+    p.cstride = (p.nch % 2 == 0 && p.remap && total >= 2 && !(flags & PG_FLAG_MID_NO_PAIRS)) ? 2 : 1;
+    p.chunks = (int)(total / p.cstride);
+    p.early_in = (flags & PG_FLAG_MID_LOADER_SYNC) ? 0 : 1;
+    const int64_t cap = grid_cap();
+    unsigned grid = (unsigned)(total < cap ? total : cap);
+    if (p.cstride == 2) grid &= ~1u;
+    static bool attr_set = false;
+    if (!attr_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_midt_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, TL_BYTES) != hipSuccess)
+            return pg::set_error(PG_ERR_HIP, "%s: cannot raise the LDS limit", name);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(ngram_midt_kernel, dim3(grid), dim3(XTHREADS), TL_BYTES, (hipStream_t)stream, p, accumulate ? 1 : 0);
+    return pg::check_launch(name);
 }
 
 #ifdef PG_MID_STAMPS

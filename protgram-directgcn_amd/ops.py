@@ -289,7 +289,8 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
 
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
     """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX.
-    Same numerics note as spmm3: the n-gram tile kernel (symmetric graphs with a plan) needs finite G and matches the
+    Same numerics note as spmm3: the n-gram tile kernels (symmetric graphs with a plan: the transposed middle-tile
+    kernel under PG_FLAG_MID_TRANSPOSED, else the 4x4-block one for F in {64, 128, 256}) need finite G and match the
     CSR kernel within fp32 rounding; PG_FLAG_NO_NGRAM selects the CSR kernel (under AMP, GradScaler's scaled
     gradients can overflow to inf: the step is skipped either way, but the skipped values differ)."""
     lib = load_library()
@@ -322,6 +323,13 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     dX = torch.empty(N, F, device=G.device, dtype=torch.float32)
     fl = default_flags() if flags is None else flags
     s = _stream(G)
+    if g.shared and g.symmetric and G.size(0) == g.n_rows and (fl & _lib.PG_FLAG_MID_TRANSPOSED) and _mid_ok(g, dX, fl):
+        ng = g.ngram  # the transposed middle-tile kernel (opt-in: slower than the 4x4-block kernel)
+        rc = lib.pg_spmm3t_ngram_mid_f32(ng.K, ng.n, N, _p(ng.mplan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,
+                                         fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_spmm3t_ngram_mid_f32")
+            return dX
     if g.shared and g.symmetric and G.size(0) == g.n_rows and _ngram_ok(g, dX, fl, (64, 128, 256)):
         ng = g.ngram
         rc = lib.pg_spmm3t_ngram_f32(ng.K, ng.n, N, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0, fl, s)

@@ -55,6 +55,8 @@ def test_ngram_spmm3_vs_csr(pkg, cuda, n, keep, F):
     Zc = ops.spmm3(g, x, flags=_csr_flag())
     assert_close(Z, Zc, f"n={n} keep={keep} F={F}")
     assert torch.equal(ops.spmm3(g, x), Z)  # deterministic
+    from protgram_directgcn_amd._lib import PG_FLAG_MID_LOADER_SYNC
+    assert torch.equal(ops.spmm3(g, x, flags=ops.default_flags() | PG_FLAG_MID_LOADER_SYNC), Z)  # speed only
     Zb = ops.spmm3(g, x, flags=b4)  # the 4x4-block tile kernel
     assert_close(Zb, Zc, f"block4 n={n} keep={keep} F={F}")
     assert torch.equal(ops.spmm3(g, x, flags=b4), Zb)
@@ -72,14 +74,36 @@ def test_ngram_spmm3_vs_csr(pkg, cuda, n, keep, F):
     assert_close(Zg, ref, f"gated n={n} F={F}")
 
 
-@pytest.mark.parametrize("n,keep", [(3, 1.0), (3, 0.5), (4, 1.0)])
-@pytest.mark.parametrize("F", [64, 128, 256])
+@pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
+@pytest.mark.parametrize("F", [16, 48, 64, 128, 256])
 def test_ngram_spmm3t_vs_csr(pkg, cuda, n, keep, F):
+    """The transposed middle-tile kernel (PG_FLAG_MID_TRANSPOSED; F % 16 == 0, odd chunk counts run without
+    workgroup pairs; both loader protocols) and the 4x4-block transposed kernel (default) against the CSR kernel; the
+    middle-tile kernel's accumulate mode."""
     from protgram_directgcn_amd import ops
+    from protgram_directgcn_amd._lib import PG_FLAG_MID_LOADER_SYNC, PG_FLAG_MID_TRANSPOSED, load_library
     g = _graph(pkg, cuda, n, keep)
     assert g.ngram is not None and g.symmetric
     G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(F)).to(cuda)
-    assert_close(ops.spmm3_t(g, G), ops.spmm3_t(g, G, flags=_csr_flag()), f"transposed n={n} F={F}")
+    ref = ops.spmm3_t(g, G, flags=_csr_flag())
+    mid = ops.default_flags() | PG_FLAG_MID_TRANSPOSED
+    got = ops.spmm3_t(g, G, flags=mid)
+    assert_close(got, ref, f"transposed middle-tile n={n} F={F}")
+    assert torch.equal(ops.spmm3_t(g, G, flags=mid), got)  # deterministic
+    assert torch.equal(ops.spmm3_t(g, G, flags=mid | PG_FLAG_MID_LOADER_SYNC), got)  # loader protocol: speed only
+    if F in (64, 128, 256):
+        assert_close(ops.spmm3_t(g, G), ref, f"block4 (default) n={n} F={F}")
+    # accumulate: dX += A^T G through the C ABI, on a strided G view
+    lib = load_library()
+    Gw = torch.randn(g.n_rows, 3 * F + 16, generator=torch.Generator().manual_seed(7)).to(cuda)
+    Gw[:, :3 * F] = G
+    dX = torch.randn(g.n_rows, F, generator=torch.Generator().manual_seed(8)).to(cuda)
+    want = dX + ref
+    ng = g.ngram
+    rc = lib.pg_spmm3t_ngram_mid_f32(ng.K, ng.n, g.n_rows, ng.mplan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
+                                     dX.data_ptr(), dX.stride(0), 1, ops.default_flags(), ops._stream(dX))
+    assert rc == 0
+    assert_close(dX, want, f"accumulate n={n} F={F}")
 
 
 def test_ngram_spmm3_vs_oracle_and_fallback_widths(pkg, cuda):

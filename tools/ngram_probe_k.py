@@ -13,7 +13,8 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
-from protgram_directgcn_amd._lib import PG_FLAG_NGRAM_BLOCK4, PG_FLAG_NO_NGRAM  # noqa: E402
+from protgram_directgcn_amd._lib import (PG_FLAG_MID_LOADER_SYNC, PG_FLAG_MID_TRANSPOSED,  # noqa: E402
+                                         PG_FLAG_NGRAM_BLOCK4, PG_FLAG_NO_NGRAM)
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 F = int(sys.argv[2]) if len(sys.argv) > 2 else 128
@@ -46,7 +47,12 @@ cases = {"fwd_ngram": lambda: ops.spmm3(g, x), "gated_ngram": lambda: ops.spmm3_
          "fwd_block4": lambda: ops.spmm3(g, x, flags=PG_FLAG_NGRAM_BLOCK4),
          "gated_block4": lambda: ops.spmm3_gated(g, x, prm, 0, flags=PG_FLAG_NGRAM_BLOCK4),
          "fwd_csr": lambda: ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM),
-         "bwd_ngram": lambda: ops.spmm3_t(g, G), "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
+         "fwd_sync": lambda: ops.spmm3(g, x, flags=ops.default_flags() | PG_FLAG_MID_LOADER_SYNC),
+         "bwd_ngram": lambda: ops.spmm3_t(g, G),
+         "bwd_mid": lambda: ops.spmm3_t(g, G, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED),
+         "bwd_mid_sync": lambda: ops.spmm3_t(g, G, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED
+                                             | PG_FLAG_MID_LOADER_SYNC),
+         "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
 for a in ALT:
     cases[f"fwd_alt{a:#x}"] = (lambda a: lambda: ops.spmm3(g, x, flags=a))(a)
     cases[f"gated_alt{a:#x}"] = (lambda a: lambda: ops.spmm3_gated(g, x, prm, 0, flags=a))(a)
@@ -59,6 +65,9 @@ ref = ops.spmm3(g, x, flags=PG_FLAG_NO_NGRAM)
 for k in [c for c in ["fwd_ngram", "fwd_block4"] + [f"fwd_alt{a:#x}" for a in ALT] if c in cases]:
     z = cases[k]()
     print(f"{k}: max |d| vs csr {float((z - ref).abs().max()):.3e}")
+refb = ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)
+for k in ("bwd_ngram", "bwd_mid"):
+    print(f"{k}: max |d| vs csr {float((cases[k]() - refb).abs().max()):.3e} (max |ref| {float(refb.abs().max()):.3e})")
 refg = ops.spmm3_gated(g, x, prm, 0, flags=PG_FLAG_NO_NGRAM)
 for k in [c for c in ("gated_ngram", "gated_block4") if c in cases]:
     z = cases[k]()

@@ -431,7 +431,7 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
     tiled fp32 kernel, PG_FLAG_DENSE_TILED; pre-gated operands) against the same formula in float64. Pre-gated: the
     operand is s_q * Z_q (what pg_spmm3_gated_f32 stores) with PG_FLAG_DENSE_PREGATED."""
     from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_TILED, PG_FLAG_NO_XCD_REMAP
+    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_A_CACHED, PG_FLAG_DENSE_TILED, PG_FLAG_NO_XCD_REMAP
     g = torch.Generator().manual_seed(M + Fin + Fout)
     Ntot = M + 37
     Z = torch.randn(M, 3 * Fin, generator=g)
@@ -465,7 +465,8 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
         y = y + (xres.double() @ W_res.double().t() + b_res.double() if proj else xres.double())
     y = torch.nn.functional.leaky_relu(y, 0.01)
     dv = {k: v.to(cuda) for k, v in prm.items()}
-    for fl in (0, PG_FLAG_DENSE_TILED, PG_FLAG_NO_XCD_REMAP | PG_FLAG_DENSE_TILED, PG_FLAG_NO_XCD_REMAP):
+    for fl in (0, PG_FLAG_DENSE_A_CACHED, PG_FLAG_DENSE_TILED, PG_FLAG_NO_XCD_REMAP | PG_FLAG_DENSE_TILED,
+               PG_FLAG_NO_XCD_REMAP):
         out = ops.layer_dense(Z.to(cuda), dv, gate, rows=None if r is None else r.to(cuda),
                               constant=None if const is None else const.to(cuda),
                               res_x=None if xres is None else xres.to(cuda),

@@ -67,7 +67,9 @@ struct DenseP {
     // and / or writes its output row (map_y) at the global n-gram row a.M.b = a K^(n-1) + 20 M + b
     int64_t map_kn1, map_m0;
     int map_res, map_y;
-    int nt_a;  // pipelined kernels: A rows (read once) by non-temporal LDS-DMA (PG_FLAG_DENSE_A_CACHED clears)
+    int nt_a;  // pipelined kernels: A rows and the per-node constant (read once) by non-temporal LDS-DMA
+               // (PG_FLAG_DENSE_A_CACHED clears)
+    int nt_r;  // experiment: the residual rows by non-temporal LDS-DMA (PG_FLAG_EXP_RES_NT)
     int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
 };
 
@@ -362,8 +364,9 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
 __device__ __forceinline__ void glds16(const float* src, float* lds_base) {
     __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 0);
 }
-// the same with the non-temporal cache policy (aux = 2): the A rows, read once (measured: 0.5587 -> 0.5496 ms per
-// bench step, the next layer's propagation finding its input in cache; PG_FLAG_DENSE_A_CACHED selects the default policy)
+// the same with the non-temporal cache policy (aux = 2): the A rows and the per-node constant, read once (measured:
+// 0.5587 -> 0.5496 ms per bench step for the A rows, the next layer's propagation finding its input in cache, and
+// 0.550 -> 0.545 ms for the constant; PG_FLAG_DENSE_A_CACHED selects the default policy for both)
 __device__ __forceinline__ void glds16nt(const float* src, float* lds_base) {
     __builtin_amdgcn_global_load_lds(src, lds_base, 16, 0, 2);
 }
@@ -869,8 +872,10 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         const float* rb = !id_res    ? p.Z + m0 * p.ldz
                           : p.map_res ? p.res_x + ngram_row(p, m0 + rr) * p.ld_res
                                       : p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res);
-        glds16(cb + 4 * (ln & 31), Cs + wave * 256);
-        glds16(rb + 4 * (ln & 31), Rs + wave * 256);
+        if (p.nt_a) glds16nt(cb + 4 * (ln & 31), Cs + wave * 256);
+        else glds16(cb + 4 * (ln & 31), Cs + wave * 256);
+        if (p.nt_r) glds16nt(rb + 4 * (ln & 31), Rs + wave * 256);
+        else glds16(rb + 4 * (ln & 31), Rs + wave * 256);
     };
     auto gates = [&](int slot, int r, float& s0, float& s1, float& s2) {
         float c[5];
@@ -1129,6 +1134,7 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.nt_a = (flags & PG_FLAG_DENSE_A_CACHED) ? 0 : 1;
+    p.nt_r = (flags & PG_FLAG_EXP_RES_NT) ? 1 : 0;
 #ifdef PG_DENSE_EXP
     p.exp = (int)((flags >> 24) & 31u);
 #endif

@@ -87,7 +87,6 @@ typedef struct pg_edge1 {
                                              before the store-out barrier */
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
-#define PG_FLAG_EXP_RES_NT (1u << 10)   /* experiment: the dense kernel's residual rows by non-temporal LDS-DMA */
 #define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernel
                                              (pg_spmm3t_ngram_mid_f32) instead of the 4x4-block one */
 

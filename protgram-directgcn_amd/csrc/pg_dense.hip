@@ -69,7 +69,6 @@ struct DenseP {
     int map_res, map_y;
     int nt_a;  // pipelined kernels: A rows and the per-node constant (read once) by non-temporal LDS-DMA
                // (PG_FLAG_DENSE_A_CACHED clears)
-    int nt_r;  // experiment: the residual rows by non-temporal LDS-DMA (PG_FLAG_EXP_RES_NT)
     int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
 };
 
@@ -874,8 +873,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                                       : p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res);
         if (p.nt_a) glds16nt(cb + 4 * (ln & 31), Cs + wave * 256);
         else glds16(cb + 4 * (ln & 31), Cs + wave * 256);
-        if (p.nt_r) glds16nt(rb + 4 * (ln & 31), Rs + wave * 256);
-        else glds16(rb + 4 * (ln & 31), Rs + wave * 256);
+        glds16(rb + 4 * (ln & 31), Rs + wave * 256);
     };
     auto gates = [&](int slot, int r, float& s0, float& s1, float& s2) {
         float c[5];
@@ -1134,7 +1132,6 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.nt_a = (flags & PG_FLAG_DENSE_A_CACHED) ? 0 : 1;
-    p.nt_r = (flags & PG_FLAG_EXP_RES_NT) ? 1 : 0;
 #ifdef PG_DENSE_EXP
     p.exp = (int)((flags >> 24) & 31u);
 #endif

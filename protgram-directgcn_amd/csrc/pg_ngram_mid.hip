@@ -253,7 +253,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         XSTAMP(XSTAMP_LAST, 6);
         asm volatile("s_barrier" ::: "memory");  // S(-1)
-        int ci = 0;
+        [[maybe_unused]] int ci = 0;  // chunk slot of the diagnostics build's time stamps
 #pragma unroll 1
         for (int g = g0; g < g1; ++g) {
             const bool more = g + 1 < g1;
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     }
     asm volatile("s_barrier" ::: "memory");  // S(-1)
     XSTAMP(XSTAMP_LAST, 6);
-    int ci = 0;
+    [[maybe_unused]] int ci = 0;  // chunk slot of the diagnostics build's time stamps
 #pragma unroll 1
     for (int g = g0; g < g1; ++g) {
         const Chunk cu = chunk_at(g);

@@ -10,7 +10,8 @@
 // fallback kernel. The model's own shape (F = 128 -> 64 -> C <= 32) runs head_x3_kernel (split-bf16 decoder 1;
 // head_f128_kernel, its fp32-MFMA predecessor, with -DPG_HEAD_FP32). A persistent form of head_x3_kernel (W1 splits
 // and W2 kept in registers across a block's 32-row tiles, next tile's rows loaded behind the math; 128 VGPRs, four
-// blocks per CU) measured 0.062 ms against 0.050 for one tile per block.
+// blocks per CU) measured 0.062 ms against 0.050 for one tile per block; two 32-row tiles per block (W1 splits loaded
+// once per block; 128 VGPRs, occupancy 4) made the bench step 0.547 -> 0.580 ms (round 3).
 #include "pg_common.h"
 #include "pg_split3.h"
 

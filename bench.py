@@ -20,9 +20,15 @@ Default (auto): AUTO_PARTITION below (by rank count, from the round-3 per-rank m
 Timing: W warmup steps, then exactly K steps between barrier + synchronize on both sides; the max
 over ranks is reported. Rank 0 prints one JSON line.
 
-Extra fields: "roofline" for the dominant kernel (pg_spmm3_f32: algorithmic bytes per launch / its
-average duration from HIP events recorded on its launch stream inside the timed region) and
-"cpu_baseline" (the oracle = the reference's CPU algorithm, timed on this host, rank 0 at N=1).
+At N = 1 the forward is captured once as a HIP graph and replayed in the timed loop, as each rank's work is at
+N > 1 (MiddleRunner), so the 1 -> N curve compares like with like (--no-graphs: eager everywhere).
+
+Extra fields: "roofline" for the dominant kernel, chosen by measured time per step, with "roofline.kernels" holding
+one entry per hot-path kernel (the propagation -- pg_spmm3_ngram_mid_f32 at B(20,4) --, the dense layer
+pg_directgcn_dense_f32 and the head): compulsory bytes per launch / its average launch duration from HIP events
+recorded on its launch stream (eager steps right after the timed region), and the L2-miss traffic of each measured by
+two rocprofv3 --pmc passes in the same run; "cpu_baseline" (the oracle = the reference's CPU algorithm, timed on
+this host, rank 0 at N=1).
 """
 from __future__ import annotations
 
@@ -73,8 +79,10 @@ def parse():
                     "rank, the last over the rank's middles (no collective); 'auto' (default) = AUTO_PARTITION by rank "
                     "count (at few ranks a rank's ghost rows go over few links: the exchange costs more than "
                     "recomputing, DESIGN.md 5c)")
-    ap.add_argument("--no-graphs", action="store_true", help="N>1 middle partition: eager launches instead of the "
-                    "per-segment HIP graphs")
+    ap.add_argument("--no-graphs", action="store_true", help="eager launches instead of HIP graph replays (N=1: the "
+                    "whole forward captured once; N>1 middle partition: the per-segment graphs)")
+    ap.add_argument("--kernel-reps", type=int, default=10, help="eager steps after the timed region whose launches "
+                    "are timed with HIP events (per-kernel roofline)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); 'gloo' only to rehearse N>1 on one GPU")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo only)")
     ap.add_argument("--launch-check", action="store_true", help="N>1 plumbing check without a GPU: start the ranks, "
@@ -208,15 +216,26 @@ def main():
     elif world > 1:
         part = shard.partition(g, rank, world)
 
-    def step():
+    def eager_step():
         with torch.no_grad():
             if mp is not None:
-                return mid_run()
+                return mid_run._run_eager()
             if hp is not None:
                 return shard.halo_forward(model, hp, halo_in)
             if part is None:
                 return model(data)
             return shard.sharded_forward(model, part, x, chunks=args.chunks or 4)
+
+    # The timed step. At N = 1 the forward is captured once as a HIP graph and replayed, as a rank's work is at
+    # N > 1 (MiddleRunner's per-segment graphs): the 1 -> N ratio compares like with like. --no-graphs: eager.
+    graph_step = None
+    if mp is not None:
+        step = mid_run  # replays its captured segments (eager with --no-graphs)
+    elif world == 1 and not args.no_graphs:
+        graph_step = GraphStep(eager_step)
+        step = graph_step
+    else:
+        step = eager_step
 
     # untimed clock ramp: the GPU's clocks take ~100 ms of load to settle (5 warm-up steps measured 0.915 ms/step,
     # 50 or 200 gave 0.62): run steps for args.clock_warmup_s seconds before the W counted warm-up steps, so a short
@@ -231,7 +250,6 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    ops.SPMM_EVENTS = []
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -242,25 +260,29 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
-    if not events and mp is not None:  # graph replays record no per-launch events: time eager forwards (untimed)
-        ops.SPMM_EVENTS = []
-        for _ in range(10):
-            with torch.no_grad():
-                mid_run._run_eager()
-        torch.cuda.synchronize()
-        events, ops.SPMM_EVENTS = ops.SPMM_EVENTS, None
-    spmm_ms = [e0.elapsed_time(e1) for e0, e1 in events]
-    t_local = torch.tensor([elapsed, sum(spmm_ms) / max(1, len(spmm_ms))], dtype=torch.float64, device=dev)
+    # per-kernel launch durations: HIP events recorded on each launch's stream around every propagation, dense and
+    # head launch of eager runs of the same step right after the timed region (graph replays carry no per-launch
+    # events; the kernels are the same). rocprofv3's kernel trace of the same command agrees (profiles/).
+    ops.SPMM_EVENTS, ops.DENSE_EVENTS, ops.HEAD_EVENTS = [], [], []
+    for _ in range(args.kernel_reps):
+        eager_step()
+    torch.cuda.synchronize()
+    evs = {"propagation": ops.SPMM_EVENTS, "dense": ops.DENSE_EVENTS, "head": ops.HEAD_EVENTS}
+    ops.SPMM_EVENTS = ops.DENSE_EVENTS = ops.HEAD_EVENTS = None
+    kms = {k: [e0.elapsed_time(e1) for e0, e1 in v] for k, v in evs.items()}
+    t_local = torch.tensor([elapsed] + [sum(v) / max(1, len(v)) for v in kms.values()], dtype=torch.float64,
+                           device=dev)
     if world > 1:
         dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
-    elapsed, spmm_avg_ms = float(t_local[0]), float(t_local[1])
+    elapsed = float(t_local[0])
+    avg_ms = dict(zip(kms, (float(v) for v in t_local[1:].tolist())))
+    spmm_avg_ms = avg_ms["propagation"]
     ms_per_step = elapsed / args.steps * 1e3
     edges_per_step = 3 * g.nnz * L
     value = edges_per_step * args.steps / elapsed
 
-    # roofline of the dominant kernel, priced on SURVEY 8(d)'s COMPULSORY bytes per launch (rowptr + records once,
-    # each X row once, 3 output rows, gates): the floor of HBM traffic for one propagation launch
+    # roofline of each hot-path kernel, priced on SURVEY 8(d)'s COMPULSORY bytes per launch (its inputs once, its
+    # outputs once): the floor of HBM traffic for one launch
     el = 2 if args.bf16 else 4
     gated = (world == 1 or hp is not None) and ops.PREGATED_INFERENCE and not args.fused_norm and not args.bf16
     if mp is not None:
@@ -301,17 +323,63 @@ def main():
             kname = "pg_spmm3_bf16" if args.bf16 else "pg_spmm3_f32"
             comp = mp.own_csr.compulsory_bytes(Fd, elem=el, gated=False)
     noreuse = sum(gi.algorithmic_bytes(Fd, elem=el) for gi in launch_graphs) // len(launch_graphs)
-    achieved = comp / (spmm_avg_ms * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "kernel": kname,
-                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_model": ("compulsory: the kernel's own inputs once (n-gram tile kernel: its plan weights; CSR kernels: "
-                                "8(N+1) rowptr + 16 B records per entry, SURVEY 8d) + X once + 3 output rows "
-                                "(+ 20 B/row gates)"),
-                "algorithmic_bytes_per_launch": comp, "avg_launch_ms": round(spmm_avg_ms, 4),
-                "launches_timed": len(spmm_ms),
-                "no_reuse_bytes_per_launch": noreuse,
-                "no_reuse_gbs": round(noreuse / (spmm_avg_ms * 1e-3) / 1e9, 1)}
+    # rows per dense launch (mean over the step's L launches) and per head launch
+    if mp is not None:
+        own = mp.n_own
+        dense_rows = ((L - 1) * N + own) / L if mid_run.replicate else own
+        head_rows = own
+    elif hp is not None:
+        dense_rows, head_rows = sum(hp.layer_rows) / L, hp.owned
+    elif part is not None:
+        dense_rows = head_rows = part.n_local
+    else:
+        dense_rows = head_rows = N
+    C = 20
+    # dense: Z (3F) + residual row (F) + constant (F_out fp32) + 5 gates (fp32; pre-gated Z: none) + Y, + weights;
+    # head: h row + log-probs + embedding row (fp32), + decoder weights
+    dense_comp = int(dense_rows * (3 * Fd * el + Fd * el + Fd * 4 + (0 if gated else 20) + Fd * el)
+                     + 4 * (4 * Fd * Fd + 6 * Fd))
+    H = Fd // 2
+    head_comp = int(head_rows * (Fd * el + C * 4 + Fd * 4) + 4 * (H * Fd + H + C * H + C))
+    dense_name = ("pg_directgcn_dense_ngram_rows_f32" if mp is not None and getattr(mid_run, "mapped", False)
+                  else "pg_directgcn_dense_" + ("bf16" if args.bf16 else "f32"))
+    head_name = "pg_directgcn_head_" + ("bf16" if args.bf16 else "f32")
+    per_step = {"propagation": L, "dense": L, "head": 1}
+
+    def entry(cls, name, nbytes, extra=None):
+        ms = avg_ms[cls]
+        ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        e = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": int(nbytes),
+             "avg_launch_ms": round(ms, 4), "launches_timed": len(kms[cls]), "launches_per_step": per_step[cls],
+             "ms_per_step": round(ms * per_step[cls], 4)}
+        if extra:
+            e.update(extra)
+        return e
+
+    kernels = {
+        "propagation": entry("propagation", kname, comp,
+                             {"no_reuse_bytes_per_launch": noreuse,
+                              "no_reuse_gbs": round(noreuse / (spmm_avg_ms * 1e-3) / 1e9, 1) if spmm_avg_ms else None,
+                              "bytes_model": "compulsory: the kernel's own inputs once (n-gram tile kernel: its plan "
+                                             "weights; CSR kernels: 8(N+1) rowptr + 16 B records per entry, SURVEY "
+                                             "8d) + X once + 3 output rows (+ 20 B/row gates)"}),
+        "dense": entry("dense", dense_name, dense_comp,
+                       {"bytes_model": "Z (3F) + residual row (F) + per-node constant (F_out, fp32) + 5 gates (fp32) "
+                                       "+ output row, per row; + the layer's weights"}),
+        "head": entry("head", head_name, head_comp,
+                      {"bytes_model": "h row + log-probs + L2-normalised embedding (fp32), per row; + the decoder"}),
+    }
+    dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+    roofline = dict(kernels[dominant])
+    roofline["dominant_by"] = ("measured time per step (avg launch ms x launches per step, HIP events): "
+                               + ", ".join(f"{k} {v['ms_per_step']} ms" for k, v in kernels.items()))
+    roofline["kernels"] = kernels
+    roofline["timing"] = ("step: " + ("HIP graph replays" if (graph_step is not None or (mp is not None and
+                                                                                     mid_run.graphs is not None))
+                                      else "eager launches")
+                          + f"; per-kernel: HIP events around each launch of {args.kernel_reps} eager steps "
+                            "after the timed region, on the launch stream")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -320,11 +388,17 @@ def main():
     if rank == 0 and world == 1 and not args.no_pmc:
         pmc = pmc_traffic(args, log)
         if pmc is not None:
-            roofline.update(pmc)
-            if roofline.get("traffic"):
-                roofline["traffic_gbs"] = round(roofline["traffic"] / (spmm_avg_ms * 1e-3) / 1e9, 1)
-                roofline["traffic_frac"] = round(roofline["traffic_gbs"] / HBM_PEAK_GBS, 4)
-                roofline["traffic_over_compulsory"] = round(roofline["traffic"] / comp, 3)
+            for cls, ent in list(kernels.items()) + [(dominant, roofline)]:
+                hit = pmc["by_class"].get(cls)
+                if not hit:
+                    continue
+                ent["traffic"] = hit["bytes_per_launch"]
+                ent["traffic_kernel"] = hit["kernel"]
+                ent["traffic_source"] = pmc["traffic_source"]
+                ms = ent["avg_launch_ms"]
+                ent["traffic_gbs"] = round(ent["traffic"] / (ms * 1e-3) / 1e9, 1) if ms else None
+                ent["traffic_frac"] = round(ent["traffic_gbs"] / HBM_PEAK_GBS, 4) if ms else None
+                ent["traffic_over_compulsory"] = round(ent["traffic"] / ent["algorithmic_bytes_per_launch"], 3)
 
     extra = {}
     if args.extra and world == 1:
@@ -360,6 +434,26 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class GraphStep:
+    """A step captured once as a HIP graph (torch.cuda.CUDAGraph) and replayed; returns the graph's static outputs
+    (overwritten by the next replay). Two eager runs first (lazy library state, allocator pools, the COO -> CSR
+    cache); the capture mode is thread-local."""
+
+    def __init__(self, fn):
+        import torch
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            self.out = fn()
+        torch.cuda.synchronize()
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out
 
 
 def bench_model(pkg, N, Fd, L, n, C=20):
@@ -417,9 +511,10 @@ def pmc_traffic(args, log, timeout=240):
     shutil.rmtree(out, ignore_errors=True)
     if not res.get("kernel"):
         return None
-    log(f"[bench] PMC traffic ({time.time() - t0:.0f}s): {res['kernel']}: {res['kernel_bytes_per_launch'] / 1e6:.1f} MB "
-        f"per launch")
-    return {"traffic": res["kernel_bytes_per_launch"], "traffic_kernel": res["kernel"],
+    log(f"[bench] PMC traffic ({time.time() - t0:.0f}s): " + "; ".join(
+        f"{k}: {v['kernel'][:60]} {v['bytes_per_launch'] / 1e6:.1f} MB per launch"
+        for k, v in res.get("by_class", {}).items()))
+    return {"by_class": res.get("by_class", {}),
             "traffic_source": "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
                               "tools/kprobe.py --forward (this bench's step), read = 2 x FETCH_SIZE KiB, "
                               "write = WRITE_SIZE KiB, per launch"}

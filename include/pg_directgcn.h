@@ -190,7 +190,7 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* args, const float* packed, uin
  * partition reads its layer input and writes its layer output in the global row layout directly (no row gather /
  * scatter around the launch). Same arithmetic as pg_directgcn_dense_f32 (bit-identical rows). Only the pipelined
  * split-bf16 kernel's shape (F_in = F_out = 128, no W_res, no rows, 16-B aligned): PG_ERR_UNSUPPORTED otherwise.
- * Requires args->M a multiple of 400 and m0 + M / 400 <= Kn1 / 20. (Replaces, for a middle range, the same
+ * Requires K = 20 (Kn1 a power of 20), args->M a multiple of 400 and m0 + M / 400 <= Kn1 / 20. (Replaces, for a middle range, the same
  * protgram_directgcn.py:100-133 + :213-215 as pg_directgcn_dense_f32.) */
 int pg_directgcn_dense_ngram_rows_f32(const pg_layer_args_t* args, const float* packed, int64_t Kn1, int64_t m0,
                                       int32_t map_res, int32_t map_y, uint32_t flags, void* stream);

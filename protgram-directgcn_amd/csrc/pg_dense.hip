@@ -1209,8 +1209,11 @@ int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32
 int pg_directgcn_dense_ngram_rows_f32(const pg_layer_args_t* a, const float* packed, int64_t Kn1, int64_t m0,
                                       int32_t map_res, int32_t map_y, uint32_t flags, void* stream) {
     PG_REQUIRE(a != nullptr, "null args");
-    PG_REQUIRE(Kn1 >= 20 && Kn1 % 20 == 0 && m0 >= 0 && m0 < Kn1, "bad n-gram map (Kn1 = %lld, m0 = %lld)",
-               (long long)Kn1, (long long)m0);
+    // the row map is the K = 20 grid (ngram_row): Kn1 must be K^(n-1) = 20^(n-1), not merely a multiple of 20
+    int64_t pw = 20;
+    while (pw < Kn1 && pw <= (int64_t(1) << 56)) pw *= 20;
+    PG_REQUIRE(Kn1 >= 20 && pw == Kn1 && m0 >= 0 && m0 < Kn1,
+               "bad n-gram map (Kn1 = %lld must be a power of K = 20; m0 = %lld)", (long long)Kn1, (long long)m0);
     PG_REQUIRE(a->M % 400 == 0 && a->M < (int64_t(1) << 31), "rows must be whole middles (M = %lld)", (long long)a->M);
     PG_REQUIRE(!map_res || a->res_x, "map_res needs res_x");
     PG_REQUIRE(m0 + a->M / 400 <= Kn1 / 20, "middles [%lld, %lld) past the graph's %lld", (long long)m0,

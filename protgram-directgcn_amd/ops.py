@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import functools
+import weakref
 from typing import Optional
 
 import torch
@@ -25,24 +26,27 @@ BF16_BACKWARD = True  # bf16 mode trains through pg_directgcn_dense_bwd_bf16 / p
 # dense kernel on the pre-gated operand; False = the training-path kernels in inference too.
 PREGATED_INFERENCE = True
 
-# Optional live timing of the propagation kernel: when set to a list, spmm3 appends one
-# (start, end) pair of HIP events recorded on the launch stream around each propagation launch.
-SPMM_EVENTS: Optional[list] = None
+# Optional live timing of the hot-path kernels: when set to a list, each launch of that class appends one
+# (start, end) pair of HIP events recorded on its launch stream around it (bench.py's per-kernel roofline):
+SPMM_EVENTS: Optional[list] = None   # propagation (spmm3, spmm3_middles, spmm3_gated)
+DENSE_EVENTS: Optional[list] = None  # dense layer (layer_dense, layer_dense_ngram_rows)
+HEAD_EVENTS: Optional[list] = None   # fused head (head)
 
 
-def _ev_start(x):
-    if SPMM_EVENTS is None:
+def _ev_start(x, kind: str = "SPMM"):
+    if globals()[kind + "_EVENTS"] is None:
         return None
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record(torch.cuda.current_stream(x.device))
     return e0
 
 
-def _ev_end(x, e0):
-    if e0 is not None:
+def _ev_end(x, e0, kind: str = "SPMM"):
+    lst = globals()[kind + "_EVENTS"]
+    if e0 is not None and lst is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(torch.cuda.current_stream(x.device))
-        SPMM_EVENTS.append((e0, e1))
+        lst.append((e0, e1))
 
 
 def _require_graph_on(g, x):
@@ -189,13 +193,39 @@ def spmm3_middles(g: CSRGraph, x: torch.Tensor, m_begin: int, m_end: int, flags:
     return Z
 
 
-def rows_gather(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[i] = src[idx[i]] (pg_rows_gather; rows of any dtype, unit column stride)."""
+_IDX_OK: dict = {}
+
+
+def _check_index(idx: torch.Tensor, n: int, distinct: bool, what: str):
+    """Range (and, for scatters, distinctness) check of a row-index tensor, once per tensor: the entry holds a weak
+    reference, so a new tensor at a reused address never hits it. One host sync on a miss: callers that capture HIP
+    graphs (shard.MiddleRunner) pass indices built and checked at setup with check=False instead."""
+    k = (idx.data_ptr(), idx._version, idx.numel(), str(idx.device), int(n), bool(distinct))
+    hit = _IDX_OK.get(k)
+    if hit is not None and hit() is idx:
+        return
+    if idx.numel():
+        lo, hi = int(idx.min()), int(idx.max())
+        if lo < 0 or hi >= n:
+            raise IndexError(f"{what}: row indices in [{lo}, {hi}] outside [0, {n})")
+        if distinct and int(torch.unique(idx).numel()) != idx.numel():
+            raise ValueError(f"{what}: indices must be distinct (each destination row written once)")
+    if len(_IDX_OK) > 256:
+        _IDX_OK.clear()
+    _IDX_OK[k] = weakref.ref(idx)
+
+
+def rows_gather(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None,
+                check_idx: bool = True) -> torch.Tensor:
+    """out[i] = src[idx[i]] (pg_rows_gather; rows of any dtype, unit column stride). The indices are range-checked
+    once per index tensor (IndexError); check_idx=False skips that (indices known valid, e.g. inside a capture)."""
     lib = load_library()
     _require_gpu(src)
     if src.dim() != 2 or src.stride(1) != 1:
         raise ValueError("rows_gather needs a 2-D source with unit column stride")
     idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+    if check_idx:
+        _check_index(idx, src.size(0), False, "rows_gather")
     out = out if out is not None else torch.empty(idx.numel(), src.size(1), device=src.device, dtype=src.dtype)
     if out.shape != (idx.numel(), src.size(1)) or out.dtype != src.dtype or out.stride(1) != 1:
         raise ValueError("rows_gather: out must be [len(idx), src.size(1)] of src's dtype")
@@ -205,8 +235,10 @@ def rows_gather(src: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor
     return out
 
 
-def rows_scatter(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
-    """dst[idx[i]] = src[i] (pg_rows_scatter; distinct indices; rows of any dtype, unit column stride)."""
+def rows_scatter(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor, check_idx: bool = True) -> torch.Tensor:
+    """dst[idx[i]] = src[i] (pg_rows_scatter; distinct indices; rows of any dtype, unit column stride). The indices
+    are checked once per index tensor for range (IndexError) and distinctness (ValueError); check_idx=False skips
+    that (indices known valid, e.g. inside a capture)."""
     lib = load_library()
     _require_gpu(src)
     if src.dim() != 2 or dst.dim() != 2 or src.size(1) != dst.size(1) or src.dtype != dst.dtype:
@@ -214,6 +246,8 @@ def rows_scatter(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor) -> tor
     if src.stride(1) != 1 or dst.stride(1) != 1 or idx.numel() != src.size(0):
         raise ValueError("rows_scatter: unit column strides and one index per source row")
     idx = idx.to(device=src.device, dtype=torch.int64).contiguous()
+    if check_idx:
+        _check_index(idx, dst.size(0), True, "rows_scatter")
     es = src.element_size()
     check(lib.pg_rows_scatter(_p(src), src.stride(0) * es, _p(idx), idx.numel(), src.size(1) * es, _p(dst),
                               dst.stride(0) * es, _stream(src)), "pg_rows_scatter")
@@ -491,13 +525,17 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
         raw = [_f32c(prm[k].detach()) for k in _PACK_KEYS]
         (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
          a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared) = [_p(t) for t in raw]
+        ev = _ev_start(Z, "DENSE")
         rc = lib.pg_directgcn_dense_f32(ctypes.byref(a), None, fl, _stream(Z))
         if rc != _lib.PG_ERR_UNSUPPORTED:
             check(rc, "pg_directgcn_dense_f32")
+            _ev_end(Z, ev, "DENSE")
             del keep, raw
             return Y
     packed = pack_weights(prm, W_res, b_res)
+    ev = _ev_start(Z, "DENSE")
     check(lib.pg_directgcn_dense_f32(ctypes.byref(a), _p(packed), fl, _stream(Z)), "pg_directgcn_dense_f32")
+    _ev_end(Z, ev, "DENSE")
     del keep
     return Y
 
@@ -534,12 +572,14 @@ def layer_dense_ngram_rows(Z, prm: dict, gate_mode: int, Kn1: int, m0: int, cons
     (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
      a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared) = [_p(t) for t in raw]
     fl = default_flags() if flags is None else flags
+    ev = _ev_start(Z, "DENSE")
     rc = lib.pg_directgcn_dense_ngram_rows_f32(ctypes.byref(a), None, int(Kn1), int(m0), int(bool(map_res)),
                                                int(bool(map_out)), fl, _stream(Z))
     del keep, raw
     if rc == _lib.PG_ERR_UNSUPPORTED:
         return None
     check(rc, "pg_directgcn_dense_ngram_rows_f32")
+    _ev_end(Z, ev, "DENSE")
     return Y
 
 
@@ -552,11 +592,13 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
     a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
+    ev = _ev_start(Z, "DENSE")
     rc = lib.pg_directgcn_dense_bf16(ctypes.byref(a), _p(packed), _p(p16), fl, _stream(Z))
     del keep
     if rc == _lib.PG_ERR_UNSUPPORTED:
         return None
     check(rc, "pg_directgcn_dense_bf16")
+    _ev_end(Z, ev, "DENSE")
     return Y
 
 
@@ -629,15 +671,19 @@ def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
     emb = torch.empty(M, F, device=h.device, dtype=torch.float32)
     if _is_bf16(h):
         hb = _bf16c(h.detach())
+        ev = _ev_start(hb, "HEAD")
         rc = lib.pg_directgcn_head_bf16(M, F, H, C, _p(hb), hb.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), float(eps),
                                         _p(logp), logp.stride(0), _p(emb), emb.stride(0), _stream(hb))
         if rc != _lib.PG_ERR_UNSUPPORTED:
             check(rc, "pg_directgcn_head_bf16")
+            _ev_end(hb, ev, "HEAD")
             return logp, emb
     h = _f32c(h.detach())
+    ev = _ev_start(h, "HEAD")
     check(lib.pg_directgcn_head_f32(M, F, H, C, _p(h), h.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), float(eps),
                                     _p(logp), logp.stride(0), _p(emb), emb.stride(0), _stream(h)),
           "pg_directgcn_head_f32")
+    _ev_end(h, ev, "HEAD")
     return logp, emb
 
 

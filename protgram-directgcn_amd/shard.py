@@ -34,6 +34,14 @@ import torch.nn.functional as F
 from . import ops
 from .graph import CSRGraph, take
 
+# Run the node-range partition's collectives (all-gather, reduce-scatter, all-reduce) even at world size 1, where they
+# are identities: lets a one-GPU box execute the RCCL code paths the 8-GPU run takes (tests/test_gpu_rccl.py).
+FORCE_COLLECTIVES = False
+
+
+def _exchanging(world: int) -> bool:
+    return world > 1 or FORCE_COLLECTIVES
+
 
 @dataclass
 class NodeRangePartition:
@@ -180,7 +188,7 @@ def sharded_forward(model, part: NodeRangePartition, x_full: torch.Tensor, group
     if model.compute_dtype == torch.bfloat16:
         h = h.to(torch.bfloat16)
     L = len(model.convs)
-    plan = gather_plan(part, chunks) if (L > 1 and part.world > 1) else None
+    plan = gather_plan(part, chunks) if (L > 1 and _exchanging(part.world)) else None
     h_local = None
     for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
         first = i == 0
@@ -294,7 +302,7 @@ def sharded_forward_train(model, part: NodeRangePartition, x_full: torch.Tensor,
         h_local = _layer_local_train(conv, part, h_full, res, own=None if own is None else own[i])
         h_local = F.dropout(h_local, p=model.dropout, training=model.training)
         if i + 1 < L:
-            h_full = _GatherRows.apply(h_local, part, group) if part.world > 1 else h_local
+            h_full = _GatherRows.apply(h_local, part, group) if _exchanging(part.world) else h_local
     return model.head(h_local)
 
 
@@ -323,7 +331,7 @@ def sharded_train_step(model, part: NodeRangePartition, x_full: torch.Tensor, y_
                 l2 = l2 + p.norm(2).pow(2) / part.world     # replicated: summed over ranks below
         loss = loss + l2_lambda * l2
     loss.backward()
-    if part.world > 1:
+    if _exchanging(part.world):
         dense = [p for name, p in model.named_parameters()
                  if p.grad is not None and not _is_node_param(name, p, part.n)]
         flat = torch.cat([p.grad.reshape(-1) for p in dense])
@@ -335,7 +343,7 @@ def sharded_train_step(model, part: NodeRangePartition, x_full: torch.Tensor, y_
             off += k
     optimizer.step()
     tot = loss.detach().reshape(1).clone()
-    if part.world > 1:
+    if _exchanging(part.world):
         dist.all_reduce(tot, group=group)
     return float(tot)
 
@@ -389,6 +397,13 @@ class ShardedTrainer:
         else:
             self.opt = optimizer_factory(self.params)
         self._train = train
+        # which parameters autograd reached this step (host-side hooks, no sync): with l2_lambda == 0 the others are
+        # not stepped, as torch.optim.Adam skips parameters whose grad is None in the reference loop (the flat
+        # buffer gives every replicated parameter a zero grad view). The replicated parameters' autograd graph is the
+        # same on every rank, so the local record is the global one.
+        self._touched: set = set()
+        for prm in self.params:
+            prm.register_post_accumulate_grad_hook(lambda t: self._touched.add(id(t)))
 
     def _grads_into_flat(self):
         off = 0
@@ -406,17 +421,23 @@ class ShardedTrainer:
         self._grads_into_flat()  # autograd accumulates into the flat buffer's views in place
         lp, _ = sharded_forward_train(self.model, part, x_full, self.group, own=self.own)
         nll = -lp.float().gather(1, y_local.view(-1, 1)).sum() / part.n
+        self._touched = set()
         nll.backward()
-        for p in self.node:  # parameters with no gradient path still get the L2 gradient and are stepped
-            if p.requires_grad and p.grad is None:
-                p.grad = torch.zeros_like(p)
+        if lam:  # parameters with no gradient path still get the L2 gradient and are stepped
+            for p in self.node:
+                if p.requires_grad and p.grad is None:
+                    p.grad = torch.zeros_like(p)
+        else:  # no L2 term: only the parameters autograd reached are stepped (torch Adam skips grad None)
+            for p in self.params:
+                if id(p) not in self._touched:
+                    p.grad = None
         if lam:
             l2_rep = train.l2_sqsum(self.dense) if self.dense else nll.new_zeros(())
             l2_own = train.l2_sqsum(self.node) if self.node else nll.new_zeros(())
         else:
             l2_rep = l2_own = nll.new_zeros(())
         parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
-        if part.world > 1:
+        if _exchanging(part.world):
             if self.flat.numel():
                 dist.all_reduce(self.flat, group=self.group)  # sum of the ranks' partial gradients
             dist.all_reduce(parts, group=self.group)
@@ -444,7 +465,7 @@ def gather_node_params(model, part: NodeRangePartition, group=None):
     """Make every rank's per-node parameters (C_*_vec, constant) whole again by all-gathering the owned
     rows (for checkpointing / switching back to single-GPU inference)."""
     for name, p in model.named_parameters():
-        if _is_node_param(name, p, part.n) and part.world > 1:
+        if _is_node_param(name, p, part.n) and _exchanging(part.world):
             flat = p.data.reshape(part.n, -1)
             full = all_gather_rows(flat[part.r0:part.r1].contiguous(), part, group)
             flat.copy_(full)
@@ -645,6 +666,7 @@ class MiddlePartition:
     chunk_send: List[List[int]] = field(default_factory=list)  # [chunk][destination] rows sent
     chunk_recv: List[List[int]] = field(default_factory=list)  # [chunk][source] rows received
     cache: dict = field(default_factory=dict)
+    loopback: bool = False      # world 1: every owned row is "sent" to this rank itself (exchange test mode)
 
     @property
     def n_own(self) -> int:
@@ -691,12 +713,16 @@ def _middle_reads(K: int, n: int, m0: int, m1: int, dev) -> torch.Tensor:
     return torch.unique(torch.cat([out_src, in_src, _middle_rows(K, n, m0, m1, dev)]))
 
 
-def middle_partition(g: CSRGraph, rank: int, world: int, chunks: int = 1) -> MiddlePartition:
+def middle_partition(g: CSRGraph, rank: int, world: int, chunks: int = 1, loopback: bool = False) -> MiddlePartition:
     """This rank's middle partition of a complete n-gram graph (see the section comment). Setup work, once per
     graph: the exchange lists of every rank pair are built from the closed-form read sets (and checked against
     the CSR's own columns), so both ends of each pair agree without communication. With chunks > 1 every rank's
     middles are cut into `chunks` sub-ranges and the lists are grouped by the sender's sub-range, so each sub-range's
-    rows can be exchanged as soon as they are computed (MiddleRunner overlaps that exchange with the next one)."""
+    rows can be exchanged as soon as they are computed (MiddleRunner overlaps that exchange with the next one).
+    loopback (world 1 only): the lists send every owned row of each sub-range to this rank itself, so a one-GPU run
+    executes the exchange path (gather, asynchronous all_to_all_single, scatter) with an identity exchange."""
+    if loopback and world != 1:
+        raise ValueError("loopback is a world-size-1 test mode")
     shape = ngram_shape(g)
     if shape is None or not g.shared:
         raise NotImplementedError("middle partition needs a shared-pattern graph over all K^n n-grams")
@@ -755,6 +781,14 @@ def middle_partition(g: CSRGraph, rank: int, world: int, chunks: int = 1) -> Mid
         recv_ids = empty
     L = m1 - m0
     chunk_bounds = [(m0 + cc * L // chunks, m0 + (cc + 1) * L // chunks) for cc in range(chunks)]
+    if loopback:  # each sub-range's own rows to itself, in owned-row order (positions = ids' order in `own`)
+        K2 = K * K
+        pos_c = [torch.arange((a - m0) * K2, (b - m0) * K2, dtype=torch.int64, device=dev) for a, b in chunk_bounds]
+        send_pos = torch.cat(pos_c)
+        recv_ids = _middle_rows(K, n, m0, m1, dev)[send_pos]
+        chunk_send = [[int(pc.numel())] for pc in pos_c]
+        chunk_recv = [[int(pc.numel())] for pc in pos_c]
+        send_counts = recv_counts = [int(send_pos.numel())]
     # the owned rows' CSR (global column ids), and the check that it reads nothing outside the closed-form set
     rp = g.rowptr
     cnt = rp[own + 1] - rp[own]
@@ -770,7 +804,7 @@ def middle_partition(g: CSRGraph, rank: int, world: int, chunks: int = 1) -> Mid
     own_csr = CSRGraph(n_rows=own.numel(), shared=True, rowptr=lrp, edges3=e, symmetric=False, nnz=tot,
                        row_order=None, n_cols=g.n_rows)
     return MiddlePartition(rank, world, g.n_rows, K, n, m0, m1, own, own_csr, send_pos, send_counts, recv_ids,
-                           recv_counts, g, chunks, chunk_bounds, chunk_send, chunk_recv)
+                           recv_counts, g, chunks, chunk_bounds, chunk_send, chunk_recv, loopback=loopback)
 
 
 @torch.no_grad()
@@ -812,15 +846,22 @@ def _exchange_rows(mp: MiddlePartition, h_own: torch.Tensor, group=None) -> torc
     reads stay unwritten. (MiddleRunner does the same per chunk, overlapped.)"""
     F_ = h_own.size(1)
     X = h_own.new_empty(mp.n, F_)
-    ops.rows_scatter(h_own, mp.own, X)
-    if mp.world > 1:
-        send = ops.rows_gather(h_own, mp.send_pos)
+    ops.rows_scatter(h_own, mp.own, X, check_idx=False)
+    if mp.world > 1 or mp.loopback:
+        send = ops.rows_gather(h_own, mp.send_pos, check_idx=False)
         stage = h_own.is_cuda and dist.get_backend(group) == "gloo"  # gloo (CPU rehearsal backend): host buffers
         if stage:
             send = send.cpu()
         recv = send.new_empty(int(mp.recv_ids.numel()), F_)
-        dist.all_to_all_single(recv, send, mp.recv_counts, mp.send_counts, group=group)
-        ops.rows_scatter(recv.to(X.device) if stage else recv, mp.recv_ids, X)
+        # send_pos / recv_ids are grouped by (chunk, rank): one all_to_all per chunk, whose slices are rank-grouped
+        # (a single call over all chunks would need the buffers grouped by rank alone)
+        s0 = r0 = 0
+        for c in range(mp.chunks):
+            ns, nr = sum(mp.chunk_send[c]), sum(mp.chunk_recv[c])
+            dist.all_to_all_single(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_recv[c], mp.chunk_send[c],
+                                   group=group)
+            s0, r0 = s0 + ns, r0 + nr
+        ops.rows_scatter(recv.to(X.device) if stage else recv, mp.recv_ids, X, check_idx=False)
     return X
 
 
@@ -834,7 +875,7 @@ def middle_forward(model, mp: MiddlePartition, x_full: torch.Tensor, inputs=None
     h = model._apply_pe(x_full)
     if model.compute_dtype == torch.bfloat16:
         h = h.to(torch.bfloat16)
-    X, res_x = h, ops.rows_gather(h, mp.own)
+    X, res_x = h, ops.rows_gather(h, mp.own, check_idx=False)
     L = len(model.convs)
     for i, (conv, res, (prm, const)) in enumerate(zip(model.convs, model.res_projs, layers)):
         gate_mode = 0 if conv.use_vector_coeffs else 1
@@ -897,8 +938,9 @@ class MiddleRunner:
                        and all(cv.in_channels == 128 and cv.out_channels == 128 for cv in model.convs)
                        and not any(isinstance(r, nn.Linear) for r in model.res_projs))
         self.Kn1 = mp.K ** (mp.ngram - 1)
-        self.send_glob = mp.own[mp.send_pos] if mp.world > 1 else None  # the sent rows' global ids
-        backend = dist.get_backend(group) if (mp.world > 1 and dist.is_initialized()) else None
+        self.xchg = mp.world > 1 or mp.loopback
+        self.send_glob = mp.own[mp.send_pos] if self.xchg else None  # the sent rows' global ids
+        backend = dist.get_backend(group) if (self.xchg and dist.is_initialized()) else None
         self.sync = (not x_full.is_cuda) or backend == "gloo"
         self.state = {}
         self.works = []
@@ -924,20 +966,20 @@ class MiddleRunner:
             if self.replicate and self.L > 1:
                 self.state["res"] = h
             else:  # mapped: the dense kernel reads the residual rows from h itself
-                self.state["res"] = None if self.mapped else ops.rows_gather(h, mp.own)
+                self.state["res"] = None if self.mapped else ops.rows_gather(h, mp.own, check_idx=False)
         elif self.replicate:
             X = self.bufs[i - 1]  # the replicated layer's output, every row
             self.state["X"] = X
             if i + 1 < self.L:
                 self.state["res"] = X
             else:
-                self.state["res"] = None if self.mapped else ops.rows_gather(X, mp.own)
+                self.state["res"] = None if self.mapped else ops.rows_gather(X, mp.own, check_idx=False)
         else:
             X, h_prev = self.bufs[i - 1], self.hout[i - 1]
             if not self.mapped:  # mapped: layer i - 1's dense kernel wrote the own rows into X
-                ops.rows_scatter(h_prev, mp.own, X)
-            if mp.world > 1 and self.recv[i - 1].size(0):
-                ops.rows_scatter(self.recv[i - 1], mp.recv_ids, X)
+                ops.rows_scatter(h_prev, mp.own, X, check_idx=False)
+            if self.xchg and self.recv[i - 1].size(0):
+                ops.rows_scatter(self.recv[i - 1], mp.recv_ids, X, check_idx=False)
             self.state["X"], self.state["res"] = X, None if self.mapped else h_prev
 
     def _compute_full(self, i: int):
@@ -991,19 +1033,21 @@ class MiddleRunner:
             return None
         h = self._compute(i, c)
         if i + 1 < self.L:
-            if self.mp.world > 1:
+            if self.xchg:
                 s0, s1 = self.send_slices[c]
                 if self.mapped:
-                    self.state[("send", i, c)] = ops.rows_gather(self.bufs[i], self.send_glob[s0:s1])
+                    self.state[("send", i, c)] = ops.rows_gather(self.bufs[i], self.send_glob[s0:s1],
+                                                                 check_idx=False)
                 else:
-                    self.state[("send", i, c)] = ops.rows_gather(self.hout[i], self.mp.send_pos[s0:s1])
+                    self.state[("send", i, c)] = ops.rows_gather(self.hout[i], self.mp.send_pos[s0:s1],
+                                                                 check_idx=False)
             return None
         return self.model.head(h)
 
     # ---- exchange (outside the graphs)
     def _exchange(self, i: int, c: int):
         mp = self.mp
-        if mp.world == 1:
+        if not self.xchg:
             return
         send = self.state[("send", i, c)]
         r0, r1 = self.recv_slices[c]

@@ -33,8 +33,20 @@ def test_bench_json_line_is_self_consistent():
     assert abs(rf["achieved"] - achieved) <= 1e-3 * achieved + 0.1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) <= 1e-3
     assert 0.0 < rf["frac"] < 1.0  # compulsory bytes: physically below peak
-    # the propagation is one of the step's kernels: its launches take less than the whole step
+    # the dominant kernel is one of the step's kernels: its launches take less than the whole step
     assert rf["avg_launch_ms"] < out["ms_per_step"]
+    # one entry per hot-path kernel, each self-consistent; the dominant one has the largest measured time per step,
+    # and together they fit inside the step
+    ks = rf["kernels"]
+    assert set(ks) == {"propagation", "dense", "head"}
+    for k, e in ks.items():
+        a = e["algorithmic_bytes_per_launch"] / (e["avg_launch_ms"] * 1e-3) / 1e9
+        assert abs(e["achieved"] - a) <= 1e-3 * a + 0.1, k
+        assert 0.0 < e["frac"] < 1.0 and e["launches_timed"] >= e["launches_per_step"], k
+    assert rf["kernel"] == max(ks.values(), key=lambda e: e["ms_per_step"])["kernel"]
+    assert sum(e["ms_per_step"] for e in ks.values()) <= out["ms_per_step"] * 1.05
+    assert ks["propagation"]["algorithmic_bytes_per_launch"] == 411_520_000  # SURVEY 8(d) / DESIGN §4 at B(20,4)
+    assert abs(ks["dense"]["algorithmic_bytes_per_launch"] - 494.7e6) < 0.5e6
 
 
 @pytest.mark.timeout(300)

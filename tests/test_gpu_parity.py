@@ -1154,6 +1154,15 @@ def test_rows_gather_scatter(pkg, cuda, dtype, F):
     ref[idx] = src[idx]
     assert torch.equal(dst, ref)
     assert ops.rows_gather(src, idx[:0]).shape == (0, F)
+    # the public calls validate their indices: out of range / repeated scatter rows raise on the host
+    with pytest.raises(IndexError):
+        ops.rows_gather(src, torch.tensor([0, 5000], device=cuda))
+    with pytest.raises(IndexError):
+        ops.rows_gather(src, torch.tensor([-1], device=cuda))
+    with pytest.raises(IndexError):
+        ops.rows_scatter(got[:2], torch.tensor([0, 5000], device=cuda), dst)
+    with pytest.raises(ValueError):
+        ops.rows_scatter(got[:2], torch.tensor([7, 7], device=cuda), dst)
 
 
 @pytest.mark.gpu

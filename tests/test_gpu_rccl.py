@@ -1,0 +1,140 @@
+"""Every RCCL-only line of shard.py executed once on a one-GPU box: a child process runs
+init_process_group("nccl") at world size 1 and drives
+
+  * MiddleRunner on a loopback middle partition (each middle sub-range's rows "sent" to the rank itself): the
+    asynchronous all_to_all_single on RCCL's stream, interleaved with HIP-graph capture and replay of the compute
+    segments -- bit-identical to the eager runner and to the single-GPU forward;
+  * the node-range partition with shard.FORCE_COLLECTIVES: RCCL all_gather_into_tensor (chunked, async) in
+    sharded_forward, the all-gather / reduce_scatter_tensor pair of sharded training and ShardedTrainer's flat
+    all_reduce -- bit-identical to the same steps with the collectives skipped (at world 1 they are identities).
+
+The 8-GPU run then is not the first execution of this code."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model(pkg, N, dims, dev, n):
+    torch.manual_seed(0)
+    model = pkg.ProtGramDirectGCN(dims, N, 20, n, 0, 512, 0.5, True)
+    with torch.no_grad():
+        gen = torch.Generator().manual_seed(5)
+        for name, p in model.named_parameters():
+            leaf = name.split(".")[-1]
+            if leaf.startswith("C_"):
+                p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+            elif "bias" in leaf:
+                p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+    return model.to(dev).eval()
+
+
+def _worker(port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.path[:0] = [REPO, HERE]
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import shard
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    bad = []
+    try:
+        assert dist.get_backend() == "nccl"
+        N, s, d, c = pkg.synth.de_bruijn_edges(3)
+        g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+        x = torch.randn(N, 128, generator=torch.Generator().manual_seed(1234)).to(dev)
+        # ---- middle partition, loopback exchange: fp32 (mapped dense launches) and bf16 (gathered rows)
+        for dt in (torch.float32, torch.bfloat16):
+            model = _model(pkg, N, [128, 128, 128], dev, 3)
+            model.compute_dtype = dt
+            xin = x.to(dt)
+            with torch.no_grad():
+                lp_r, emb_r = model(pkg.Data(x=xin, graph=g))
+            mpart = shard.middle_partition(g, 0, 1, chunks=2, loopback=True)
+            run_g = shard.MiddleRunner(model, mpart, xin, graphs=True)
+            if run_g.graphs is None or run_g.sync:
+                bad.append((str(dt), "capture failed or synchronous exchange", run_g.sync))
+            lp1, emb1 = (t.clone() for t in run_g())
+            lp2, emb2 = run_g()  # a second replay: same values
+            run_e = shard.MiddleRunner(model, mpart, xin, graphs=False)
+            lp3, emb3 = run_e()
+            torch.cuda.synchronize()
+            rows = mpart.global_rows
+            # the all_to_all delivered the rows: the receive buffer holds exactly the sent (own) rows
+            got = run_g.recv[0].float()
+            want = run_g.bufs[0][mpart.recv_ids].float()
+            if got.shape[0] != mpart.n_own or not torch.equal(got, want):
+                bad.append((str(dt), "loopback receive buffer"))
+            for name, a, b in (("replay", lp1, lp2), ("eager", lp1, lp3), ("eager emb", emb1, emb3)):
+                if not torch.equal(a, b):
+                    bad.append((str(dt), name, float((a - b).abs().max())))
+            if dt == torch.float32:  # bit-identical to the single-GPU forward (same kernels, same per-row sums)
+                if not (torch.equal(lp1, lp_r[rows]) and torch.equal(emb1, emb_r[rows])):
+                    bad.append(("fp32 vs single GPU", float((lp1 - lp_r[rows]).abs().max())))
+            else:  # bf16: the middle partition's dense launches run on row subsets (within bf16 rounding)
+                if not torch.allclose(lp1, lp_r[rows], rtol=0.05, atol=0.05):
+                    bad.append(("bf16 vs single GPU", float((lp1 - lp_r[rows]).abs().max())))
+        # ---- node-range partition: RCCL all-gather (chunked, async) in the forward
+        model = _model(pkg, N, [128, 128, 128], dev, 3)
+        part = shard.partition(g, 0, 1, transpose=True)
+        with torch.no_grad():
+            shard.FORCE_COLLECTIVES = False
+            ref = shard.sharded_forward(model, part, x, chunks=2)
+            shard.FORCE_COLLECTIVES = True
+            got = shard.sharded_forward(model, part, x, chunks=2)
+        torch.cuda.synchronize()
+        for a, b in zip(got, ref):
+            if not torch.equal(a, b):
+                bad.append(("sharded_forward", float((a - b).abs().max())))
+        # ---- ShardedTrainer: all-gather / reduce_scatter_tensor autograd pair + flat all_reduce (fp32 and bf16)
+        y = (torch.arange(N, device=dev) // 400) % 20
+        for dt in (torch.float32, torch.bfloat16):
+            res = {}
+            for force in (False, True):
+                shard.FORCE_COLLECTIVES = force
+                m = _model(pkg, N, [128, 128, 128], dev, 3)
+                m.compute_dtype = dt  # eval mode: no dropout masks (the two runs draw the same values)
+                tr = shard.ShardedTrainer(m, part, lr=1e-3, l2_lambda=1e-3)
+                losses = [tr.step(x, y).clone() for _ in range(2)]
+                tr.gather()
+                res[force] = (torch.stack(losses), {k: v.detach().clone() for k, v in m.state_dict().items()})
+            torch.cuda.synchronize()
+            if not torch.equal(res[False][0], res[True][0]):
+                bad.append((str(dt), "trainer loss", res[False][0].tolist(), res[True][0].tolist()))
+            for k, v in res[False][1].items():
+                if not torch.equal(v, res[True][1][k]):
+                    bad.append((str(dt), "trainer param", k, float((v - res[True][1][k]).abs().max())))
+        shard.FORCE_COLLECTIVES = False
+        out_q.put((not bad, str(bad[:6])))
+    except Exception as e:  # report, then re-raise for the exit code
+        out_q.put((False, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_rccl_paths_world1(pkg, cuda):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_free_port(), q))
+    p.start()
+    ok, msg = q.get(timeout=220)
+    p.join(timeout=60)
+    assert p.exitcode == 0, msg
+    assert ok, msg

@@ -117,8 +117,8 @@ def _worker(rank, world, port, out_q):
     from test_shard_gloo import _cpu_layer_dense, _cpu_spmm3
     ops.spmm3 = _cpu_spmm3
     ops.layer_dense = _cpu_layer_dense
-    ops.rows_gather = lambda src, idx, out=None: src[idx] if out is None else out.copy_(src[idx])
-    ops.rows_scatter = lambda src, idx, dst: dst.index_copy_(0, idx, src)
+    ops.rows_gather = lambda src, idx, out=None, check_idx=True: src[idx] if out is None else out.copy_(src[idx])
+    ops.rows_scatter = lambda src, idx, dst, check_idx=True: dst.index_copy_(0, idx, src)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         N, m, g = _graph(pkg, 3)
@@ -143,6 +143,10 @@ def _worker(rank, world, port, out_q):
         mpc = shard.middle_partition(g, rank, world, chunks=2)  # layer 1 in two sub-ranges, exchanged per sub-range
         lp3, emb3 = shard.MiddleRunner(model, mpc, x)()
         ok = ok and torch.equal(lp3, lp) and torch.equal(emb3, emb)
+        # middle_forward on the chunked partition: its lists are (chunk, rank)-grouped (at world >= 3
+        # one all_to_all over all chunks sent rows to the wrong ranks)
+        lp5, emb5 = shard.middle_forward(model, mpc, x)
+        ok = ok and torch.equal(lp5, lp) and torch.equal(emb5, emb)
         lp4, emb4 = shard.MiddleRunner(model, mp_, x, replicate=True)()  # layer 1 on every row, no exchange
         ok = ok and torch.allclose(lp4, lp, rtol=1e-5, atol=1e-6) and torch.allclose(emb4, emb, rtol=1e-5, atol=1e-6)
         out_q.put((rank, int(rows.numel()), bool(ok), float((lp - lp_r[rows]).abs().max())))

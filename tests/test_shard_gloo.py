@@ -342,6 +342,53 @@ def _trainer_worker(rank, world, port, out_q, bf16):
         dist.destroy_process_group()
 
 
+def _untouched_worker(rank, world, port, out_q):
+    """ShardedTrainer with l2_lambda = 0 steps only the parameters autograd reached: a positional
+    embedding that the forward does not apply (x width != n * one_gram_dim) keeps its value and gets no Adam state,
+    as torch.optim.Adam skips grad None in the reference loop; with l2_lambda > 0 its L2 gradient steps it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard, train
+    from oracle import graph_cpu as og
+    ops.spmm3 = _cpu_spmm3
+    ops.spmm3_t = _cpu_spmm3_t
+    ops.layer_dense = _cpu_layer_dense
+    ops.layer_dense_backward = _cpu_layer_dense_backward
+    train.l2_sqsum = lambda ps: sum((p.detach().float() ** 2).sum() for p in ps)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, s, d, c = pkg.synth.de_bruijn_edges(2)
+        m = og.build_matrices(N, s, d, c)
+        g = pkg.graph.csr_from_coo(N, *m["in"], *m["out"], *m["und"], cache=False)
+        x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
+        y = (torch.arange(N) // 20) % 5
+        part = shard.partition(g, rank, world, transpose=True)
+        res = []
+        for lam in (0.0, 1e-3):
+            torch.manual_seed(0)
+            model = pkg.ProtGramDirectGCN([16, 16, 12], N, 5, 2, 3, 4, 0.5, True).eval()  # PE 2 x 3 != 16: unused
+            pe0 = model.pe_layer.weight.detach().clone()
+            w0 = model.convs[0].lin_shared.weight.detach().clone()
+            tr = shard.ShardedTrainer(model, part, l2_lambda=lam,
+                                      optimizer_factory=lambda ps: torch.optim.Adam(ps, lr=1e-2))
+            for _ in range(2):
+                tr.step(x, y[part.r0:part.r1])
+            pe_moved = not torch.equal(model.pe_layer.weight.detach(), pe0)
+            res.append((lam, pe_moved, len(tr.opt.state.get(model.pe_layer.weight, {})) > 0,
+                        not torch.equal(model.convs[0].lin_shared.weight.detach(), w0)))
+        ok = res[0][1:] == (False, False, True) and res[1][1:] == (True, True, True)
+        out_q.put((rank, ok, str(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_trainer_skips_untouched_without_l2():
+    for r in _run(_untouched_worker, 2):
+        assert r[1], f"rank {r[0]}: {r[2]}"
+
+
 def _run(target, world, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

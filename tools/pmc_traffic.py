@@ -55,11 +55,25 @@ def reduce(fetch_dir, write_dir, prefer=("ngram", "spmm")):
            "kernels": kernels}
     ranked = sorted((k for k in kernels if k in dur), key=lambda k: -dur[k][0])
     pref = [k for k in ranked if any(t in k for t in prefer)]
-    ranked = pref or ranked
-    if ranked:
-        res["kernel"] = ranked[0]
-        res["kernel_bytes_per_launch"] = kernels[ranked[0]]["bytes_per_launch"]
+    if pref or ranked:
+        res["kernel"] = (pref or ranked)[0]
+        res["kernel_bytes_per_launch"] = kernels[res["kernel"]]["bytes_per_launch"]
+    # per class of hot-path kernel (bench.py's roofline entries): the kernel of that class with the largest total
+    # duration in the pass
+    res["by_class"] = {}
+    for cls, tags in CLASSES.items():
+        hits = [k for k in ranked if any(t in k for t in tags)]
+        if hits:
+            res["by_class"][cls] = {"kernel": hits[0], "bytes_per_launch": kernels[hits[0]]["bytes_per_launch"],
+                                    "avg_ns_under_pmc": kernels[hits[0]]["avg_ns_under_pmc"]}
     return res
+
+
+# kernel-name tags of the hot-path kernel classes (the HIP kernels' symbol names)
+CLASSES = {"propagation": ("ngram_mid_kernel", "ngram_spmm3_kernel", "spmm_win_kernel", "spmm_vec_kernel",
+                           "spmm_scalar_kernel", "spmm_bf16_kernel"),
+           "dense": ("dense_",),
+           "head": ("head_",)}
 
 
 def main():

@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--clock-warmup-s", type=float, default=1.0,
                     help="untimed seconds of steps before the warm-up steps (clock ramp)")
     ap.add_argument("--ngram", type=int, default=4)
+    ap.add_argument("--graph", choices=("debruijn", "fasta"), default="debruijn",
+                    help="debruijn (default): the complete n-gram graph B(20,n); fasta: a builder-produced level "
+                    "(ngram.ngram_transitions on seeded protein-like sequences with the builder's ' ' padding and "
+                    "rare X/U/B/Z, sorted-string node ids: not the complete grid) on the mapped middle-tile plan")
+    ap.add_argument("--fasta-seqs", type=int, default=8000, help="--graph fasta: sequences (mean length 350)")
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--fused-norm", action="store_true", help="compute edge weights inside the SpMM")
@@ -154,13 +159,13 @@ def main():
             print(*a, file=sys.stderr, flush=True)
 
     n, Fd, L = args.ngram, args.feat, args.layers
-    sizes = pkg.synth.de_bruijn_sizes(n)
-    N = sizes["N"]
     t0 = time.time()
-    s, d, c = pkg.synth.de_bruijn_edges(n)[1:]
-    g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm or args.extra)
+    wl = build_workload(pkg, args, dev, keep_raw=args.fused_norm or args.extra)
+    N, g, tr = wl["N"], wl["graph"], wl["transitions"]
     torch.cuda.synchronize()
-    log(f"[bench] graph B(20,{n}): N={N} E={s.size} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s")
+    log(f"[bench] graph {wl['desc']}: N={N} E={wl['E']} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s"
+        + (f"; mapped plan: {g.ngram_map.n_grid} grid nodes, {g.ngram_map.rows_off.numel()} off-grid rows, "
+           f"{g.ngram_map.nnz_res} residual entries" if g.ngram_map is not None else ""))
 
     model = bench_model(pkg, N, Fd, L, n).to(dev).eval()
     dims = [Fd] * (L + 1)
@@ -180,8 +185,11 @@ def main():
         del g
         with torch.no_grad():
             g = model.graph_of(data)
+            if tr is not None:  # a builder-produced level: the trainer hands its node map over once
+                pkg.attach_ngram_map(g, tr)
         torch.cuda.synchronize()
-        log(f"[bench] entry coo: csr_from_coo -> plan {'attached' if g.ngram is not None else 'NOT attached'}")
+        log(f"[bench] entry coo: csr_from_coo -> plan "
+            + ("attached" if g.ngram is not None else "mapped" if g.ngram_map is not None else "NOT attached"))
     else:
         data = pkg.Data(x=x, graph=g)
 
@@ -295,7 +303,12 @@ def main():
         launch_graphs = [part.local]
     ngram = (all(gi.ngram is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm
              and Fd in (64, 128, 256))
-    if args.bf16:
+    mapped = (all(gi.ngram_map is not None for gi in launch_graphs) and not args.bf16 and not args.fused_norm
+              and Fd % 16 == 0)
+    if mapped:  # builder-produced graph: mapped middle-tile kernel + the residual CSR pass (one propagation)
+        gated = False
+        kname = "pg_spmm3_ngram_mid_map_f32 + pg_spmm3_rows_f32"
+    elif args.bf16:
         kname = ("pg_spmm3_ngram_mid_bf16" if all(gi.ngram is not None and gi.ngram.mplan is not None
                                                   for gi in launch_graphs) and Fd % 16 == 0 else "pg_spmm3_bf16")
     elif args.fused_norm:
@@ -410,8 +423,8 @@ def main():
             "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.bf16 else "f32", "data": "synthetic",
-            "config": {"workload": f"directgcn_fwd_B(20,{n})", "graph": f"complete n-gram de Bruijn B(20,{n})",
-                       "num_nodes": N, "transitions": int(s.size), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
+            "config": {"workload": wl["workload"], "graph": wl["desc"],
+                       "num_nodes": N, "transitions": int(wl["E"]), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,
                        "layers": L, "layer_dims": dims, "classes": C,
                        "propagation": "fused-norm" if args.fused_norm else "precomputed-weights",
                        "entry": ("trainer COO (edge_index_*/edge_weight_* -> csr_from_coo)" if entry == "coo"
@@ -434,6 +447,28 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def build_workload(pkg, args, dev, keep_raw=False):
+    """The bench graph: the complete B(20, n) (--graph debruijn) or a builder-produced level (--graph fasta:
+    ngram.ngram_transitions over synth.protein_sequences(args.fasta_seqs, 350, seed=1) -- the padding ' ' of
+    data_builder.py:29-35, rare X/U/B/Z, sorted-string ids -- with the mapped middle-tile plan attached).
+    Shared with tools/kprobe.py (the PMC passes run the same workload)."""
+    n = args.ngram
+    if getattr(args, "graph", "debruijn") == "debruijn":
+        N, s, d, c = pkg.synth.de_bruijn_edges(n)
+        g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=keep_raw)
+        return {"N": N, "E": int(s.size), "graph": g, "transitions": None,
+                "desc": f"complete n-gram de Bruijn B(20,{n})", "workload": f"directgcn_fwd_B(20,{n})"}
+    seqs = pkg.synth.protein_sequences(args.fasta_seqs, 350, seed=1)
+    tr = pkg.ngram.ngram_transitions(seqs, n, device=dev)
+    g = pkg.build_propagation_csr(tr.num_nodes, tr.src.cpu().numpy(), tr.dst.cpu().numpy(), tr.cnt.cpu().numpy(),
+                                  device=dev, keep_raw=keep_raw, transitions=tr)
+    res = sum(len(q) for q in seqs)
+    return {"N": tr.num_nodes, "E": int(tr.src.numel()), "graph": g, "transitions": tr,
+            "desc": (f"builder-produced {n}-gram level: {args.fasta_seqs} padded protein-like sequences ({res} "
+                     f"residues, Swiss-Prot composition, 0.1% X/U/B/Z), sorted-string ids"),
+            "workload": f"directgcn_fwd_fasta{n}"}
 
 
 class GraphStep:
@@ -489,7 +524,8 @@ def pmc_traffic(args, log, timeout=240):
     import pmc_traffic as pt
     out = tempfile.mkdtemp(prefix="pg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     child = [sys.executable, os.path.join(REPO, "tools", "kprobe.py"), "--forward", "3", "--ngram", str(args.ngram),
-             "--feat", str(args.feat), "--layers", str(args.layers), "--entry", args.entry] \
+             "--feat", str(args.feat), "--layers", str(args.layers), "--entry", args.entry,
+             "--graph", args.graph, "--fasta-seqs", str(args.fasta_seqs)] \
         + (["--bf16"] if args.bf16 else []) \
         + (["--fused-norm"] if args.fused_norm else [])
     env = dict(os.environ)

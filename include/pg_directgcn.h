@@ -268,6 +268,28 @@ int pg_spmm3_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, con
 int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* X, int64_t ldx,
                                  int64_t F, int64_t m_begin, int64_t m_end, uint16_t* Z, int64_t ldz, uint32_t flags,
                                  void* stream);
+/* Builder-produced graphs (run_graph_builder.py -> data_builder.py:29-35, 164-173): node ids are the sorted-string
+ * ranks of the n-grams PRESENT, over an alphabet that includes the padding ' ' (and rare letters), so N != 20^n and
+ * the grid arithmetic of the kernels above does not hold for node ids. The MAPPED form runs the same middle-tile
+ * kernel on the K = 20 grid of the standard letters with a row map:
+ *   ginv [n_nodes] int32: grid row (base-20 n-gram) of node i, -1 when the n-gram has a non-standard character;
+ *   gmap [K^n] int32:     node row of grid row g, -1 when that n-gram is not a node.
+ * pg_ngram_mplan_map_f32: the middle plan of the grid part (zeroed first); resid[e] (uint8, one per CSR entry) = 1
+ *   for every entry that does not go to a grid slot (an end off the grid, or no out / in / diagonal slot), else 0.
+ * pg_spmm3_ngram_mid_map_f32: Z = the grid part of [A_in X | A_out X | A_und X] at the node rows (X read at node
+ *   rows gmap[.]; rows of nodes off the grid are NOT written). Same requirements and numerics as
+ *   pg_spmm3_ngram_mid_f32; grid K^n < 2^31.
+ * pg_spmm3_rows_f32: pg_spmm3_f32 over the rows rows[0 .. n_list) only (any CSR with n_rows + 1 rowptr entries), each
+ *   Z row overwritten (accumulate = 0) or added to (accumulate != 0): the residual entries (resid = 1) as their own
+ *   CSR, overwriting the off-grid rows and accumulating into grid rows with residual entries. Bit-exact order per
+ *   row as pg_spmm3_f32. */
+int pg_ngram_mplan_map_f32(int K, int n, int64_t n_nodes, const int64_t* rowptr, const pg_edge3_t* edges,
+                           const int32_t* ginv, float* plan, int64_t plan_floats, uint8_t* resid, void* stream);
+int pg_spmm3_ngram_mid_map_f32(int K, int n, const float* plan, const int32_t* gmap, const float* X, int64_t ldx,
+                               int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream);
+int pg_spmm3_rows_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
+                      const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, int accumulate, uint32_t flags,
+                      void* stream);
 /* Transposed middle-tile kernel: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k;
  * the backward of the six propagates, protgram_directgcn.py:101-112, replacing pg_spmm3t_ngram_f32 / pg_spmm3t_f32
  * on graphs over all K^n n-grams). Same middle plan, stream and loader as the forward; per chunk three sub-chunks

@@ -8,5 +8,6 @@ ctypes); there is no CPU fallback -- without the library the layer raises.
 from . import cluster, ngram, synth, train  # noqa: F401
 from ._lib import load_library, library_path, NativeLibraryError  # noqa: F401
 from .data import Data  # noqa: F401
-from .graph import CSRGraph, ShapedAdjacency, build_propagation_csr, csr_from_coo  # noqa: F401
+from .graph import (CSRGraph, ShapedAdjacency, attach_ngram_map, build_ngram_map, build_propagation_csr,  # noqa: F401
+                    csr_from_coo)
 from .layer import DirectGCNLayer, ProtGramDirectGCN  # noqa: F401

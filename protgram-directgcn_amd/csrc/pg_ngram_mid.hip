@@ -73,10 +73,12 @@ struct ML {
     static constexpr int LPART = LSELF + OUTB;                      // partial     [a][row k K + b (3K)][16 f] fp32
     static constexpr int LDIAG = LPART + XK * 3 * XK * 64;          // diagonal weights [a][b][k]
     static constexpr int LBYTES = LDIAG + XR * 3 * 4;               // 160,448 B fp32; 122,560 B bf16
+    static constexpr int LMAP = LBYTES;                             // mapped kernel: node rows of a middle's 400
+    static constexpr int LBYTES_MAP = LMAP + 2 * XR * 4;            //   self rows, double-buffered by middle parity
     static constexpr int NOI = OUTB / 1024, NII = LINB / 1024;      // wave-instructions per region
 };
 static_assert(ML<false>::LBYTES == 160448 && ML<false>::OUTB == XR * 64, "fp32 LDS image");
-static_assert(ML<true>::LBYTES <= 163840 && ML<false>::LBYTES <= 163840, "LDS image exceeds 160 KiB");
+static_assert(ML<true>::LBYTES_MAP <= 163840 && ML<false>::LBYTES_MAP <= 163840, "LDS image exceeds 160 KiB");
 static_assert(XTILES % XCW == 0 && XTPW % 2 == 0, "tiles per wave");
 
 struct XP {
@@ -95,6 +97,7 @@ struct XP {
     int remap;
     int early_in;          // loader: out / self DMA of chunk t + 1 waited for at W(t), not S(t) (PG_FLAG_MID_LOADER_SYNC clears)
     int exp;               // diagnostics build only: timing experiments (bit 0: no Z stores, 1: no out/self DMA, 2: no in DMA)
+    const int* gmap;       // mapped kernel: grid row (base-K n-gram) -> node row of X / Z, -1 = n-gram not in the graph
     unsigned long long* stamps;  // diagnostics build only (PG_MID_STAMPS): s_memtime per block, chunk and point
 };
 
@@ -157,7 +160,13 @@ struct Chunk {
     int M, ch, first;  // middle, chunk index, first chunk of this middle in the workgroup's range
 };
 
-template <bool BF>
+// MAP (pg_spmm3_ngram_mid_map_f32: a graph whose nodes are a subset of the K^n grid plus others, e.g. the builder's
+// padded sequences): X rows are read and Z rows written at node rows gmap[grid row] instead of at the grid rows. The
+// loader waves fetch the node rows of a middle's 1,200 source rows one middle ahead (registers); the 400 self-row
+// entries also go to an LDS row map (double-buffered by middle parity) that the store-out reads, and rows whose
+// n-gram is absent (-1) are not stored (their DMA reads row 0: its weights are 0). Z rows of nodes off the grid are
+// left to the caller (the residual CSR pass).
+template <bool BF, bool MAP>
 __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     using C = ML<BF>;
     using ET = std::conditional_t<BF, uint16_t, float>;
@@ -216,8 +225,69 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             const int c = rl / XCB, a = rl - c * XCB;
             off_i[t] = (a >= XK || c >= XK) ? q * EPP : (c * p.Kn1 + a * p.Kn2) * ldx + q * EPP;  // in: c.a.M; pad: row M
         }
+        // MAP: per-lane grid offsets of the pieces' rows (out: M K^2 + go_o, self: 20 M + go_s, in: M + go_i; -1 =
+        // an in-source pad piece) and the node rows of the current middle (cr_*) and of the next one (nr_*)
+        [[maybe_unused]] int go_o[NO], go_s[NO], go_i[NI], cr_o[NO], cr_s[NO], cr_i[NI], nr_o[NO], nr_s[NO], nr_i[NI];
+        [[maybe_unused]] const int qe = (lane & (PPR - 1)) * EPP;
+        if constexpr (MAP) {
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                const int it = lw + t * XLW;
+                int rl = (int)((unsigned)(it * 64 + lane) / PPR);
+                if (rl >= XR) rl = 0;
+                go_o[t] = rl;
+                const int a = rl / XK, b = rl - a * XK;
+                go_s[t] = a * (int)p.Kn1 + b;
+            }
+#pragma unroll
+            for (int t = 0; t < NI; ++t) {
+                const int it = lw + t * XLW;
+                const int rl = (int)((unsigned)(it * 64 + lane) / PPR);
+                const int c = rl / XCB, a = rl - c * XCB;
+                go_i[t] = (a >= XK || c >= XK) ? -1 : c * (int)p.Kn1 + a * (int)p.Kn2;
+            }
+        }
+        auto fetch_map = [&](int M, int (&o)[NO], int (&s_)[NO], int (&i_)[NI]) {
+            const int* gm = p.gmap;
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                o[t] = gm[M * XR + go_o[t]];
+                s_[t] = gm[M * XK + go_s[t]];
+            }
+#pragma unroll
+            for (int t = 0; t < NI; ++t) i_[t] = go_i[t] < 0 ? 0 : gm[M + go_i[t]];
+        };
+        auto put_map = [&](int M) {  // the self pieces' node rows -> the LDS row map of middle M's parity
+            int* mb = reinterpret_cast<int*>(L + C::LMAP + (M & 1) * XR * 4);
+#pragma unroll
+            for (int t = 0; t < NO; ++t) {
+                const int it = lw + t * XLW;
+                const int rl = (int)((unsigned)(it * 64 + lane) / PPR);
+                if (it < C::NOI && rl < XR && (lane & (PPR - 1)) == 0) mb[rl] = cr_s[t];
+            }
+        };
         auto dma_rows = [&](int region, int kind, int M, int ch) {
             const ET* xc = reinterpret_cast<const ET*>(p.X) + ch * XFC;
+            if constexpr (MAP) {
+                (void)M;
+                if (kind == 0) {
+#pragma unroll
+                    for (int t = 0; t < NO; ++t)
+                        if (lw + t * XLW < C::NOI)
+                            glds16(xc + (int64_t)max(cr_o[t], 0) * ldx + qe, L + region + (lw + t * XLW) * 1024);
+                } else if (kind == 1) {
+#pragma unroll
+                    for (int t = 0; t < NI; ++t)
+                        if (lw + t * XLW < C::NII)
+                            glds16(xc + (int64_t)max(cr_i[t], 0) * ldx + qe, L + region + (lw + t * XLW) * 1024);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NO; ++t)
+                        if (lw + t * XLW < C::NOI)
+                            glds16(xc + (int64_t)max(cr_s[t], 0) * ldx + qe, L + region + (lw + t * XLW) * 1024);
+                }
+                return;
+            }
             if (kind == 0) {
                 const ET* base = xc + (int64_t)M * XR * ldx;
 #pragma unroll
@@ -243,14 +313,21 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
                 if (P < XR * 3 / 4) glds16(d + P * 4, L + LDIAG + it * 1024);
             }
         };
+        const int mlast = (int)p.Kn2 - 1;
         if (g0 < g1) {
             const Chunk c0 = chunk_at(g0);
+            if constexpr (MAP) {
+                fetch_map(c0.M, cr_o, cr_s, cr_i);
+                fetch_map(min(c0.M + 1, mlast), nr_o, nr_s, nr_i);  // one middle ahead
+                put_map(c0.M);
+            }
             dma_rows(LOUT, 0, c0.M, c0.ch);
             dma_rows(LIN, 1, c0.M, c0.ch);
             dma_rows(LSELF, 2, c0.M, c0.ch);
             dma_diag(c0.M);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (MAP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         XSTAMP(XSTAMP_LAST, 6);
         asm volatile("s_barrier" ::: "memory");  // S(-1)
         [[maybe_unused]] int ci = 0;  // chunk slot of the diagnostics build's time stamps
@@ -262,10 +339,24 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
             asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done, partial written; out / self / diag free
             XSTAMP(ci, 1);
             if (more && !XEXP(1)) {
+                if constexpr (MAP) {
+                    if (nx.first) {  // the next chunk starts middle nx.M = (this one) + 1: its rows were prefetched
+#pragma unroll
+                        for (int t = 0; t < NO; ++t) {
+                            cr_o[t] = nr_o[t];
+                            cr_s[t] = nr_s[t];
+                        }
+#pragma unroll
+                        for (int t = 0; t < NI; ++t) cr_i[t] = nr_i[t];
+                        put_map(nx.M);  // read by nx's store-out, after S(t + 1)
+                        fetch_map(min(nx.M + 1, mlast), nr_o, nr_s, nr_i);
+                    }
+                }
                 dma_rows(LOUT, 0, nx.M, nx.ch);
                 dma_rows(LSELF, 2, nx.M, nx.ch);
                 if (nx.first) dma_diag(nx.M);
             }
+            if constexpr (MAP) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             // The out / self rows of chunk t + 1 are first read after W(t): with early_in they stay in flight across
             // S(t) and the store-out, and only the in-source pieces issued after S(t) may still be in flight at W(t)
             if (!p.early_in) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -393,7 +484,7 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
         // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
-        ET* zso = reinterpret_cast<ET*>(p.Z) + ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz +
+        ET* zso = reinterpret_cast<ET*>(p.Z) + (MAP ? 0 : ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz) +
                   (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
         auto rd_in = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
@@ -437,7 +528,21 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         for (int j = 0; j < XTPW; j += 2) {
             const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
             const f4_t v1 = *reinterpret_cast<const f4_t*>(L + so_lds + (2 * j + 2) * 3 * XK * 64);
-            if (!XEXP(0)) {
+            if constexpr (MAP) {  // node rows of (a = 2 j + wb [+ 2], b = so_b) from the LDS row map; -1: not stored
+                const int* mb = reinterpret_cast<const int*>(L + C::LMAP + (M & 1) * XR * 4) + wb * XK + so_b;
+                const int r0 = mb[2 * j * XK], r1 = mb[(2 * j + 2) * XK];
+                if constexpr (BF) {
+                    if (r0 >= 0)
+                        *reinterpret_cast<uint2*>(zso + (int64_t)r0 * p.ldz) =
+                            make_uint2(pgbf::pack2(v0[0], v0[1]), pgbf::pack2(v0[2], v0[3]));
+                    if (r1 >= 0)
+                        *reinterpret_cast<uint2*>(zso + (int64_t)r1 * p.ldz) =
+                            make_uint2(pgbf::pack2(v1[0], v1[1]), pgbf::pack2(v1[2], v1[3]));
+                } else {
+                    if (r0 >= 0) *reinterpret_cast<f4_t*>(zso + (int64_t)r0 * p.ldz) = v0;
+                    if (r1 >= 0) *reinterpret_cast<f4_t*>(zso + (int64_t)r1 * p.ldz) = v1;
+                }
+            } else if (!XEXP(0)) {
                 if constexpr (BF) {  // one rounding to bf16 (RNE), 8-B stores
                     *reinterpret_cast<uint2*>(zso + (int64_t)j * zstep) =
                         make_uint2(pgbf::pack2(v0[0], v0[1]), pgbf::pack2(v0[2], v0[3]));
@@ -802,17 +907,71 @@ int grid_cap() {  // one persistent workgroup per CU (device-properties cache: i
     return cus[dev];
 }
 
-template <bool BF>
+template <bool BF, bool MAP>
 int mid_go(unsigned grid, hipStream_t s, const XP& p, const char* name) {
+    constexpr int lds = MAP ? ML<BF>::LBYTES_MAP : ML<BF>::LBYTES;
     static bool attr_set = false;  // the kernel's dynamic LDS exceeds the 64 KiB default (set once; idempotent)
     if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_mid_kernel<BF>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, ML<BF>::LBYTES) != hipSuccess)
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_mid_kernel<BF, MAP>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
             return pg::set_error(PG_ERR_HIP, "%s: cannot raise the LDS limit", name);
         attr_set = true;
     }
-    hipLaunchKernelGGL(ngram_mid_kernel<BF>, dim3(grid), dim3(XTHREADS), ML<BF>::LBYTES, s, p);
+    hipLaunchKernelGGL((ngram_mid_kernel<BF, MAP>), dim3(grid), dim3(XTHREADS), lds, s, p);
     return pg::check_launch(name);
+}
+
+// Plan of a MAPPED graph (pg_ngram_mplan_map_f32): node i sits at grid row ginv[i] (-1: off the grid). Each CSR entry
+// (i <- j) with both ends on the grid goes to its slot as in ngram_mplan_kernel; every other entry -- an end off the
+// grid, or no out / in / diagonal slot -- is marked resid[e] = 1 and left to the residual CSR pass.
+__global__ __launch_bounds__(256) void ngram_mplan_map_kernel(int64_t Kn1, int64_t n_nodes, const int64_t* rowptr,
+                                                              const int4* edges, const int* ginv, float* plan,
+                                                              uint8_t* resid) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= n_nodes) return;
+    const int K = XK;
+    const int64_t i = ginv[v];
+    for (int64_t e = rowptr[v]; e < rowptr[v + 1]; ++e) {
+        const int4 rec = edges[e];
+        const int64_t j = i < 0 ? -1 : ginv[rec.x];
+        if (j < 0) {
+            resid[e] = 1;
+            continue;
+        }
+        const int a = (int)(i / Kn1), b = (int)(i % K);
+        const int64_t M = (i % Kn1) / K, suffix = i % Kn1, prefix = i / K;
+        int type, c;
+        if (j / K == suffix) {
+            type = 0;
+            c = (int)(j % K);
+        } else if (j % Kn1 == prefix) {
+            type = 1;
+            c = (int)(j / Kn1);
+        } else if (j == i) {
+            type = 2;
+            c = 0;
+        } else {
+            resid[e] = 1;
+            continue;
+        }
+        resid[e] = 0;
+        float* W = plan + M * XMB;
+        const float w3[3] = {__int_as_float(rec.y), __int_as_float(rec.z), __int_as_float(rec.w)};
+        for (int k = 0; k < 3; ++k) {
+            int64_t off;
+            if (type == 2) {
+                off = XPD + ((int64_t)(a * K + b) * 3 + k);
+            } else {
+                const int grp = type == 0 ? b : a;
+                const int rr = k * K + (type == 0 ? a : b);
+                const int m = rr >> 4, li = rr & 15;
+                const int s = c >> 2, lk = c & 3;
+                off = (type == 0 ? XPO : XPI) + ((int64_t)((grp * 4 + m) * XS + s) * 64 + lk * 16 + li);
+                if (rr >= 3 * K - 4) W[off + 4] = w3[k];
+            }
+            W[off] = w3[k];
+        }
+    }
 }
 
 }  // namespace
@@ -841,10 +1000,11 @@ int pg_ngram_mplan_f32(int K, int n, int64_t n_rows, const int64_t* rowptr, cons
     return pg::check_launch("pg_ngram_mplan_f32");
 }
 
-// bf: X and Z are bf16 rows (the bf16 kernel); ldx / ldz in elements
+// bf: X and Z are bf16 rows (the bf16 kernel); ldx / ldz in elements; gmap: the mapped kernel (n_rows = the grid's K^n)
 static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const void* X, int64_t ldx, int64_t F,
                       int64_t m_begin, int64_t m_end, bool middle_major, const pg_layer_args_t* gates, void* Z,
-                      int64_t ldz, uint32_t flags, unsigned long long* stamps, bool bf, void* stream) {
+                      int64_t ldz, uint32_t flags, unsigned long long* stamps, bool bf, void* stream,
+                      const int* gmap = nullptr) {
     const char* name = bf ? "pg_spmm3_ngram_mid_bf16" : "pg_spmm3_ngram_mid_f32";
     int64_t Kn1 = 0, Kn2 = 0;
     PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
@@ -864,7 +1024,10 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const voi
         return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned X rows and aligned Z rows", name);
     PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 30), "too many column chunks");
     PG_REQUIRE(!(bf && stamps), "time stamps: fp32 kernel only");
+    PG_REQUIRE(!gmap || (!middle_major && m_begin == 0 && m_end == Kn2 && n_rows < (int64_t(1) << 31) && !stamps),
+               "the mapped kernel covers the whole grid (< 2^31 rows)");
     XP p{};
+    p.gmap = gmap;
     p.Kn1 = Kn1;
     p.Kn2 = Kn2;
     p.m0 = m_begin;
@@ -890,12 +1053,38 @@ static int mid_launch(int K, int n, int64_t n_rows, const float* plan, const voi
     unsigned grid = (unsigned)(total < cap ? total : cap);
     if (p.cstride == 2) grid &= ~1u;
     hipStream_t s = (hipStream_t)stream;
-    return bf ? mid_go<true>(grid, s, p, name) : mid_go<false>(grid, s, p, name);
+    if (gmap) return bf ? mid_go<true, true>(grid, s, p, name) : mid_go<false, true>(grid, s, p, name);
+    return bf ? mid_go<true, false>(grid, s, p, name) : mid_go<false, false>(grid, s, p, name);
 }
 
 int pg_spmm3_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,
                            const pg_layer_args_t* gates, float* Z, int64_t ldz, uint32_t flags, void* stream) {
     return mid_launch(K, n, n_rows, plan, X, ldx, F, 0, -1, false, gates, Z, ldz, flags, nullptr, false, stream);
+}
+
+int pg_ngram_mplan_map_f32(int K, int n, int64_t n_nodes, const int64_t* rowptr, const pg_edge3_t* edges,
+                           const int32_t* ginv, float* plan, int64_t plan_floats, uint8_t* resid, void* stream) {
+    int64_t Kn1 = 0, Kn2 = 0, grid = 1;
+    for (int t = 0; t < n && grid < (int64_t(1) << 40); ++t) grid *= K;
+    PG_REQUIRE(mid_shape(K, n, grid, Kn1, Kn2), "the grid must be K^n with K = %d (K=%d, n=%d)", XK, K, n);
+    PG_REQUIRE(grid < (int64_t(1) << 31), "grid of %lld rows: the mapped kernel takes < 2^31", (long long)grid);
+    PG_REQUIRE(plan_floats >= Kn2 * XMB, "plan buffer too small");
+    PG_REQUIRE(n_nodes >= 0 && (n_nodes == 0 || (rowptr && edges && ginv && plan && resid)), "null pointer");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(plan, 0, sizeof(float) * plan_floats, s) != hipSuccess)
+        return pg::set_error(PG_ERR_HIP, "pg_ngram_mplan_map_f32: memset failed");
+    if (n_nodes == 0) return PG_OK;
+    hipLaunchKernelGGL(ngram_mplan_map_kernel, dim3((unsigned)((n_nodes + 255) / 256)), dim3(256), 0, s, Kn1, n_nodes,
+                       rowptr, reinterpret_cast<const int4*>(edges), ginv, plan, resid);
+    return pg::check_launch("pg_ngram_mplan_map_f32");
+}
+
+int pg_spmm3_ngram_mid_map_f32(int K, int n, const float* plan, const int32_t* gmap, const float* X, int64_t ldx,
+                               int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream) {
+    int64_t grid = 1;
+    for (int t = 0; t < n && grid < (int64_t(1) << 40); ++t) grid *= K;
+    PG_REQUIRE(gmap != nullptr, "null row map");
+    return mid_launch(K, n, grid, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, nullptr, false, stream, gmap);
 }
 
 int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,

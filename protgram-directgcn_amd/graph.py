@@ -58,6 +58,31 @@ class NgramPlan:
     mplan: Optional[torch.Tensor] = None  # fp32 [pg_ngram_mplan_floats(K, n, K^n)]: middle layout (middle-tile forward)
 
 
+# The K = 20 grid of the mapped plan: the standard amino-acid letters (any other character -- the builder's padding
+# ' ', X / U / B / Z / O -- puts an n-gram off the grid).
+GRID_LETTERS = "ACDEFGHIKLMNPQRSTVWY"
+
+
+@dataclass
+class NgramMap:
+    """A builder-produced graph (run_graph_builder.py: node ids = sorted-string ranks of the n-grams PRESENT over an
+    alphabet with the padding ' ', data_builder.py:29-35, 164-173) laid out for the middle-tile kernel on the grid of
+    the K = 20 standard letters (build_ngram_map): the grid part runs pg_spmm3_ngram_mid_map_f32 (X / Z at node rows
+    through gmap), the rest -- rows off the grid and entries with no grid slot -- the residual CSR pass
+    (pg_spmm3_rows_f32: overwrite the off-grid rows, accumulate into the grid rows with residual entries)."""
+    K: int
+    n: int
+    mplan: torch.Tensor      # fp32 [K^(n-2) * 52,400]: middle plan of the grid part
+    gmap: torch.Tensor       # int32 [K^n]: node row of grid row g, -1 = n-gram not a node
+    ginv: torch.Tensor       # int32 [N]: grid row of node i, -1 = off the grid
+    res_rowptr: torch.Tensor  # int64 [N + 1]: residual entries per node row
+    res_edges: torch.Tensor   # int32 [nnz_res, 4]: the residual entries (records as edges3, CSR order kept)
+    rows_off: torch.Tensor    # int32: node rows off the grid (residual pass overwrites)
+    rows_acc: torch.Tensor    # int32: grid node rows holding residual entries (residual pass accumulates)
+    n_grid: int = 0           # nodes on the grid
+    nnz_res: int = 0
+
+
 @dataclass
 class CSRGraph:
     n_rows: int
@@ -75,6 +100,7 @@ class CSRGraph:
     row_order: Optional[torch.Tensor] = None  # int32 processing schedule of destination rows (None = 0..n-1)
     n_cols: Optional[int] = None             # rows of X (= output rows of the transpose); None = n_rows
     ngram: Optional[NgramPlan] = None        # n-gram tile plan (build_ngram_plan), used instead of the CSR kernels
+    ngram_map: Optional[NgramMap] = None     # mapped middle plan of a builder-produced graph (build_ngram_map)
 
     @property
     def device(self):
@@ -98,12 +124,19 @@ class CSRGraph:
         if self.ngram is not None:
             g.ngram = NgramPlan(self.ngram.K, self.ngram.n, self.ngram.plan.to(device),
                                 None if self.ngram.mplan is None else self.ngram.mplan.to(device))
+        if self.ngram_map is not None:
+            m = self.ngram_map
+            g.ngram_map = NgramMap(m.K, m.n, *(mv(t) for t in (m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_edges,
+                                                                 m.rows_off, m.rows_acc)), m.n_grid, m.nnz_res)
         return g
 
     def tensors(self):
         ts = [self.rowptr, self.edges3, self.rowptr_t, self.edges3_t, self.row_order,
               self.ngram.plan if self.ngram is not None else None,
               self.ngram.mplan if self.ngram is not None else None]
+        if self.ngram_map is not None:
+            m = self.ngram_map
+            ts += [m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_edges, m.rows_off, m.rows_acc]
         for a in self.adj:
             ts += [a.rowptr, a.edges, a.rowptr_t, a.edges_t]
         return [t for t in ts if t is not None]
@@ -129,6 +162,11 @@ class CSRGraph:
         g = 20 * n if gated else 0
         if self.ngram is not None and self.ngram.mplan is not None and F % 16 == 0 and elem in (2, 4):
             return 4 * self.ngram.mplan.numel() + nx * F * elem + 3 * n * F * elem + g  # middle-tile kernel: its plan
+        if self.ngram_map is not None and F % 16 == 0 and elem == 4:  # mapped middle-tile kernel + residual CSR pass
+            m = self.ngram_map
+            nr = m.rows_off.numel() + m.rows_acc.numel()  # residual rows: list + rowptr pair + records (+ Z re-read)
+            return (4 * m.mplan.numel() + 4 * m.gmap.numel() + nx * F * elem + 3 * n * F * elem + g
+                    + 20 * nr + 16 * m.nnz_res + 3 * m.rows_acc.numel() * F * elem)
         if self.ngram is not None and F in (64, 128, 256) and elem == 4:  # the n-gram tile kernel reads its plan instead
             return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g
         if self.shared:
@@ -398,14 +436,94 @@ def build_ngram_plan(g: CSRGraph, K: int = 20) -> Optional[NgramPlan]:
     return NgramPlan(K, n, plan, mplan)
 
 
+def _grid_rows(node_keys: torch.Tensor, alphabet: str, n: int, letters: str) -> torch.Tensor:
+    """Grid row (base-len(letters) number over `letters`) of every node key (base-len(alphabet) number over
+    `alphabet`'s code), -1 where a character is not one of `letters`."""
+    Ka, Kg = max(len(alphabet), 1), len(letters)
+    lut = torch.full((Ka,), -1, dtype=torch.int64)
+    for code, ch in enumerate(alphabet):
+        pos = letters.find(ch)
+        if pos >= 0:
+            lut[code] = pos
+    lut = lut.to(node_keys.device)
+    k = node_keys.to(torch.int64).clone()
+    grid = torch.zeros_like(k)
+    ok = torch.ones_like(k, dtype=torch.bool)
+    scale = 1
+    for _ in range(n):  # last character first
+        d = lut[k % Ka]
+        ok &= d >= 0
+        grid += d.clamp(min=0) * scale
+        scale *= Kg
+        k //= Ka
+    return torch.where(ok, grid, torch.full_like(grid, -1))
+
+
+def build_ngram_map(g: CSRGraph, node_keys: torch.Tensor, alphabet: str, n: int, letters: str = GRID_LETTERS,
+                    min_fill: float = 0.5) -> Optional[NgramMap]:
+    """The mapped middle plan (NgramMap) of a shared-pattern device graph whose node i is the n-gram with key
+    node_keys[i] (base-len(alphabet) digits in `alphabet`'s code, e.g. ngram.NgramTransitions), or None when the
+    grid part is too small to pay (fewer than min_fill * 20^n nodes on the grid: the kernel walks the whole grid),
+    or the graph is not shared-pattern on the GPU. Every CSR entry goes either to its grid slot or to the
+    residual CSR, so the result covers the whole propagation; integer work only (torch sorts and one plan kernel)."""
+    from . import ops
+    K = len(letters)
+    if (K != 20 or len(set(letters)) != K or not g.shared or g.edges3 is None or not g.rowptr.is_cuda or n < 2
+            or node_keys.numel() != g.n_rows):
+        return None
+    grid_n = K ** n
+    if grid_n >= 2 ** 31:
+        return None
+    dev = g.rowptr.device
+    ginv = _grid_rows(node_keys.to(dev), alphabet, n, letters)
+    on = ginv >= 0
+    n_grid = int(on.sum())
+    if n_grid < min_fill * grid_n:
+        return None
+    if n_grid and int(torch.unique(ginv[on]).numel()) != n_grid:
+        raise ValueError("two nodes share one n-gram (node keys must be distinct)")
+    gmap = torch.full((grid_n,), -1, dtype=torch.int32, device=dev)
+    gmap[ginv[on]] = torch.nonzero(on).view(-1).to(torch.int32)
+    ginv = ginv.to(torch.int32).contiguous()
+    lib = ops.load_library()
+    floats = int(lib.pg_ngram_mplan_floats(K, n, grid_n))
+    mplan = torch.empty(floats, dtype=torch.float32, device=dev)
+    resid = torch.empty(max(g.nnz, 1), dtype=torch.uint8, device=dev)
+    ops.check(lib.pg_ngram_mplan_map_f32(K, n, g.n_rows, ops._p(g.rowptr), ops._p(g.edges3), ops._p(ginv),
+                                         ops._p(mplan), floats, ops._p(resid), ops._stream(mplan)),
+              "pg_ngram_mplan_map_f32")
+    rmask = resid[:g.nnz].bool()
+    rows = torch.repeat_interleave(torch.arange(g.n_rows, device=dev), g.rowptr[1:] - g.rowptr[:-1])
+    res_rows = rows[rmask]
+    res_rowptr = _rowptr(res_rows, g.n_rows)
+    res_edges = g.edges3[rmask].contiguous()  # CSR order kept: ascending column within a row
+    has_res = (res_rowptr[1:] - res_rowptr[:-1]) > 0
+    rows_off = torch.nonzero(~on).view(-1).to(torch.int32)
+    rows_acc = torch.nonzero(on & has_res).view(-1).to(torch.int32)
+    return NgramMap(K, n, mplan, gmap, ginv, res_rowptr, res_edges, rows_off, rows_acc, n_grid, int(res_edges.size(0)))
+
+
+def attach_ngram_map(g: CSRGraph, transitions, letters: str = GRID_LETTERS, min_fill: float = 0.5) -> CSRGraph:
+    """Attach the mapped middle plan to a graph of a builder-produced level (`transitions`: an
+    ngram.NgramTransitions -- ngram_transitions, read_level or transitions_from_table -- whose node ids are the
+    graph's rows). For the reference trainer's wiring (csr_from_coo on mathcal_A_*), pass the level the matrices
+    were built from. A graph that already runs the complete-grid plan (g.ngram) is left as it is."""
+    if g.ngram is None:
+        g.ngram_map = build_ngram_map(g, transitions.node_keys, transitions.alphabet, transitions.n, letters,
+                                      min_fill)
+    return g
+
+
 def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: float = 1e-9,
                           keep_raw: bool = True, schedule: bool = True,
-                          ngram_alphabet: Optional[int] = 20) -> CSRGraph:
+                          ngram_alphabet: Optional[int] = 20, transitions=None) -> CSRGraph:
     """Shared-pattern device CSR of (mathcal_A_in, mathcal_A_out, A_undirected_norm) from raw counts.
 
     Weights are materialised on the GPU by ``pg_edges_normalize_f32`` (bit-exact closed form of
     graph_utils.py:198-273 / :160-196). When the node set is all ngram_alphabet^n n-grams (node id = base-K
-    number), the n-gram tile plan is attached as well (build_ngram_plan; None to skip)."""
+    number), the n-gram tile plan is attached as well (build_ngram_plan; None to skip). With `transitions` (the
+    ngram.NgramTransitions of a builder-produced level these counts come from) a graph that is not the complete grid
+    gets the mapped middle plan instead (attach_ngram_map)."""
     from . import ops
 
     if int(num_nodes) > 0 and np.asarray(src).size == 0:
@@ -418,4 +536,6 @@ def build_propagation_csr(num_nodes: int, src, dst, cnt, device="cuda", eps: flo
                  node_norm=rc.node_norm if keep_raw else None, eps=eps, nnz=rc.nnz, row_order=rc.row_order)
     if ngram_alphabet and g.edges3.is_cuda:
         g.ngram = build_ngram_plan(g, ngram_alphabet)
+        if g.ngram is None and transitions is not None:
+            attach_ngram_map(g, transitions)
     return g

@@ -117,6 +117,30 @@ def _ngram_fwd(lib, g, x, a, Z, fl, s):
     return _lib.PG_ERR_UNSUPPORTED
 
 
+def _map_ok(g: CSRGraph, x: torch.Tensor, fl: int) -> bool:
+    """The mapped middle-tile forward (builder-produced graphs, g.ngram_map) takes this call: fp32 x with the graph's
+    rows, F a multiple of 16, and PG_FLAG_NO_NGRAM not set."""
+    return (g.ngram_map is not None and not (fl & PG_FLAG_NO_NGRAM) and x.dtype == torch.float32
+            and x.size(0) == g.n_rows and x.size(1) % 16 == 0)
+
+
+def _map_fwd(lib, g, x, Z, fl, s):
+    """Mapped n-gram forward: the grid part by pg_spmm3_ngram_mid_map_f32, then the residual CSR pass
+    (pg_spmm3_rows_f32) over the off-grid rows (overwrite) and the grid rows with residual entries (accumulate).
+    Returns the first non-zero return code (PG_ERR_UNSUPPORTED before anything launched: the caller falls back)."""
+    m, F = g.ngram_map, x.size(1)
+    rc = lib.pg_spmm3_ngram_mid_map_f32(m.K, m.n, _p(m.mplan), _p(m.gmap), _p(x), x.stride(0), F, _p(Z), Z.stride(0),
+                                        fl, s)
+    if rc:
+        return rc
+    for rows, acc in ((m.rows_off, 0), (m.rows_acc, 1)):
+        if rows.numel():
+            rc = lib.pg_spmm3_rows_f32(rows.numel(), _p(m.res_rowptr), _p(rows), _p(m.res_edges), _p(x), x.stride(0),
+                                       F, _p(Z), Z.stride(0), acc, fl, s)
+            check(rc, "pg_spmm3_rows_f32")
+    return 0
+
+
 def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fused: bool = False,
           flags: Optional[int] = None) -> torch.Tensor:
     """Z = [A_in x | A_out x | A_und x] ([n_rows, 3F]) through the HIP kernels. bf16 x -> bf16 Z
@@ -145,6 +169,12 @@ def spmm3(g: CSRGraph, x: torch.Tensor, out: Optional[torch.Tensor] = None, fuse
         rc = _ngram_fwd(lib, g, x, None, Z, fl, s)
         if rc != _lib.PG_ERR_UNSUPPORTED:  # unaligned operands / other widths: the CSR kernel below
             check(rc, "pg_spmm3_ngram_(mid_)f32")
+            _ev_end(x, ev)
+            return Z
+    if g.shared and not fused and _map_ok(g, x, fl):  # builder-produced graphs: mapped middle-tile + residual
+        rc = _map_fwd(lib, g, x, Z, fl, s)
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_spmm3_ngram_mid_map_f32")
             _ev_end(x, ev)
             return Z
     if g.shared:
@@ -295,7 +325,7 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     if _is_bf16(x) or not g.shared or g.edges3 is None:
         return None
     fl = default_flags() if flags is None else flags
-    if _mid_ok(g, x, fl):  # the middle-tile kernel has no gated store: the dense kernel applies the gates
+    if _mid_ok(g, x, fl) or _map_ok(g, x, fl):  # the middle-tile kernels have no gated store: the dense kernel gates
         return None
     lib = load_library()
     x = _f32c(x)
@@ -378,6 +408,29 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
         for k, a in enumerate(g.adj):
             check(lib.pg_spmm1_f32(N, _p(a.rowptr_t), None, _p(a.edges_t), _p(G[:, k * F:]), G.stride(0), F, _p(dX),
                                    dX.stride(0), 1 if k else 0, fl, s), "pg_spmm1_f32")
+    return dX
+
+
+def spmm3t_rows(rowptr_t: torch.Tensor, edges3_t: torch.Tensor, rows: torch.Tensor, G: torch.Tensor, n_out: int,
+                flags: Optional[int] = None) -> torch.Tensor:
+    """dX[r] = sum_e (w_in G[col, 0:F] + w_out G[col, F:2F] + w_und G[col, 2F:3F]) for the rows r in `rows` (int32)
+    of a transposed CSR over n_out rows (pg_spmm3t_f32 / pg_spmm3t_bf16 with `rows` as the row order); the other rows
+    of the [n_out, F] result are left unwritten. The middle trainer's propagation backward (shard.MiddleTranspose)."""
+    lib = load_library()
+    bf = _is_bf16(G)
+    G = _bf16c(G) if bf else _f32c(G)
+    _require_gpu(G, rowptr_t, edges3_t, rows)
+    if rows.dtype != torch.int32 or rowptr_t.numel() != n_out + 1:
+        raise ValueError("spmm3t_rows: int32 rows and a rowptr of n_out + 1 entries")
+    F = G.size(1) // 3
+    dX = torch.empty(n_out, F, device=G.device, dtype=G.dtype)
+    fl = default_flags() if flags is None else flags
+    if bf:
+        check(lib.pg_spmm3t_bf16(rows.numel(), _p(rowptr_t), _p(rows), _p(edges3_t), _p(G), G.stride(0), F, _p(dX),
+                                 dX.stride(0), fl, _stream(G)), "pg_spmm3t_bf16")
+    else:
+        check(lib.pg_spmm3t_f32(rows.numel(), _p(rowptr_t), _p(rows), _p(edges3_t), _p(G), G.stride(0), F, _p(dX),
+                                dX.stride(0), 0, fl, _stream(G)), "pg_spmm3t_f32")
     return dX
 
 

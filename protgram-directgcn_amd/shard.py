@@ -1126,3 +1126,278 @@ class MiddleRunner:
                 self._exchange(i, c)
         self._wait()
         return self.out
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Middle-partition training (BASELINE config 5: the trainer's full-batch step on P ranks without any N x F collective)
+# ---------------------------------------------------------------------------------------------------------------
+# Per layer the rank propagates its middles with the middle-tile kernel (spmm3_middles: Z of its rows, middle-major)
+# from the layer input in the global row layout, in which only its own rows and the ghost rows its middles read are
+# valid (the forward exchange: MiddlePartition's lists, one all_to_all per layer boundary and chunk). Backward:
+#   * the propagation's input gradient is A[own, :]^T dZ_own -- nonzero exactly on own + ghost rows -- from the
+#     transposed CSR kernel over the rank's COLUMN block (MiddleTranspose: rows = own + ghost, columns = owned-row
+#     positions; the n-gram matrices are symmetric, so it is the owned rows' CSR transposed);
+#   * the exchange's backward sends each ghost row's gradient back to its owner (the reverse all_to_all over the same
+#     lists, F wide like the forward) and the owner adds what it receives to its own rows' gradients, one source
+#     rank at a time (each slice holds distinct rows: deterministic sums);
+#   * dense weights / biases are replicated (one flat all-reduce of their gradients per step), per-node parameters
+#     (gates, constant) are owned-row leaves in middle-major order (no communication; `sync_model` writes them back).
+# So a layer boundary costs 2 x (ghost rows x F) per rank over xGMI instead of the node-range trainer's N x F
+# all-gather + N x F reduce-scatter. Reference: protgram_directgcn_trainer.py:76-108 (loop), config.py:63 (dims).
+class TorchComm:
+    """The collectives the middle trainer uses, over torch.distributed (RCCL for CUDA tensors on 'nccl'; gloo stages
+    device tensors through host buffers)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
+        if inp.is_cuda and dist.get_backend(self.group) == "gloo":
+            o = out.new_empty(out.shape, device="cpu")
+            dist.all_to_all_single(o, inp.cpu(), list(out_splits), list(in_splits), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.group)
+
+    def all_reduce(self, t: torch.Tensor):
+        if t.is_cuda and dist.get_backend(self.group) == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=self.group)
+
+
+@dataclass
+class MiddleTranspose:
+    """The rank's column block of the (symmetric) propagation matrices as a transposed CSR over all N rows: row j
+    holds an entry (column = owned-row position of i, the weights of A[i, j]) for every owned row i that reads j.
+    `rows` (int32) lists the rows with entries (own + ghost) -- the rows pg_spmm3t_f32 / _bf16 compute."""
+    rowptr: torch.Tensor
+    edges3: torch.Tensor
+    rows: torch.Tensor
+    nnz: int
+
+
+def middle_transpose(mp: MiddlePartition) -> MiddleTranspose:
+    hit = mp.cache.get("transpose")
+    if hit is not None:
+        return hit
+    if not mp.graph.symmetric:
+        raise NotImplementedError("middle training needs symmetric propagation matrices (n-gram graphs)")
+    oc = mp.own_csr
+    dev = oc.rowptr.device
+    cnt = oc.rowptr[1:] - oc.rowptr[:-1]
+    pos = torch.repeat_interleave(torch.arange(mp.n_own, dtype=torch.int64, device=dev), cnt)
+    j = oc.edges3[:, 0].to(torch.int64)
+    order = torch.sort(j * max(mp.n_own, 1) + pos).indices  # by (row j, owned position): ascending within a row
+    e = take(oc.edges3, order).clone()
+    e[:, 0] = take(pos, order).to(torch.int32)
+    js = take(j, order)
+    rowptr = torch.zeros(mp.n + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(torch.bincount(js, minlength=mp.n), 0)
+    rows = torch.unique(js).to(torch.int32)
+    mt = MiddleTranspose(rowptr, e.contiguous(), rows, int(e.size(0)))
+    mp.cache["transpose"] = mt
+    return mt
+
+
+class _MidPropagate(torch.autograd.Function):
+    """X (global row layout; own + ghost rows valid) -> Z of the owned rows [n_own, 3F] (middle-major)."""
+
+    @staticmethod
+    def forward(ctx, X, mp: MiddlePartition):
+        ctx.mp = mp
+        return _owned_spmm3(mp, X)
+
+    @staticmethod
+    def backward(ctx, dZ):
+        if not ctx.needs_input_grad[0]:
+            return None, None
+        mp = ctx.mp
+        mt = middle_transpose(mp)
+        return ops.spmm3t_rows(mt.rowptr, mt.edges3, mt.rows, dZ.contiguous(), mp.n), None
+
+
+def reverse_exchange(mp: MiddlePartition, dX: torch.Tensor, comm) -> torch.Tensor:
+    """Backward of the forward exchange: the gradients of this rank's ghost rows (dX at mp.recv_ids) go back to their
+    owners; returns the [n_own, F] sum of what the other ranks sent for this rank's rows (at least fp32), each source's slice
+    added in turn (distinct rows per slice: deterministic)."""
+    F_ = dX.size(1)
+    send = dX.index_select(0, mp.recv_ids)  # ordered (chunk, source) as received forward
+    recv = send.new_empty(int(mp.send_pos.numel()), F_)
+    s0 = r0 = 0
+    for c in range(mp.chunks):
+        ns, nr = sum(mp.chunk_recv[c]), sum(mp.chunk_send[c])
+        comm.all_to_all(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_send[c], mp.chunk_recv[c])
+        s0, r0 = s0 + ns, r0 + nr
+    out = torch.zeros(mp.n_own, F_, dtype=torch.promote_types(dX.dtype, torch.float32), device=dX.device)
+    off = 0
+    for c in range(mp.chunks):
+        for q in range(len(mp.chunk_send[c])):
+            k = mp.chunk_send[c][q]
+            if k:
+                out.index_add_(0, mp.send_pos[off:off + k], recv[off:off + k].to(out.dtype))
+            off += k
+    return out
+
+
+def forward_exchange(mp: MiddlePartition, h_own: torch.Tensor, comm) -> torch.Tensor:
+    """The next layer's input in the global row layout: own rows + the ghost rows received from their owners (other
+    rows unwritten); per chunk one all_to_all (the lists are grouped by (chunk, rank))."""
+    F_ = h_own.size(1)
+    X = h_own.new_empty(mp.n, F_)
+    X.index_copy_(0, mp.own, h_own)
+    if mp.world > 1 or mp.loopback:
+        send = h_own.index_select(0, mp.send_pos)
+        recv = send.new_empty(int(mp.recv_ids.numel()), F_)
+        s0 = r0 = 0
+        for c in range(mp.chunks):
+            ns, nr = sum(mp.chunk_send[c]), sum(mp.chunk_recv[c])
+            comm.all_to_all(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_recv[c], mp.chunk_send[c])
+            s0, r0 = s0 + ns, r0 + nr
+        X.index_copy_(0, mp.recv_ids, recv)
+    return X
+
+
+class _MidExchange(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h_own, mp: MiddlePartition, comm):
+        ctx.mp, ctx.comm = mp, comm
+        return forward_exchange(mp, h_own, comm)
+
+    @staticmethod
+    def backward(ctx, dX):
+        mp = ctx.mp
+        if mp.loopback:  # the received copies overwrote the own rows: they carry the whole gradient
+            d = reverse_exchange(mp, dX, ctx.comm)
+        else:
+            d = dX.index_select(0, mp.own).float()
+            if mp.world > 1:
+                d = d + reverse_exchange(mp, dX, ctx.comm)
+        return d.to(dX.dtype), None, None
+
+
+class MiddleTrainer:
+    """ShardedTrainer's step (the reference's full-batch loop, protgram_directgcn_trainer.py:91-100: zero_grad ->
+    forward -> nll_loss (mean over all N nodes) + l2_lambda * sum_p ||p||^2 -> backward -> Adam step) on the middle
+    partition (see the section comment): the middle-tile forward over the rank's middles, ghost-row exchanges only.
+    Same optimizer semantics as ShardedTrainer (train.Adam with the L2 gradient folded in, device-side loss, no host
+    sync per step); `comm` = the collectives (TorchComm(group) by default). Per-node parameters live in owned-row
+    leaves in middle-major order (self.own[layer][name]); `sync_model()` writes them into this rank's rows of the
+    model's full per-node parameters (rows owned elsewhere stay stale on this rank, as with ShardedTrainer)."""
+
+    def __init__(self, model, mp: MiddlePartition, lr: float = 1e-3, l2_lambda: float = 1e-7, comm=None,
+                 optimizer_factory=None, **adam_kw):
+        from . import train
+        self.model, self.mp, self.l2_lambda = model, mp, float(l2_lambda)
+        self.comm = comm if comm is not None else TorchComm()
+        self.xchg = mp.world > 1 or mp.loopback
+        self.own: List[dict] = []
+        node_ids, dense, node_leaves = set(), [], []
+        rows = mp.own
+        for conv in model.convs:
+            d = {}
+            for name, p in conv.named_parameters(recurse=False):
+                if _is_node_param(name, p, mp.n):
+                    leaf = nn.Parameter(p.detach().index_select(0, rows.to(p.device)).contiguous(),
+                                        requires_grad=p.requires_grad)
+                    d[name] = leaf
+                    node_ids.add(id(p))
+                    node_leaves.append(leaf)
+            self.own.append(d)
+        for name, p in model.named_parameters():
+            if id(p) not in node_ids and p.requires_grad:
+                dense.append(p)
+        self.dense, self.node = dense, node_leaves
+        dev = dense[0].device if dense else mp.own.device
+        self.flat = torch.zeros(sum(p.numel() for p in dense), dtype=torch.float32, device=dev)
+        self.params = dense + [p for p in node_leaves if p.requires_grad]
+        self.opt = (train.Adam(self.params, lr=lr, **adam_kw) if optimizer_factory is None
+                    else optimizer_factory(self.params))
+        self._train = train
+        self._touched: set = set()
+        for prm in self.params:
+            prm.register_post_accumulate_grad_hook(lambda t: self._touched.add(id(t)))
+        middle_transpose(mp)  # setup work, outside the steps
+
+    def forward(self, x_full: torch.Tensor):
+        """(log_probs, emb) of the owned rows (middle-major) with autograd."""
+        model, mp = self.model, self.mp
+        h = model._apply_pe(x_full)
+        if model.compute_dtype == torch.bfloat16:
+            h = h.to(torch.bfloat16)
+        elif model.compute_dtype != torch.float32:
+            raise ValueError("compute_dtype must be torch.float32 or torch.bfloat16")
+        X, res_x = h, h.index_select(0, mp.own)
+        L = len(model.convs)
+        h_own = None
+        for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
+            Z = _MidPropagate.apply(X, mp)
+            vec = conv.use_vector_coeffs
+            params = conv._dense_params()
+            own = self.own[i]
+            if vec:
+                params = params[:10] + tuple(own[k] for k in _GATE_NAMES)
+                constant = own["constant"]
+            else:
+                constant = None
+            W_res, b_res = (res.weight, res.bias) if isinstance(res, nn.Linear) else (None, None)
+            h_own = ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, None, 0 if vec else 1, True,
+                                         ops.LEAKY_SLOPE, *params)
+            h_own = F.dropout(h_own, p=model.dropout, training=model.training)
+            if i + 1 < L:
+                X = _MidExchange.apply(h_own, mp, self.comm)
+                res_x = h_own
+        return model.head(h_own)
+
+    def step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
+        """One step; y_own = the labels of the owned rows (y[mp.own]). Returns the global loss (device scalar)."""
+        mp, lam, train = self.mp, self.l2_lambda, self._train
+        for p in self.node:
+            p.grad = None
+        self.flat.zero_()
+        off = 0
+        for p in self.dense:
+            k = p.numel()
+            p.grad = self.flat[off:off + k].view_as(p)
+            off += k
+        lp, _ = self.forward(x_full)
+        nll = -lp.float().gather(1, y_own.view(-1, 1)).sum() / mp.n
+        self._touched = set()
+        nll.backward()
+        if lam:
+            for p in self.node:
+                if p.requires_grad and p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            l2_rep = train.l2_sqsum(self.dense) if self.dense else nll.new_zeros(())
+            l2_own = train.l2_sqsum(self.node) if self.node else nll.new_zeros(())
+        else:
+            for p in self.params:
+                if id(p) not in self._touched:
+                    p.grad = None
+            l2_rep = l2_own = nll.new_zeros(())
+        parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
+        if self.xchg and mp.world > 1:
+            if self.flat.numel():
+                self.comm.all_reduce(self.flat)
+            self.comm.all_reduce(parts)
+        fold = bool(lam) and isinstance(self.opt, train.Adam)
+        if lam and not fold:
+            ps = [p for p in self.params if p.grad is not None]
+            torch._foreach_add_([p.grad for p in ps], [p.detach() for p in ps], alpha=2.0 * lam)
+        if fold:
+            self.opt._l2_extra = 2.0 * lam
+        try:
+            self.opt.step()
+        finally:
+            if fold:
+                self.opt._l2_extra = 0.0
+        return parts.sum() + lam * l2_rep
+
+    @torch.no_grad()
+    def sync_model(self):
+        """Write this rank's owned-row leaves into the model's full per-node parameters (rows mp.own)."""
+        for conv, d in zip(self.model.convs, self.own):
+            for name, leaf in d.items():
+                getattr(conv, name).data.index_copy_(0, self.mp.own.to(leaf.device), leaf.data)

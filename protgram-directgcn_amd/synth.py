@@ -12,7 +12,10 @@ Two generators:
   ``data_builder.py:38-54`` does (no space padding), then grouped into unique
   ``(source, target) -> count`` rows as ``data_builder.py:267-273`` does.
 
-Both return ``(num_nodes, src int64[E], dst int64[E], count float32[E])`` with unique
+:func:`protein_sequences` makes seeded protein-like inputs for ``ngram.ngram_transitions`` (the builder's padded
+graphs, off the complete grid).
+
+Both edge generators return ``(num_nodes, src int64[E], dst int64[E], count float32[E])`` with unique
 ``(src, dst)`` pairs sorted row-major, i.e. the content of the reference's edge parquet.
 """
 from __future__ import annotations
@@ -56,6 +59,38 @@ def random_sequences(num_seqs: int, length: int, seed: int = 0) -> list[str]:
     rng = np.random.default_rng(seed)
     letters = np.array(list(ALPHABET))
     return ["".join(letters[rng.integers(0, SIGMA, size=length)]) for _ in range(num_seqs)]
+
+
+# UniProtKB/Swiss-Prot amino-acid composition (percent, ALPHABET order), for protein-like synthetic sequences
+_AA_PERCENT = (8.25, 1.38, 5.46, 6.72, 3.86, 7.07, 2.27, 5.91, 5.80, 9.64, 2.41, 4.06, 4.74, 3.93, 5.53, 6.65, 5.36,
+               6.86, 1.10, 2.92)
+
+
+def protein_sequences(num_seqs: int, mean_len: int = 350, seed: int = 0, rare: float = 0.001,
+                      composition: str = "swissprot") -> list[str]:
+    """Seeded protein-like sequences for builder-produced graphs (the input run_graph_builder.py reads): lengths
+    uniform in [mean_len / 2, 3 mean_len / 2], letters drawn with the Swiss-Prot composition ('uniform': equal), and
+    a `rare` share of positions replaced by the non-standard letters X / U / B / Z (which put n-grams off the
+    20-letter grid, as the padding ' ' of data_builder.py:29-35 does)."""
+    rng = np.random.default_rng(seed)
+    letters = np.array(list(ALPHABET))
+    if composition == "uniform":
+        prob = np.full(SIGMA, 1.0 / SIGMA)
+    else:
+        prob = np.asarray(_AA_PERCENT, dtype=np.float64)
+        prob = prob / prob.sum()
+    lo, hi = max(1, mean_len // 2), max(1, mean_len // 2) + mean_len
+    odd = np.array(list("XUBZ"))
+    out = []
+    for _ in range(num_seqs):
+        L = int(rng.integers(lo, hi + 1))
+        seq = letters[rng.choice(SIGMA, size=L, p=prob)]
+        if rare > 0:
+            hit = rng.random(L) < rare
+            if hit.any():
+                seq[hit] = odd[rng.integers(0, odd.size, size=int(hit.sum()))]
+        out.append("".join(seq))
+    return out
 
 
 def fasta_edges(n: int, sequences: list[str]):

@@ -1,0 +1,123 @@
+"""BASELINE config 5 (3-layer DirectGCN, 4-gram graph, dims [128, 256, 256, 256], the trainer's full-batch step on
+8 MI355X) through shard.MiddleTrainer at its size: P = 8 ranks as 8 processes sharing this one GPU, gloo carrying
+the ghost-row exchanges, their transposes and the gradient all-reduce (the same calls RCCL runs on the 8-GPU node;
+tests/test_gpu_rccl.py runs the RCCL branch itself). Every rank propagates its middles on the middle-tile kernel
+(launches counted) and backpropagates through the transposed CSR kernel over its column block.
+
+Each rank checks its own share against the single-GPU step on the same model and inputs (computed in the rank's
+process before the trainer runs): the global loss, every replicated parameter gradient after the all-reduce and the
+owned rows of every per-node parameter gradient. fp32: |d| <= 1e-4 max|ref| + 1e-4 |ref| (the kernels sum in
+other orders than the single-GPU step's); bf16 mode against the fp32 step (as test_gpu_configs' config-5 test):
+loss within 2 %, gradient cosine > 0.99. Reference loop: protgram_directgcn_trainer.py:76-108; dims: config.py:63."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+WORLD = 8
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_q, bf16):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard, train
+    from test_gpu_configs import _labels, _model
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bad = []
+    try:
+        n, dims, lam = 4, [128, 256, 256, 256], 1e-7
+        N, s, d, c = pkg.synth.de_bruijn_edges(n)
+        g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+        x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(dev)
+        y = _labels(N, n).to(dev)
+        # single-GPU reference step (fp32): loss and gradients
+        ref = _model(pkg, dims, N, n).to(dev).eval()
+        lp, _ = ref(pkg.Data(x=x, graph=g))
+        loss_r = train.nll_mean(lp, y) + lam * sum(p.norm(2).pow(2) for p in ref.parameters())
+        loss_r.backward()
+        rgrad = {k: p.grad.detach().float().clone() for k, p in ref.named_parameters()}
+        loss_r = float(loss_r.detach())
+        del ref, lp
+        torch.cuda.synchronize()
+        # this rank of the middle partition
+        mp_ = shard.middle_partition(g, rank, world)
+        m = _model(pkg, dims, N, n).to(dev).eval()
+        if bf16:
+            m.compute_dtype = torch.bfloat16
+        tr = shard.MiddleTrainer(m, mp_, l2_lambda=lam)
+        hits = []
+        real = ops.spmm3_middles
+        ops.spmm3_middles = lambda *a, **k: hits.append(1) or real(*a, **k)
+        loss = float(tr.step(x, y[mp_.own]))
+        torch.cuda.synchronize()
+        if len(hits) != len(dims) - 1:
+            bad.append(("middle-tile launches", len(hits)))
+        if bf16:
+            if abs(loss - loss_r) > 2e-2 * abs(loss_r):
+                bad.append(("loss", loss, loss_r))
+        elif abs(loss - loss_r) > 1e-5 * abs(loss_r):
+            bad.append(("loss", loss, loss_r))
+        own = mp_.own
+        for name, p in m.named_parameters():
+            r = rgrad[name]
+            if shard._is_node_param(name, p, N):
+                gg = tr.own[int(name.split(".")[1])][name.split(".")[-1]].grad
+                r = r[own]
+            else:
+                gg = p.grad
+            if gg is None:
+                bad.append((name, "no grad"))
+                continue
+            gg = gg.detach().float()
+            if bf16:
+                cos = float((gg * r).sum() / (gg.norm() * r.norm() + 1e-30))
+                if cos < 0.99:
+                    bad.append((name, "cos", cos))
+            else:
+                err = (gg - r).abs()
+                if bool((err > 1e-4 * float(r.abs().max()) + 1e-4 * r.abs()).any()):
+                    bad.append((name, "grad", float(err.max()), float(r.abs().max())))
+        out_q.put((rank, mp_.n_own, int(mp_.recv_ids.numel()), not bad, str(bad[:4]), loss, loss_r))
+    except Exception as e:  # report instead of hanging the parent
+        out_q.put((rank, 0, 0, False, repr(e)[:400], 0.0, 0.0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("bf16", [False, True])
+def test_config5_middle_trainer_p8_one_gpu(cuda, bf16):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, bf16)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=840) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=120)
+    assert env_keep is None or os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") == env_keep
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert sum(r[1] for r in res) == 160_000
+    for r in res:
+        assert r[3], f"rank {r[0]}: {r[4]}"
+    print("ranks (rank, own rows, ghost rows, loss, single-GPU loss):", [(r[0], r[1], r[2], r[5], r[6]) for r in res])

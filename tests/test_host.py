@@ -206,3 +206,28 @@ def test_bench_launches_its_own_ranks():
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["world_size"] == 2 and out["ranks"] == 2 and out["rank_sum"] == 1.0
+
+
+def test_grid_rows_of_builder_keys(pkg):
+    """graph._grid_rows: the node keys of a builder-produced level (alphabet with the padding ' ' and rare letters,
+    code = index in the sorted alphabet, ngram.encode) map to the base-20 number over GRID_LETTERS, -1 off the grid."""
+    from protgram_directgcn_amd import graph as gr, ngram
+    alphabet = " ABCDEFGHIKLMNPQRSTUVWXYZ"
+    strings = sorted({"ACD", " AC", "WYA", "AXA", "YYY", "CD ", "AAA", "ZAA"})
+    keys = torch.from_numpy(ngram._keys_of(strings, alphabet, 3))
+    got = gr._grid_rows(keys, alphabet, 3, gr.GRID_LETTERS).tolist()
+    for s_, g_ in zip(strings, got):
+        if all(ch in gr.GRID_LETTERS for ch in s_):
+            want = 0
+            for ch in s_:
+                want = want * 20 + gr.GRID_LETTERS.index(ch)
+            assert g_ == want, s_
+        else:
+            assert g_ == -1, s_
+
+
+def test_protein_sequences_seeded(pkg):
+    a = pkg.synth.protein_sequences(5, 40, seed=3, rare=0.2)
+    assert a == pkg.synth.protein_sequences(5, 40, seed=3, rare=0.2)
+    assert all(20 <= len(s) <= 60 for s in a)
+    assert set("".join(a)) <= set(pkg.synth.ALPHABET + "XUBZ") and set("".join(a)) & set("XUBZ")

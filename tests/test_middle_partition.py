@@ -169,3 +169,148 @@ def test_middle_forward_gloo(world):
     assert all(p.exitcode == 0 for p in procs)
     assert sum(r[1] for r in res) == 8000
     assert all(r[2] for r in res), res
+
+
+def _cpu_spmm3t_rows(rowptr_t, edges3_t, rows, G, n_out, flags=None):
+    """CPU stand-in for ops.spmm3t_rows (pg_spmm3t_f32 over a row list); rows outside the list stay NaN."""
+    n = rowptr_t.numel() - 1
+    r = torch.repeat_interleave(torch.arange(n), rowptr_t[1:] - rowptr_t[:-1])
+    col = edges3_t[:, 0].long()
+    F = G.size(1) // 3
+    dX = torch.zeros(n_out, F, dtype=torch.float32)
+    for k in range(3):
+        w = edges3_t[:, 1 + k].contiguous().view(torch.float32)
+        dX.index_add_(0, r, w[:, None] * G[col, k * F:(k + 1) * F].float())
+    keep = torch.zeros(n_out, dtype=torch.bool)
+    keep[rows.long()] = True
+    dX[~keep] = float("nan")
+    return dX.to(G.dtype)
+
+
+def _mid_train_worker(rank, world, port, out_q, chunks, bf16):
+    """shard.MiddleTrainer (middle partition: owned-middle propagation, ghost-row exchange forward and its transpose
+    backward, owned-row per-node state, replicated-gradient all-reduce) for two steps against the single-process
+    oracle's autograd + Adam; also the exchange's adjointness <E h, g> = <h, E^T g> summed over ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard, train
+    from oracle import directgcn_cpu as oc
+    import torch.nn.functional as F
+    from test_shard_gloo import (_any_dtype, _cpu_layer_dense, _cpu_layer_dense_backward, _cpu_spmm3)
+    ops.spmm3 = _any_dtype(_cpu_spmm3)
+    ops.spmm3t_rows = _cpu_spmm3t_rows
+    ops.layer_dense = _any_dtype(_cpu_layer_dense)
+    ops.layer_dense_backward = _any_dtype(_cpu_layer_dense_backward, out_keys=("dpre", "dZ", "dres"))
+    train.l2_sqsum = lambda ps: sum((p.detach().float() ** 2).sum() for p in ps)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bad = []
+    try:
+        N, m, g = _graph(pkg, 3)
+        g.symmetric = True  # the n-gram matrices are symmetric (csr_from_coo on the CPU keeps a separate transpose)
+        mp_ = shard.middle_partition(g, rank, world, chunks=chunks)
+        comm = shard.TorchComm()
+        # adjointness of the exchange (F = 3)
+        gen = torch.Generator().manual_seed(100 + rank)
+        h = torch.randn(mp_.n_own, 3, generator=gen, dtype=torch.float64)
+        G = torch.randn(N, 3, generator=gen, dtype=torch.float64)
+        X = shard.forward_exchange(mp_, h, comm)
+        valid = torch.cat([mp_.own, mp_.recv_ids])
+        lhs = (X[valid] * G[valid]).sum()
+        d = G[mp_.own] + shard.reverse_exchange(mp_, G, comm).double()
+        rhs = (h * d).sum()
+        t = torch.stack([lhs, rhs])
+        dist.all_reduce(t)
+        if abs(float(t[0] - t[1])) > 1e-9 * abs(float(t[0])):
+            bad.append(("adjoint", float(t[0]), float(t[1])))
+        mt = shard.middle_transpose(mp_)
+        if not torch.equal(torch.sort(mt.rows.long()).values, torch.sort(valid).values):
+            bad.append("transpose rows != own + ghost rows")
+        # the training step
+        dims = [16, 16, 16, 12]
+        torch.manual_seed(0)
+        model = pkg.ProtGramDirectGCN(dims, N, 5, 3, 0, 512, 0.5, True).eval()
+        with torch.no_grad():
+            gen = torch.Generator().manual_seed(5)
+            for name, p in model.named_parameters():
+                leaf = name.split(".")[-1]
+                if leaf.startswith("C_"):
+                    p.copy_(torch.rand(p.shape, generator=gen) + 0.5)
+                elif "bias" in leaf:
+                    p.copy_(torch.rand(p.shape, generator=gen) * 0.2 - 0.1)
+        if bf16:
+            model.compute_dtype = torch.bfloat16
+        ref = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+        x = torch.randn(N, 16, generator=torch.Generator().manual_seed(1234))
+        y = (torch.arange(N) // 400) % 5
+        lam, steps, lr = 1e-3, 2, 1e-2
+        tr = shard.MiddleTrainer(model, mp_, l2_lambda=lam, comm=comm,
+                                 optimizer_factory=lambda ps: torch.optim.Adam(ps, lr=lr))
+        losses, grads = [], []
+        for _ in range(steps):
+            loss = tr.step(x, y[mp_.own])
+            losses.append(float(loss))
+            gd = {}
+            for name, p in model.named_parameters():
+                if shard._is_node_param(name, p, N):
+                    gd[name] = tr.own[int(name.split(".")[1])][name.split(".")[-1]].grad.clone()
+                else:
+                    gd[name] = p.grad.clone()
+            grads.append(gd)
+        ropt = torch.optim.Adam(list(ref.values()), lr=lr)
+        rlosses, rgrads = [], []
+        for _ in range(steps):
+            ropt.zero_grad()
+            lp, _ = oc.model_forward(ref, dims, x, *m["in"], *m["out"], *m["und"], n_gram_len=3)
+            loss = F.nll_loss(lp, y) + lam * sum(v.norm(2).pow(2) for v in ref.values())
+            loss.backward()
+            rgrads.append({k: v.grad.clone() for k, v in ref.items()})
+            ropt.step()
+            rlosses.append(float(loss))
+        for st in range(steps):
+            tol = 2e-2 * abs(rlosses[st]) if bf16 else 1e-5 * abs(rlosses[st]) + 1e-6
+            if abs(losses[st] - rlosses[st]) > tol:
+                bad.append(("loss", st, losses[st], rlosses[st]))
+        for name, gg in grads[0].items():
+            r = rgrads[0][name]
+            if shard._is_node_param(name, r, N):
+                r = r[mp_.own]
+            if bf16:
+                cos = float((gg.float() * r).sum() / (gg.float().norm() * r.norm() + 1e-30))
+                if cos < 0.99:
+                    bad.append((name, "cos", cos))
+            else:
+                err = float((gg - r).abs().max())
+                if err > 2e-5 * float(r.abs().max()) + 1e-6:
+                    bad.append((name, "grad", err))
+        tr.sync_model()
+        if not bf16:
+            for name, p in model.named_parameters():
+                got, want = p.detach(), ref[name].detach()
+                if shard._is_node_param(name, p, N):
+                    got, want = got[mp_.own], want[mp_.own]
+                err = float((got - want).abs().max())
+                if err > 2e-5:
+                    bad.append(("param " + name, err))
+        out_q.put((rank, mp_.n_own, not bad, str(bad[:4])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,chunks,bf16", [(2, 1, False), (3, 2, False), (3, 1, True)])
+def test_middle_trainer_gloo(world, chunks, bf16):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mid_train_worker, args=(r, world, port, q, chunks, bf16)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=280) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert sum(r[1] for r in res) == 8000
+    for r in res:
+        assert r[2], f"rank {r[0]}: {r[3]}"

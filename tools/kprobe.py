@@ -28,14 +28,16 @@ ap.add_argument("--layers", type=int, default=2)
 ap.add_argument("--bf16", action="store_true")
 ap.add_argument("--fused-norm", action="store_true")
 ap.add_argument("--entry", choices=("coo", "graph"), default="coo")
+ap.add_argument("--graph", choices=("debruijn", "fasta"), default="debruijn")
+ap.add_argument("--fasta-seqs", type=int, default=8000)
 args = ap.parse_args()
 reps = args.reps
 dev = torch.device("cuda:0")
-N, s, d, c = pkg.synth.de_bruijn_edges(args.ngram)
-g = pkg.build_propagation_csr(N, s, d, c, device=dev, keep_raw=args.fused_norm or not args.forward)
+import bench  # noqa: E402
+wl = bench.build_workload(pkg, args, dev, keep_raw=args.fused_norm or not args.forward)
+N, g, tr = wl["N"], wl["graph"], wl["transitions"]
 
 if args.forward:
-    import bench  # noqa: E402
     model = bench.bench_model(pkg, N, args.feat, args.layers, args.ngram).to(dev).eval()
     model.fused_norm = args.fused_norm
     x = torch.randn(N, args.feat, generator=torch.Generator().manual_seed(1234)).to(dev)
@@ -45,6 +47,9 @@ if args.forward:
     if args.entry == "coo" and not args.fused_norm:  # bench.py's default: the trainer's COO wiring
         data = pkg.synth.trainer_data(g, x)
         del g
+        if tr is not None:  # as bench.py: the level's node map attached to the graph the COO wiring yields
+            with torch.no_grad():
+                pkg.attach_ngram_map(model.graph_of(data), tr)
     else:
         data = pkg.Data(x=x, graph=g)
     with torch.no_grad():

@@ -164,8 +164,9 @@ def main():
     N, g, tr = wl["N"], wl["graph"], wl["transitions"]
     torch.cuda.synchronize()
     log(f"[bench] graph {wl['desc']}: N={N} E={wl['E']} nnz/adj={g.nnz} built in {time.time() - t0:.1f}s"
-        + (f"; mapped plan: {g.ngram_map.n_grid} grid nodes, {g.ngram_map.rows_off.numel()} off-grid rows, "
-           f"{g.ngram_map.nnz_res} residual entries" if g.ngram_map is not None else ""))
+        + (f"; mapped plan: {g.ngram_map.n_grid} grid nodes, {g.ngram_map.n_off} off-grid rows, "
+           f"{g.ngram_map.n_acc} grid rows with {g.ngram_map.nnz_res} residual entries" if g.ngram_map is not None
+           else ""))
 
     model = bench_model(pkg, N, Fd, L, n).to(dev).eval()
     dims = [Fd] * (L + 1)
@@ -307,7 +308,7 @@ def main():
               and Fd % 16 == 0)
     if mapped:  # builder-produced graph: mapped middle-tile kernel + the residual CSR pass (one propagation)
         gated = False
-        kname = "pg_spmm3_ngram_mid_map_f32 + pg_spmm3_rows_f32"
+        kname = "pg_spmm3_ngram_mid_map_f32 + pg_spmm3_resid_f32"
     elif args.bf16:
         kname = ("pg_spmm3_ngram_mid_bf16" if all(gi.ngram is not None and gi.ngram.mplan is not None
                                                   for gi in launch_graphs) and Fd % 16 == 0 else "pg_spmm3_bf16")

@@ -279,17 +279,15 @@ int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan
  * pg_spmm3_ngram_mid_map_f32: Z = the grid part of [A_in X | A_out X | A_und X] at the node rows (X read at node
  *   rows gmap[.]; rows of nodes off the grid are NOT written). Same requirements and numerics as
  *   pg_spmm3_ngram_mid_f32; grid K^n < 2^31.
- * pg_spmm3_rows_f32: pg_spmm3_f32 over the rows rows[0 .. n_list) only (any CSR with n_rows + 1 rowptr entries), each
- *   Z row overwritten (accumulate = 0) or added to (accumulate != 0): the residual entries (resid = 1) as their own
- *   CSR, overwriting the off-grid rows and accumulating into grid rows with residual entries. Bit-exact order per
- *   row as pg_spmm3_f32. */
+ * pg_spmm3_resid_f32: the residual pass -- list position i (rows[i] = node row, bit 31 set = add to Z instead of
+ *   overwriting) over the compact CSR entries [rowptr[i], rowptr[i + 1]) of pg_edge3_t records: Z[row] (+)= the three
+ *   aggregates of those entries (fp32 sums in entry order, 16-B aligned X / Z rows, F % 4 == 0). */
 int pg_ngram_mplan_map_f32(int K, int n, int64_t n_nodes, const int64_t* rowptr, const pg_edge3_t* edges,
                            const int32_t* ginv, float* plan, int64_t plan_floats, uint8_t* resid, void* stream);
 int pg_spmm3_ngram_mid_map_f32(int K, int n, const float* plan, const int32_t* gmap, const float* X, int64_t ldx,
                                int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream);
-int pg_spmm3_rows_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
-                      const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, int accumulate, uint32_t flags,
-                      void* stream);
+int pg_spmm3_resid_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
+                       const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream);
 /* Transposed middle-tile kernel: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k;
  * the backward of the six propagates, protgram_directgcn.py:101-112, replacing pg_spmm3t_ngram_f32 / pg_spmm3t_f32
  * on graphs over all K^n n-grams). Same middle plan, stream and loader as the forward; per chunk three sub-chunks

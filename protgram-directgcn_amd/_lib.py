@@ -89,8 +89,7 @@ SIGNATURES = {
                                               c_vp]),
     "pg_spmm3_ngram_mid_map_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp,
                                                   c_i64, c_u32, c_vp]),
-    "pg_spmm3_rows_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
-                                         c_vp]),
+    "pg_spmm3_resid_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_rows_gather": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "pg_rows_scatter": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,

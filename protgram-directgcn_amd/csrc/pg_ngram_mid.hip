@@ -974,6 +974,57 @@ __global__ __launch_bounds__(256) void ngram_mplan_map_kernel(int64_t Kn1, int64
     }
 }
 
+// Residual pass of a mapped graph (pg_spmm3_resid_f32): one wave per listed row, all of its residual entries, the
+// three aggregates in fp32 (lane q: float4 columns q, q + 64, ...); the row's Z slices are overwritten (a node off the
+// grid) or added to (a grid node: bit 31 of its list entry). Compact CSR: entries of list position i at
+// [rowptr[i], rowptr[i + 1]), so the row id and the entry range load in parallel (no dependent rowptr read).
+__global__ __launch_bounds__(256) void ngram_resid_kernel(int64_t n_list, const int64_t* rowptr, const int* rows,
+                                                          const int4* edges, const float* X, int64_t ldx, int F,
+                                                          float* Z, int64_t ldz) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= n_list) return;
+    const int code = rows[i];
+    const bool add = code < 0;
+    const int64_t row = code & 0x7fffffff;
+    const int64_t e0 = rowptr[i], e1 = rowptr[i + 1];
+    const int F4 = F >> 2;
+    for (int q = lane; q < F4; q += 64) {
+        f4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
+        int64_t e = e0;
+        for (; e + 4 <= e1; e += 4) {  // four gathers in flight
+            int4 r[4];
+            f4_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = edges[e + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const f4_t*>(X + (int64_t)r[u].x * ldx + 4 * q);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                a0 += __int_as_float(r[u].y) * x[u];
+                a1 += __int_as_float(r[u].z) * x[u];
+                a2 += __int_as_float(r[u].w) * x[u];
+            }
+        }
+        for (; e < e1; ++e) {
+            const int4 r = edges[e];
+            const f4_t x = *reinterpret_cast<const f4_t*>(X + (int64_t)r.x * ldx + 4 * q);
+            a0 += __int_as_float(r.y) * x;
+            a1 += __int_as_float(r.z) * x;
+            a2 += __int_as_float(r.w) * x;
+        }
+        f4_t* z = reinterpret_cast<f4_t*>(Z + row * ldz) + q;
+        if (add) {
+            a0 += z[0];
+            a1 += z[F4];
+            a2 += z[2 * F4];
+        }
+        z[0] = a0;
+        z[F4] = a1;
+        z[2 * F4] = a2;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1085,6 +1136,21 @@ int pg_spmm3_ngram_mid_map_f32(int K, int n, const float* plan, const int32_t* g
     for (int t = 0; t < n && grid < (int64_t(1) << 40); ++t) grid *= K;
     PG_REQUIRE(gmap != nullptr, "null row map");
     return mid_launch(K, n, grid, plan, X, ldx, F, 0, -1, false, nullptr, Z, ldz, flags, nullptr, false, stream, gmap);
+}
+
+int pg_spmm3_resid_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
+                       const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream) {
+    (void)flags;
+    PG_REQUIRE(n_list >= 0 && n_list < (int64_t(1) << 31), "bad list length");
+    if (n_list == 0) return PG_OK;
+    PG_REQUIRE(rowptr && rows && edges && X && Z, "null pointer");
+    PG_REQUIRE(F > 0 && F % 4 == 0 && F < (1 << 20), "F must be a positive multiple of 4");
+    PG_REQUIRE(ldx >= F && ldz >= 3 * F, "leading dimensions too small");
+    if (!pg::aligned16(X) || !pg::aligned16(Z) || ldx % 4 || ldz % 4)
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_resid_f32: needs 16-B aligned rows");
+    hipLaunchKernelGGL(ngram_resid_kernel, dim3((unsigned)((n_list + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n_list,
+                       rowptr, rows, reinterpret_cast<const int4*>(edges), X, ldx, (int)F, Z, ldz);
+    return pg::check_launch("pg_spmm3_resid_f32");
 }
 
 int pg_spmm3_ngram_mid_rows_f32(int K, int n, int64_t n_rows, const float* plan, const float* X, int64_t ldx, int64_t F,

@@ -591,17 +591,6 @@ int pg_spmm3_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order
     return dispatch<M3>(p, flags, (hipStream_t)stream, "pg_spmm3_f32");
 }
 
-int pg_spmm3_rows_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
-                      const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, int accumulate, uint32_t flags,
-                      void* stream) {
-    int rc = common_checks(n_list, rowptr, edges, X, ldx, F, Z, ldz, 3 * F, F);
-    if (rc) return rc;
-    PG_REQUIRE(n_list == 0 || rows, "null row list");
-    // the row list is the processing order (row_order): position p computes row rows[p] only
-    SpmmParams p{n_list, rowptr, rows, edges, X, ldx, Z, ldz, nullptr, 0.f, (int)F, accumulate ? 1 : 0, 1};
-    return dispatch<M3>(p, flags & ~(uint32_t)PG_FLAG_EDGE_LDS, (hipStream_t)stream, "pg_spmm3_rows_f32");
-}
-
 int pg_spmm3_gated_f32(int64_t n_rows, const int64_t* rowptr, const int32_t* row_order, const pg_edge3_t* edges,
                        const float* X, int64_t ldx, int64_t F, const pg_layer_args_t* gates, float* Z, int64_t ldz,
                        uint32_t flags, void* stream) {

@@ -68,19 +68,20 @@ class NgramMap:
     """A builder-produced graph (run_graph_builder.py: node ids = sorted-string ranks of the n-grams PRESENT over an
     alphabet with the padding ' ', data_builder.py:29-35, 164-173) laid out for the middle-tile kernel on the grid of
     the K = 20 standard letters (build_ngram_map): the grid part runs pg_spmm3_ngram_mid_map_f32 (X / Z at node rows
-    through gmap), the rest -- rows off the grid and entries with no grid slot -- the residual CSR pass
-    (pg_spmm3_rows_f32: overwrite the off-grid rows, accumulate into the grid rows with residual entries)."""
+    through gmap), the rest -- rows off the grid and entries with no grid slot -- one residual pass
+    (pg_spmm3_resid_f32: overwrite the off-grid rows, add into the grid rows with residual entries)."""
     K: int
     n: int
     mplan: torch.Tensor      # fp32 [K^(n-2) * 52,400]: middle plan of the grid part
     gmap: torch.Tensor       # int32 [K^n]: node row of grid row g, -1 = n-gram not a node
     ginv: torch.Tensor       # int32 [N]: grid row of node i, -1 = off the grid
-    res_rowptr: torch.Tensor  # int64 [N + 1]: residual entries per node row
+    res_rowptr: torch.Tensor  # int64 [n_res + 1]: compact CSR of the residual rows (list position -> entries)
+    res_rows: torch.Tensor    # int32 [n_res]: node row; bit 31 set = a grid row (the pass adds to the tile output)
     res_edges: torch.Tensor   # int32 [nnz_res, 4]: the residual entries (records as edges3, CSR order kept)
-    rows_off: torch.Tensor    # int32: node rows off the grid (residual pass overwrites)
-    rows_acc: torch.Tensor    # int32: grid node rows holding residual entries (residual pass accumulates)
     n_grid: int = 0           # nodes on the grid
     nnz_res: int = 0
+    n_off: int = 0            # residual rows off the grid (overwritten)
+    n_acc: int = 0            # residual rows on the grid (added to)
 
 
 @dataclass
@@ -126,8 +127,8 @@ class CSRGraph:
                                 None if self.ngram.mplan is None else self.ngram.mplan.to(device))
         if self.ngram_map is not None:
             m = self.ngram_map
-            g.ngram_map = NgramMap(m.K, m.n, *(mv(t) for t in (m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_edges,
-                                                                 m.rows_off, m.rows_acc)), m.n_grid, m.nnz_res)
+            g.ngram_map = NgramMap(m.K, m.n, *(mv(t) for t in (m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_rows,
+                                                                 m.res_edges)), m.n_grid, m.nnz_res, m.n_off, m.n_acc)
         return g
 
     def tensors(self):
@@ -136,7 +137,7 @@ class CSRGraph:
               self.ngram.mplan if self.ngram is not None else None]
         if self.ngram_map is not None:
             m = self.ngram_map
-            ts += [m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_edges, m.rows_off, m.rows_acc]
+            ts += [m.mplan, m.gmap, m.ginv, m.res_rowptr, m.res_rows, m.res_edges]
         for a in self.adj:
             ts += [a.rowptr, a.edges, a.rowptr_t, a.edges_t]
         return [t for t in ts if t is not None]
@@ -164,9 +165,9 @@ class CSRGraph:
             return 4 * self.ngram.mplan.numel() + nx * F * elem + 3 * n * F * elem + g  # middle-tile kernel: its plan
         if self.ngram_map is not None and F % 16 == 0 and elem == 4:  # mapped middle-tile kernel + residual CSR pass
             m = self.ngram_map
-            nr = m.rows_off.numel() + m.rows_acc.numel()  # residual rows: list + rowptr pair + records (+ Z re-read)
+            nr = m.n_off + m.n_acc  # residual rows: list entry + rowptr + records (+ the added-to Z rows re-read)
             return (4 * m.mplan.numel() + 4 * m.gmap.numel() + nx * F * elem + 3 * n * F * elem + g
-                    + 20 * nr + 16 * m.nnz_res + 3 * m.rows_acc.numel() * F * elem)
+                    + 12 * nr + 16 * m.nnz_res + 3 * m.n_acc * F * elem)
         if self.ngram is not None and F in (64, 128, 256) and elem == 4:  # the n-gram tile kernel reads its plan instead
             return 4 * self.ngram.plan.numel() + nx * F * elem + 3 * n * F * elem + g
         if self.shared:
@@ -494,13 +495,20 @@ def build_ngram_map(g: CSRGraph, node_keys: torch.Tensor, alphabet: str, n: int,
               "pg_ngram_mplan_map_f32")
     rmask = resid[:g.nnz].bool()
     rows = torch.repeat_interleave(torch.arange(g.n_rows, device=dev), g.rowptr[1:] - g.rowptr[:-1])
-    res_rows = rows[rmask]
-    res_rowptr = _rowptr(res_rows, g.n_rows)
     res_edges = g.edges3[rmask].contiguous()  # CSR order kept: ascending column within a row
-    has_res = (res_rowptr[1:] - res_rowptr[:-1]) > 0
-    rows_off = torch.nonzero(~on).view(-1).to(torch.int32)
-    rows_acc = torch.nonzero(on & has_res).view(-1).to(torch.int32)
-    return NgramMap(K, n, mplan, gmap, ginv, res_rowptr, res_edges, rows_off, rows_acc, n_grid, int(res_edges.size(0)))
+    cnt = torch.bincount(rows[rmask], minlength=g.n_rows)
+    # listed rows: every node off the grid (even without entries: its Z row is written as 0), and the grid nodes with
+    # residual entries; node order, so the compact CSR is the residual entries in their CSR order
+    listed = (~on) | (cnt > 0)
+    ids = torch.nonzero(listed).view(-1)
+    res_rowptr = torch.zeros(ids.numel() + 1, dtype=torch.int64, device=dev)
+    res_rowptr[1:] = torch.cumsum(cnt[ids], 0)
+    add = on[ids]
+    res_rows = torch.where(add, ids | (1 << 31), ids).to(torch.int64)
+    res_rows = (res_rows - (res_rows >= 2 ** 31).to(torch.int64) * 2 ** 32).to(torch.int32)  # bit 31 as int32 sign
+    n_acc = int(add.sum())
+    return NgramMap(K, n, mplan, gmap, ginv, res_rowptr, res_rows.contiguous(), res_edges, n_grid,
+                    int(res_edges.size(0)), int(ids.numel()) - n_acc, n_acc)
 
 
 def attach_ngram_map(g: CSRGraph, transitions, letters: str = GRID_LETTERS, min_fill: float = 0.5) -> CSRGraph:

@@ -125,19 +125,17 @@ def _map_ok(g: CSRGraph, x: torch.Tensor, fl: int) -> bool:
 
 
 def _map_fwd(lib, g, x, Z, fl, s):
-    """Mapped n-gram forward: the grid part by pg_spmm3_ngram_mid_map_f32, then the residual CSR pass
-    (pg_spmm3_rows_f32) over the off-grid rows (overwrite) and the grid rows with residual entries (accumulate).
+    """Mapped n-gram forward: the grid part by pg_spmm3_ngram_mid_map_f32, then one residual pass
+    (pg_spmm3_resid_f32) over the off-grid rows (overwritten) and the grid rows with residual entries (added to).
     Returns the first non-zero return code (PG_ERR_UNSUPPORTED before anything launched: the caller falls back)."""
     m, F = g.ngram_map, x.size(1)
     rc = lib.pg_spmm3_ngram_mid_map_f32(m.K, m.n, _p(m.mplan), _p(m.gmap), _p(x), x.stride(0), F, _p(Z), Z.stride(0),
                                         fl, s)
     if rc:
         return rc
-    for rows, acc in ((m.rows_off, 0), (m.rows_acc, 1)):
-        if rows.numel():
-            rc = lib.pg_spmm3_rows_f32(rows.numel(), _p(m.res_rowptr), _p(rows), _p(m.res_edges), _p(x), x.stride(0),
-                                       F, _p(Z), Z.stride(0), acc, fl, s)
-            check(rc, "pg_spmm3_rows_f32")
+    if m.res_rows.numel():
+        check(lib.pg_spmm3_resid_f32(m.res_rows.numel(), _p(m.res_rowptr), _p(m.res_rows), _p(m.res_edges), _p(x),
+                                     x.stride(0), F, _p(Z), Z.stride(0), fl, s), "pg_spmm3_resid_f32")
     return 0
 
 

@@ -1,5 +1,5 @@
 """Builder-produced graphs on the middle-tile kernel (graph.build_ngram_map / pg_spmm3_ngram_mid_map_f32 + the residual
-CSR pass pg_spmm3_rows_f32).
+pass pg_spmm3_resid_f32).
 
 run_graph_builder.py pads every sequence (data_builder.py:29-35) and numbers the n-grams PRESENT by sorted-string rank
 (:164-173), so a real level-n graph is not the complete 20^n grid: the mapped plan runs its grid part on the tile
@@ -53,7 +53,7 @@ def test_fasta3_golden_layer_on_mapped_plan(pkg, cuda, monkeypatch):
     g = pkg.build_propagation_csr(N, fx["src"], fx["dst"], fx["cnt"], device=cuda, transitions=tr)
     assert g.ngram is None and g.ngram_map is not None
     m = g.ngram_map
-    assert m.n_grid == N and m.rows_off.numel() == 0 and m.nnz_res == 0  # all on the grid, all in grid slots
+    assert m.n_grid == N and m.n_off == 0 and m.nnz_res == 0  # all on the grid, all in grid slots
     lib = ops.load_library()
     hits = _count(monkeypatch, lib, "pg_spmm3_ngram_mid_map_f32")
     layer = pkg.DirectGCNLayer(*(int(v) for v in fx["L_cfg"][:3]), bool(fx["L_cfg"][3]))
@@ -82,7 +82,7 @@ def test_padded_builder_graph_small(pkg, cuda, monkeypatch, n, nseq, rare, F):
     assert g.ngram is None
     g.ngram_map = gr.build_ngram_map(g, tr.node_keys, tr.alphabet, n, min_fill=0.0)
     m = g.ngram_map
-    assert m is not None and m.rows_off.numel() > 0 and m.nnz_res > 0
+    assert m is not None and m.n_off > 0 and m.n_acc > 0 and m.nnz_res > 0
     # every node string on the grid maps to its base-20 number; the others are off
     strings = tr.node_strings()
     ginv = m.ginv.cpu().numpy()
@@ -98,16 +98,16 @@ def test_padded_builder_graph_small(pkg, cuda, monkeypatch, n, nseq, rare, F):
     x = torch.randn(tr.num_nodes, F, generator=torch.Generator().manual_seed(3)).to(cuda)
     lib = ops.load_library()
     hits = _count(monkeypatch, lib, "pg_spmm3_ngram_mid_map_f32")
-    res = _count(monkeypatch, lib, "pg_spmm3_rows_f32")
+    res = _count(monkeypatch, lib, "pg_spmm3_resid_f32")
     Z = ops.spmm3(g, x).cpu()
-    assert hits and len(res) == 1 + (m.rows_acc.numel() > 0)
+    assert hits and len(res) == 1
     Zc = ops.spmm3(g, x, flags=_csr_flags()).cpu()
     ei, w = _oracle_mats(g)
     for j in range(3):
         ref = oc.propagate(ei, x.cpu(), w[j])
         assert torch.equal(Zc[:, j * F:(j + 1) * F], ref), j
         assert_close(Z[:, j * F:(j + 1) * F], ref, f"mapped propagation {j} (n={n})")
-    assert int(m.res_rowptr[-1]) == m.nnz_res
+    assert int(m.res_rowptr[-1]) == m.nnz_res and m.res_rows.numel() == m.n_off + m.n_acc
 
 
 def test_padded_fasta_4gram_at_size(pkg, cuda, monkeypatch):
@@ -123,7 +123,7 @@ def test_padded_fasta_4gram_at_size(pkg, cuda, monkeypatch):
                                   transitions=tr)
     assert g.ngram is None and g.ngram_map is not None
     m = g.ngram_map
-    assert m.n_grid > 0.9 * N and m.rows_off.numel() > 0
+    assert m.n_grid > 0.9 * N and m.n_off > 0
     F = 128
     torch.manual_seed(0)
     layer = pkg.DirectGCNLayer(F, F, N, True)

@@ -6,7 +6,8 @@ tests/test_gpu_rccl.py runs the RCCL branch itself). Every rank propagates its m
 
 Each rank checks its own share against the single-GPU step on the same model and inputs (computed in the rank's
 process before the trainer runs): the global loss, every replicated parameter gradient after the all-reduce and the
-owned rows of every per-node parameter gradient. fp32: |d| <= 1e-4 max|ref| + 1e-4 |ref| (the kernels sum in
+owned rows of every per-node parameter gradient (plus the L2 term 2 lam p, which the trainer's train.Adam folds
+into its update instead of the gradient). fp32: |d| <= 1e-4 max|ref| + 1e-4 |ref| (the kernels sum in
 other orders than the single-GPU step's); bf16 mode against the fp32 step (as test_gpu_configs' config-5 test):
 loss within 2 %, gradient cosine > 0.99. Reference loop: protgram_directgcn_trainer.py:76-108; dims: config.py:63."""
 import os
@@ -62,6 +63,8 @@ def _worker(rank, world, port, out_q, bf16):
         if bf16:
             m.compute_dtype = torch.bfloat16
         tr = shard.MiddleTrainer(m, mp_, l2_lambda=lam)
+        # pre-step values (the model's full per-node parameters are not written by the trainer: its leaves are)
+        pre_dense = {k: p.detach().float().clone() for k, p in m.named_parameters()}
         hits = []
         real = ops.spmm3_middles
         ops.spmm3_middles = lambda *a, **k: hits.append(1) or real(*a, **k)
@@ -85,7 +88,8 @@ def _worker(rank, world, port, out_q, bf16):
             if gg is None:
                 bad.append((name, "no grad"))
                 continue
-            gg = gg.detach().float()
+            pre = p.detach().float()[own] if shard._is_node_param(name, p, N) else pre_dense[name]
+            gg = gg.detach().float() + 2 * lam * pre  # train.Adam folds the L2 gradient into its update
             if bf16:
                 cos = float((gg * r).sum() / (gg.norm() * r.norm() + 1e-30))
                 if cos < 0.99:

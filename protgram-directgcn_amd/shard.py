@@ -1167,6 +1167,15 @@ class TorchComm:
         else:
             dist.all_reduce(t, group=self.group)
 
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor):
+        """out [world * rows, ...] <- every rank's t [rows, ...], rank-major."""
+        if t.is_cuda and dist.get_backend(self.group) == "gloo":
+            o = out.new_empty(out.shape, device="cpu")
+            dist.all_gather_into_tensor(o, t.cpu(), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, t, group=self.group)
+
 
 @dataclass
 class MiddleTranspose:
@@ -1401,3 +1410,27 @@ class MiddleTrainer:
         for conv, d in zip(self.model.convs, self.own):
             for name, leaf in d.items():
                 getattr(conv, name).data.index_copy_(0, self.mp.own.to(leaf.device), leaf.data)
+
+    @torch.no_grad()
+    def gather(self):
+        """Every rank's per-node parameters whole on every rank (checkpointing): the owned rows of all ranks,
+        all-gathered (padded to the largest share) and written at their global rows."""
+        self.sync_model()
+        mp = self.mp
+        if mp.world == 1:
+            return
+        Kn2 = mp.K ** (mp.ngram - 2)
+        dev = mp.own.device
+        rows = [_middle_rows(mp.K, mp.ngram, a, b, dev) for a, b in middle_bounds(Kn2, mp.world)]
+        most = max(r.numel() for r in rows)
+        for conv, d in zip(self.model.convs, self.own):
+            for name, leaf in d.items():
+                full = getattr(conv, name).data
+                flat = leaf.data.reshape(leaf.size(0), -1)
+                pad = flat.new_zeros(most, flat.size(1))
+                pad[:flat.size(0)] = flat
+                out = pad.new_empty(mp.world * most, flat.size(1))
+                self.comm.all_gather(out, pad)
+                fv = full.view(full.size(0), -1)
+                for q, r in enumerate(rows):
+                    fv.index_copy_(0, r.to(full.device), out[q * most:q * most + r.numel()])

@@ -284,13 +284,10 @@ def _mid_train_worker(rank, world, port, out_q, chunks, bf16):
                 err = float((gg - r).abs().max())
                 if err > 2e-5 * float(r.abs().max()) + 1e-6:
                     bad.append((name, "grad", err))
-        tr.sync_model()
+        tr.gather()  # every rank's rows, on every rank
         if not bf16:
             for name, p in model.named_parameters():
-                got, want = p.detach(), ref[name].detach()
-                if shard._is_node_param(name, p, N):
-                    got, want = got[mp_.own], want[mp_.own]
-                err = float((got - want).abs().max())
+                err = float((p.detach() - ref[name].detach()).abs().max())
                 if err > 2e-5:
                     bad.append(("param " + name, err))
         out_q.put((rank, mp_.n_own, not bad, str(bad[:4])))

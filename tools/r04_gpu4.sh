@@ -13,3 +13,5 @@ cd $GRAFT_REPO_ROOT && timeout -k 10 300 python -u bench.py --graph fasta --no-c
 cut -c1-300 gpurun_out/r04_fasta3.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_mtp -o k --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/middle_train_probe.py --ranks 0 --reps 10 > $GRAFT_REPO_ROOT/gpurun_out/r04_mtp2.json 2> $GRAFT_REPO_ROOT/gpurun_out/r04_mtp2.err || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r04_mtp2.err; exit 1; }
 head -25 $(find $GRAFT_REPO_ROOT/gpurun_out/prof_mtp -name "*kernel_stats.csv" | head -1) | cut -c1-160
+cd $GRAFT_REPO_ROOT && timeout -k 10 300 python -u tools/map_probe.py > gpurun_out/r04_mapprobe.json 2> gpurun_out/r04_mapprobe.err || { tail -20 gpurun_out/r04_mapprobe.err; exit 1; }
+cat gpurun_out/r04_mapprobe.json

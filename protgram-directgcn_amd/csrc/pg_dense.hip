@@ -76,8 +76,22 @@ struct DenseP {
 // 2: no Y stores, 3: no A DMA, 4: no constant / residual DMA). Results are garbage in those runs.
 #ifdef PG_DENSE_EXP
 #define DEXP(bit) ((p.exp >> (bit)) & 1)
+// per-iteration s_memtime stamps of dense_x3p_kernel (tools/dense_exp.py --stamps): blocks < DST_BLOCKS, waves 0 and
+// 4 (the MFMA-first and the split-first wave of SIMD 0), iterations < DST_IT, points < DST_PT; vector stores into a
+// buffer of their own (no kernel output depends on them)
+constexpr int DST_BLOCKS = 64, DST_IT = 48, DST_PT = 8;
+__device__ unsigned long long* g_dense_stamps = nullptr;
+#define DSTAMP(it, pt)                                                                                            \
+    do {                                                                                                          \
+        unsigned long long* st_ = g_dense_stamps;                                                                 \
+        if (st_ && lane == 0 && (wave == 0 || wave == 4) && blockIdx.x < DST_BLOCKS && (it) < DST_IT)             \
+            st_[((blockIdx.x * 2 + (wave >> 2)) * DST_IT + (it)) * DST_PT + (pt)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define DEXP(bit) 0
+#define DSTAMP(it, pt) \
+    do {               \
+    } while (0)
 #endif
 
 // global n-gram row of middle-major row m (K = 20: 400 rows per middle); see DenseP::map_*
@@ -963,9 +977,12 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     bool y_pending = false;  // the previous epilogue left exactly one Y store per thread in flight
     for (int64_t i = 0; i <= ntl && ntl > 0; ++i) {
         const int ab = (int)(i & 1);
+        [[maybe_unused]] const int si = (int)i;
+        DSTAMP(si, 0);
         if (y_pending) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // A(i+1), G(i+1) have landed
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();  // B1: A(i+1) and split(i) visible; epilogue(i-2) done with Es / Cs / Rs; As[ab ^ 1] free
+        DSTAMP(si, 1);
         if (i >= 1) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) lds_stf(&Es[(4 * kg + e) * ELD + col], acc[e]);
@@ -973,18 +990,24 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         issue_CR(tile_of(i - 1));
         issue_A(tile_of(i + 2), ab ? Af1 : Af0);  // Af[(i + 2) & 1] = Af[ab]: split(i) is done with it
         if (wave == 0) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
+        DSTAMP(si, 2);
         const bool do_mfma = i < ntl, do_split = i + 1 < ntl;
         if (mfma_first) {
             if (do_mfma) mfma_tile(ab);
+            DSTAMP(si, 3);
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
         } else {
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
+            DSTAMP(si, 3);
             if (do_mfma) mfma_tile(ab);
         }
+        DSTAMP(si, 4);
         // CR(i-1) has landed: younger are A(i+2) (+ G(i+2) on wave 0)
         if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + NG) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+        DSTAMP(si, 5);
         lds_barrier();  // B2: Es and Cs / Rs visible
+        DSTAMP(si, 6);
         y_pending = false;
         if (i >= 1) {
             const int64_t m0 = tile_of(i - 1) * BM;
@@ -1015,6 +1038,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                 }
             }
         }
+        DSTAMP(si, 7);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles' DMA must land before the LDS is freed
 }
@@ -1205,6 +1229,13 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
 int pg_directgcn_dense_f32(const pg_layer_args_t* a, const float* packed, uint32_t flags, void* stream) {
     return dense_launch(a, packed, flags, nullptr, stream);
 }
+
+#ifdef PG_DENSE_EXP
+// diagnostics library only (tools/dense_exp.py --stamps): the stamp buffer of dense_x3p_kernel (NULL: off)
+int pg_dense_set_stamps(unsigned long long* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dense_stamps), &buf, sizeof(buf)) == hipSuccess ? PG_OK : PG_ERR_HIP;
+}
+#endif
 
 int pg_directgcn_dense_ngram_rows_f32(const pg_layer_args_t* a, const float* packed, int64_t Kn1, int64_t m0,
                                       int32_t map_res, int32_t map_y, uint32_t flags, void* stream) {

@@ -5,6 +5,7 @@ results are garbage in those runs), and times the bench's layer-1 dense launch a
 phases skipped (min of interleaved rounds, HIP events).
 usage: python tools/dense_exp.py --build (in the container), then python tools/dense_exp.py [n=4] [reps=20]"""
 import ctypes
+import json
 import os
 import subprocess
 import sys
@@ -73,6 +74,41 @@ def timeit(exp):
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
 
+
+if "--stamps" in sys.argv:  # per-iteration cycle breakdown of waves 0 (MFMA first) and 4 (split first)
+    import numpy as np
+    NB, NIT, NPT = 64, 48, 8
+    buf = torch.zeros(NB * 2 * NIT * NPT, dtype=torch.int64, device=dev)
+    lib.pg_dense_set_stamps.argtypes = [ctypes.c_void_p]
+    for _ in range(20):
+        run(0)
+    torch.cuda.synchronize()
+    assert lib.pg_dense_set_stamps(ctypes.c_void_p(buf.data_ptr())) == 0
+    run(0)
+    torch.cuda.synchronize()
+    lib.pg_dense_set_stamps(None)
+    t = buf.view(NB, 2, NIT, NPT).cpu().numpy().astype(np.float64)
+    names = ["wait_A+B1", "issue_dma", "first_phase", "second_phase", "wait_CR", "B2", "epilogue", "to_next_top"]
+    res = {}
+    for w, wn in ((0, "wave0_mfma_first"), (1, "wave4_split_first")):
+        seg = {}
+        v = t[:, w]
+        its = slice(2, 36)
+        for k in range(NPT - 1):
+            d = v[:, its, k + 1] - v[:, its, k]
+            seg[names[k + 1 if k else 0]] = float(np.median(d))
+        seg["wait_A+B1"] = float(np.median(v[:, its, 1] - v[:, its, 0]))
+        seg["issue_dma"] = float(np.median(v[:, its, 2] - v[:, its, 1]))
+        seg["first_phase"] = float(np.median(v[:, its, 3] - v[:, its, 2]))
+        seg["second_phase"] = float(np.median(v[:, its, 4] - v[:, its, 3]))
+        seg["wait_CR"] = float(np.median(v[:, its, 5] - v[:, its, 4]))
+        seg["B2"] = float(np.median(v[:, its, 6] - v[:, its, 5]))
+        seg["epilogue"] = float(np.median(v[:, its, 7] - v[:, its, 6]))
+        seg["iteration"] = float(np.median(v[:, 3:37, 0] - v[:, 2:36, 0]))
+        res[wn] = {k: round(x, 1) for k, x in seg.items()}
+    print("stamps (median cycles per iteration, s_memtime ticks, iterations 2..35 of blocks 0..63):",
+          json.dumps(res) if "json" in globals() else res)
+    sys.exit(0)
 
 run(0)
 ref = ops.layer_dense(Z, prm, 0, constant=layer.constant, res_x=x, act=True, pregated=pregated)

@@ -54,7 +54,7 @@ class TensorList:
                 desc[i, k] = f[i].data_ptr()
             desc[i, -1] = x.numel()
             chunks[i + 1] = chunks[i] + lib.pg_multi_chunks(x.numel())
-        self.fields = fields  # keep the tensors alive while the descriptors may be in use
+        self.fields = fields  # keep the tensors alive while the descriptors may be in use (dropped when cached)
         self.desc = _upload(desc, dev)
         self.chunk_ptr = _upload(chunks, dev)
         self.nchunks = int(chunks[-1])
@@ -130,6 +130,21 @@ class Adam(torch.optim.Optimizer):
         if lr < 0 or eps < 0 or not (0 <= betas[0] < 1 and 0 <= betas[1] < 1) or weight_decay < 0:
             raise ValueError("invalid Adam hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        # device descriptor lists by the (address, numel) of every field: a step whose parameters, gradients and
+        # moments sit where they sat before (persistent gradient buffers, or the caching allocator handing the same
+        # blocks back) reuses the uploaded descriptors -- no host-side table and no host-to-device copy per step
+        self._tl_cache: dict = {}
+
+    def _tensor_list(self, fields) -> TensorList:
+        key = tuple((t.data_ptr(), t.numel()) for f in fields for t in f)
+        tl = self._tl_cache.get(key)
+        if tl is None:
+            tl = TensorList(*fields)
+            tl.fields = None  # the descriptors hold addresses only; the key guarantees they are current
+            if len(self._tl_cache) >= 16:
+                self._tl_cache.pop(next(iter(self._tl_cache)))
+            self._tl_cache[key] = tl
+        return tl
 
     def _cohorts(self, ps: List[torch.Tensor]) -> List[tuple]:
         """Group the parameters being stepped by their step counter (one pg_adam_f32 launch per counter).
@@ -207,8 +222,8 @@ class Adam(torch.optim.Optimizer):
             fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
             for members, step in self._cohorts(ps):
                 grads = [p.grad.contiguous() for p in members]
-                tl = TensorList(members, grads, [self.state[p]["exp_avg"] for p in members],
-                                [self.state[p]["exp_avg_sq"] for p in members])
+                tl = self._tensor_list((members, grads, [self.state[p]["exp_avg"] for p in members],
+                                        [self.state[p]["exp_avg_sq"] for p in members]))
                 if want_sq:
                     sq_parts.append(tl.partial[:tl.nchunks])
                 check(lib.pg_adam_f32(len(members), ctypes.c_void_p(tl.desc.data_ptr()),

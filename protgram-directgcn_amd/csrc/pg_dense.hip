@@ -769,7 +769,11 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
 // LDS: Af 2 x 24 KB, As 2 x 36 KB, Cs/Rs 16 KB, Es 8.3 KB, gate inputs 4 x 512 B, bias sums 2 KB.
 __device__ __forceinline__ int a_unit16(int s, int r, int g) { return 64 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
 
-template <bool PRE>
+// IL (PG_FLAG_DENSE_DMA_IL): the A and gate-input LDS-DMA pieces of tile i + 2 are issued between the k-steps of
+// the wave's MFMA phase instead of all at the top of the iteration (stamps: issuing the five or seven pieces at once
+// took ~1,750 of an iteration's ~7,300 cycles, the memory pipeline pushing back); the constant / residual pieces stay
+// first, so the counted vmcnt waits are unchanged.
+template <bool PRE, bool IL>
 __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     constexpr int F_IN = 128, K = 384;
     constexpr int CH = K / 4;    // fp32 16-B chunks per row
@@ -848,22 +852,23 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     const bool id_res = p.res_x && !p.proj_res;
     auto tile_of = [&](int64_t kt) { return lo + max((int64_t)0, min(kt, ntl - 1)) * step; };
 
-    auto issue_A = [&](int64_t tile, float* Ad) {
+    auto issue_A_piece = [&](int64_t tile, float* Ad, int i) {
         if (DEXP(3)) return;
         const int64_t m0 = tile * BM;
         const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
         const float* zb = p.Z + m0 * p.ldz;
         int ln = lane;
         asm volatile("" : "+v"(ln));
+        const int idx = (wave * NI + i) * 64 + ln;
+        const int r = idx / CH, pos = idx - r * CH;
+        const int k = 4 * (pos ^ r);
+        const int rr = min(r, rmax);
+        if (p.nt_a) glds16nt(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
+        else glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
+    };
+    auto issue_A = [&](int64_t tile, float* Ad) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int idx = (wave * NI + i) * 64 + ln;
-            const int r = idx / CH, pos = idx - r * CH;
-            const int k = 4 * (pos ^ r);
-            const int rr = min(r, rmax);
-            if (p.nt_a) glds16nt(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
-            else glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
-        }
+        for (int i = 0; i < NI; ++i) issue_A_piece(tile, Ad, i);
     };
     // gate inputs of a tile (wave 0): piece 0 = C_in | C_out | C_dir | C_und (16 lanes each), piece 1 = C_all
     auto issue_G = [&](int64_t tile, int slot) {
@@ -939,13 +944,20 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         }
     };
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    auto mfma_tile = [&](int ab) {
+    // IL: the next-but-one tile's A pieces (after k-steps 2, 5, 8) and gate inputs (wave 0, after k-step 10)
+    auto mfma_tile = [&](int ab, int64_t a_tile, float* a_dst, int g_slot, bool issue) {
         const uint4* a0 = &As[ab][0][a_unit16(0, lc, kg)];
         const uint4* a1 = &As[ab][1][a_unit16(0, lc, kg)];
         const uint4* a2 = &As[ab][2][a_unit16(0, lc, kg)];
         uint4 op[2][3];
         acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (DEXP(0)) return;
+        if (DEXP(0)) {
+            if (IL && issue) {
+                issue_A(a_tile, a_dst);
+                if (wave == 0) issue_G(a_tile, g_slot);
+            }
+            return;
+        }
         op[0][0] = a0[0];
         op[0][1] = a1[0];
         op[0][2] = a2[0];
@@ -963,6 +975,10 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
             acc = mfma_bf(x1, w0[s], acc);
             acc = mfma_bf(x0, w1[s], acc);
             acc = mfma_bf(x0, w0[s], acc);
+            if constexpr (IL) {
+                if (issue && (s == 2 || s == 5 || s == 8)) issue_A_piece(a_tile, a_dst, s / 3);
+                if (issue && s == 10 && wave == 0) issue_G(a_tile, g_slot);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -995,18 +1011,23 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
             for (int e = 0; e < 4; ++e) lds_stf(&Es[(4 * kg + e) * ELD + col], acc[e]);
         }
         issue_CR(tile_of(i - 1));
-        issue_A(tile_of(i + 2), ab ? Af1 : Af0);  // Af[(i + 2) & 1] = Af[ab]: split(i) is done with it
-        if (wave == 0) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
-        DSTAMP(si, 2);
+        const int64_t a_tile = tile_of(i + 2);
+        float* const a_dst = ab ? Af1 : Af0;  // Af[(i + 2) & 1] = Af[ab]: split(i) is done with it
+        const int g_slot = (int)((i + 2) & 3);
         const bool do_mfma = i < ntl, do_split = i + 1 < ntl;
+        if (!IL || !do_mfma) {  // IL: the MFMA phase issues them (or here, past the last tile)
+            issue_A(a_tile, a_dst);
+            if (wave == 0) issue_G(a_tile, g_slot);
+        }
+        DSTAMP(si, 2);
         if (mfma_first) {
-            if (do_mfma) mfma_tile(ab);
+            if (do_mfma) mfma_tile(ab, a_tile, a_dst, g_slot, IL);
             DSTAMP(si, 3);
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
         } else {
             if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
             DSTAMP(si, 3);
-            if (do_mfma) mfma_tile(ab);
+            if (do_mfma) mfma_tile(ab, a_tile, a_dst, g_slot, IL);
         }
         DSTAMP(si, 4);
         // CR(i-1) has landed: younger are A(i+2) (+ G(i+2) on wave 0)
@@ -1048,262 +1069,6 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
         DSTAMP(si, 7);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles' DMA must land before the LDS is freed
-}
-
-// Direct-epilogue variant of dense_x3p_kernel (PG_FLAG_DENSE_DIRECT; opt-in while measured): the same tiles, splits,
-// products and rounding steps (epi_sum), but every wave finishes its own 16 x 16 output block straight from the MFMA
-// accumulators (lane: rows 4 kg .. 4 kg + 3 of column 16 w + lc, four 4-B stores), so the accumulator hand-off
-// through LDS and its barrier go away (one barrier per tile), and the constant / residual rows of tile t + 1 are
-// fetched during tile t into a second buffer (the LDS the hand-off used pays for it): their DMA latency is covered
-// by a whole iteration instead of one compute phase.
-// LDS: Af 2 x 24 KB, As 2 x 36 KB, Cs/Rs 2 x 16 KB, gate inputs 4 x 512 B, bias sums 2 KB = 156 KB.
-template <bool PRE>
-__global__ __launch_bounds__(512) void dense_x3d_kernel(DenseP p) {
-    constexpr int F_IN = 128, K = 384;
-    constexpr int CH = K / 4;
-    constexpr int NU = K / 8;
-    constexpr int NS = K / 32;
-    constexpr int BM = 16;
-    constexpr int NI = BM * CH / 64 / 8;
-    constexpr int NG = 2;
-    static_assert(BM * CH % 512 == 0 && NI == 3, "tile shape");
-    __shared__ __attribute__((aligned(16))) float Af0[BM * K];
-    __shared__ __attribute__((aligned(16))) float Af1[BM * K];
-    __shared__ __attribute__((aligned(16))) uint4 As[2][3][BM * NU];
-    __shared__ __attribute__((aligned(16))) float Cs0[BM * 128];
-    __shared__ __attribute__((aligned(16))) float Cs1[BM * 128];
-    __shared__ __attribute__((aligned(16))) float Rs0[BM * 128];
-    __shared__ __attribute__((aligned(16))) float Rs1[BM * 128];
-    __shared__ __attribute__((aligned(16))) float Gi[4][8][BM];
-    __shared__ __attribute__((aligned(16))) float Bs[4][128];
-
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
-    const int lc = lane & 15, kg = lane >> 4;
-    const int col = 16 * wave + lc;
-    const bool mfma_first = wave < 4;
-    const int64_t T = (p.M + BM - 1) / BM;
-    {
-        const int q = tid >> 7, n = tid & 127;
-        float bv = 0.f;
-        if (p.rawW) {
-            if (q < 3) bv = q == 0 ? p.bm0[n] + p.bs0[n] : q == 1 ? p.bm1[n] + p.bs1[n] : p.bm2[n] + p.bs2[n];
-        } else if (q < 3 || p.proj_res) {
-            bv = p.bsum[q * p.F_out + n];
-        }
-        Bs[q][n] = bv;
-    }
-    const int nb = gridDim.x, b = blockIdx.x;
-    int64_t ntl, lo, step;
-    if ((nb & 7) == 0 && nb >= 8) {
-        const int x = b & 7, i = b >> 3, bpx = nb >> 3;
-        const int64_t xlo = T * x / 8, xhi = T * (x + 1) / 8;
-        ntl = (xhi - xlo - i + bpx - 1) / bpx;
-        lo = xlo + i;
-        step = bpx;
-    } else {
-        ntl = (T - b + nb - 1) / nb;
-        lo = b;
-        step = nb;
-    }
-    if (ntl < 0) ntl = 0;
-
-    uint4 w0[NS], w1[NS], w2[NS];
-    if (p.rawW) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const float* wq = s < 4 ? p.Wq0 : s < 8 ? p.Wq1 : p.Wq2;
-            const int64_t o = (int64_t)col * F_IN + (32 * s) % F_IN + 4 * kg;
-            const float4 a0 = ld4(wq + o), a1 = ld4(wq + o + 16), h0 = ld4(p.Wsh + o), h1 = ld4(p.Wsh + o + 16);
-            const float v[8] = {a0.x + h0.x, a0.y + h0.y, a0.z + h0.z, a0.w + h0.w,
-                                a1.x + h1.x, a1.y + h1.y, a1.z + h1.z, a1.w + h1.w};
-            split8(v, w0[s], w1[s], w2[s]);
-        }
-    } else {
-        const float* src = p.Bp + (int64_t)col * K + 4 * kg;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const float4 x0 = ld4(src + 32 * s), x1 = ld4(src + 32 * s + 16);
-            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            split8(v, w0[s], w1[s], w2[s]);
-        }
-    }
-    const bool has_const = p.constant && p.gate_mode == PG_GATES_VECTOR;
-    const bool id_res = p.res_x && !p.proj_res;
-    auto tile_of = [&](int64_t kt) { return lo + max((int64_t)0, min(kt, ntl - 1)) * step; };
-
-    auto issue_A = [&](int64_t tile, float* Ad) {
-        const int64_t m0 = tile * BM;
-        const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
-        const float* zb = p.Z + m0 * p.ldz;
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const int idx = (wave * NI + i) * 64 + ln;
-            const int r = idx / CH, pos = idx - r * CH;
-            const int k = 4 * (pos ^ r);
-            const int rr = min(r, rmax);
-            if (p.nt_a) glds16nt(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
-            else glds16(zb + (rr * (int)p.ldz + k), Ad + (wave * NI + i) * 256);
-        }
-    };
-    auto issue_G = [&](int64_t tile, int slot) {
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int64_t r = p.gate_mode == PG_GATES_SCALAR ? 0 : min(tile * BM + (ln & 15), p.M - 1);
-        const float* c0 = p.C_in;
-        const float* c1 = p.C_out;
-        const float* c2 = p.C_dir;
-        const float* c3 = p.C_und;
-        const float* c4 = p.C_all;
-        asm volatile("" : "+s"(c0), "+s"(c1), "+s"(c2), "+s"(c3), "+s"(c4));
-        const int q = ln >> 4;
-        const float* cq = q == 0 ? c0 : q == 1 ? c1 : q == 2 ? c2 : c3;
-        glds4(cq + r, &Gi[slot][0][0]);
-        glds4(c4 + r, &Gi[slot][4][0]);
-    };
-    auto issue_CR = [&](int64_t tile, float* Cd, float* Rd) {  // wave w: rows 2w, 2w + 1
-        const int64_t m0 = tile * BM;
-        const int rmax = (int)min((int64_t)(BM - 1), p.M - 1 - m0);
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const int rr = min(2 * wave + (ln >> 5), rmax);
-        const float* cb = has_const ? p.constant + m0 * p.ld_const + (rr * (int)p.ld_const) : p.Z + m0 * p.ldz;
-        const float* rb = !id_res    ? p.Z + m0 * p.ldz
-                          : p.map_res ? p.res_x + ngram_row(p, m0 + rr) * p.ld_res
-                                      : p.res_x + m0 * p.ld_res + (rr * (int)p.ld_res);
-        if (p.nt_a) glds16nt(cb + 4 * (ln & 31), Cd + wave * 256);
-        else glds16(cb + 4 * (ln & 31), Cd + wave * 256);
-        glds16(rb + 4 * (ln & 31), Rd + wave * 256);
-    };
-    auto gates = [&](int slot, int r, float& s0, float& s1, float& s2) {
-        float c[5];
-        lds_gates5<BM * 4>(&Gi[slot][0][r], c);
-        const float cad = c[4] * c[2];
-        s0 = cad * c[0];
-        s1 = cad * c[1];
-        s2 = c[4] * c[3];
-    };
-    auto split_tile = [&](const float* Af, int ab, int gslot) {
-        const int r = tid & 15;
-        const bool two = tid + 512 < BM * NU;
-        const int u0 = tid >> 4, u1 = u0 + 32;
-        const int c00 = 8 * (u0 >> 2) + (u0 & 3), c10 = 8 * (u1 >> 2) + (u1 & 3);
-        float4 x[4];
-        if (two) lds_ld4x4(&Af[r * K + 4 * (c00 ^ r)], &Af[r * K + 4 * ((c00 + 4) ^ r)], &Af[r * K + 4 * (c10 ^ r)],
-                           &Af[r * K + 4 * ((c10 + 4) ^ r)], x);
-        else lds_ld4x2(&Af[r * K + 4 * (c00 ^ r)], &Af[r * K + 4 * ((c00 + 4) ^ r)], x[0], x[1]);
-        float sg[3] = {1.f, 1.f, 1.f};
-        if (!PRE) gates(gslot, r, sg[0], sg[1], sg[2]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            if (i == 1 && !two) break;
-            const int u = i ? u1 : u0;
-            const int s = u >> 2, g = u & 3;
-            const float4 a = x[2 * i], c = x[2 * i + 1];
-            float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-            if (!PRE) {
-                const float sc = sg[(32 * s) / F_IN];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = __fmul_rn(v[e], sc);
-            }
-            uint4 s0, s1, s2;
-            split8(v, s0, s1, s2);
-            const int pos = a_unit16(s, r, g);
-            lds_st16(&As[ab][0][pos], s0);
-            lds_st16(&As[ab][1][pos], s1);
-            lds_st16(&As[ab][2][pos], s2);
-        }
-    };
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    auto mfma_tile = [&](int ab) {
-        const uint4* a0 = &As[ab][0][a_unit16(0, lc, kg)];
-        const uint4* a1 = &As[ab][1][a_unit16(0, lc, kg)];
-        const uint4* a2 = &As[ab][2][a_unit16(0, lc, kg)];
-        uint4 op[2][3];
-        acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        op[0][0] = a0[0];
-        op[0][1] = a1[0];
-        op[0][2] = a2[0];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            if (s + 1 < NS) {
-                op[(s + 1) & 1][0] = a0[64 * (s + 1)];
-                op[(s + 1) & 1][1] = a1[64 * (s + 1)];
-                op[(s + 1) & 1][2] = a2[64 * (s + 1)];
-            }
-            const uint4 x0 = op[s & 1][0], x1 = op[s & 1][1], x2 = op[s & 1][2];
-            acc = mfma_bf(x2, w0[s], acc);
-            acc = mfma_bf(x1, w1[s], acc);
-            acc = mfma_bf(x0, w2[s], acc);
-            acc = mfma_bf(x1, w0[s], acc);
-            acc = mfma_bf(x0, w1[s], acc);
-            acc = mfma_bf(x0, w0[s], acc);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-
-    // prologue: CR(0), A(0), G(0), A(1), G(1) in flight; split(0) once A(0) (and CR(0)) have landed
-    if (ntl > 0) {
-        issue_CR(tile_of(0), Cs0, Rs0);
-        issue_A(tile_of(0), Af0);
-        if (wave == 0) issue_G(tile_of(0), 0);
-        issue_A(tile_of(1), Af1);
-        if (wave == 0) issue_G(tile_of(1), 1);
-        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI + NG) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-        lds_barrier();
-        split_tile(Af0, 0, 0);
-    }
-    float bq[4] = {0.f, 0.f, 0.f, 0.f};  // bias sums of this lane's column (segments 0..2, residual projection)
-    if (ntl > 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bq[q] = Bs[q][col];
-    }
-    bool y_pending = false;  // the previous tile's epilogue left exactly 4 Y stores per wave in flight
-    for (int64_t i = 0; i < ntl; ++i) {
-        const int ab = (int)(i & 1);
-        if (y_pending) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // CR(i), A(i+1), G(i+1) have landed
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();  // A(i+1), CR(i), split(i) visible; epilogue(i-1) done with Cs/Rs[(i+1)&1]; As[ab ^ 1] free
-        issue_CR(tile_of(i + 1), ab ? Cs0 : Cs1, ab ? Rs0 : Rs1);
-        issue_A(tile_of(i + 2), ab ? Af1 : Af0);
-        if (wave == 0) issue_G(tile_of(i + 2), (int)((i + 2) & 3));
-        const bool do_split = i + 1 < ntl;
-        if (mfma_first) {
-            mfma_tile(ab);
-            if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
-        } else {
-            if (do_split) split_tile(ab ? Af0 : Af1, ab ^ 1, (int)((i + 1) & 3));
-            mfma_tile(ab);
-        }
-        // epilogue of tile i from the accumulators: rows 4 kg + e, column col
-        const int64_t m0 = tile_of(i) * BM;
-        const float* Cc = ab ? Cs1 : Cs0;
-        const float* Rc = ab ? Rs1 : Rs0;
-        const int gs = (int)(i & 3);
-        const bool full = m0 + BM <= p.M;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * kg + e;
-            if (m0 + r < p.M) {
-                float c[5];
-                lds_gates5<BM * 4>(&Gi[gs][0][r], c);
-                const float cv = has_const ? Cc[r * 128 + col] : 0.f;
-                const float rv = id_res ? Rc[r * 128 + col] : 0.f;
-                const float cad = c[4] * c[2];
-                const float s0 = cad * c[0], s1 = cad * c[1], s2 = c[4] * c[3];
-                const float qv = epi_sum(acc[e], s0, s1, s2, bq[0], bq[1], bq[2], bq[3], cv, rv);
-                const float y = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
-                const int64_t yr = p.map_y ? ngram_row(p, m0 + r) : m0 + r;
-                p.Y[yr * p.ldy + col] = y;
-            }
-        }
-        if (!full) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a partial tile issued fewer stores
-        y_pending = full;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ __launch_bounds__(256) void pack_kernel(int F_in, int F_out, int K, const float* W0, const float* W1,
@@ -1459,13 +1224,13 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
                 return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights must be 16-B aligned");
             const int64_t T16 = (a->M + 15) / 16;
             const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
-            if (flags & PG_FLAG_DENSE_DIRECT) {
-                if (p.pregated) hipLaunchKernelGGL((dense_x3d_kernel<true>), dim3(g16), dim3(512), 0, s, p);
-                else hipLaunchKernelGGL((dense_x3d_kernel<false>), dim3(g16), dim3(512), 0, s, p);
-            } else if (p.pregated) {
-                hipLaunchKernelGGL((dense_x3p_kernel<true>), dim3(g16), dim3(512), 0, s, p);
+            const bool il = (flags & PG_FLAG_DENSE_DMA_IL) != 0;
+            if (p.pregated) {
+                if (il) hipLaunchKernelGGL((dense_x3p_kernel<true, true>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<true, false>), dim3(g16), dim3(512), 0, s, p);
             } else {
-                hipLaunchKernelGGL((dense_x3p_kernel<false>), dim3(g16), dim3(512), 0, s, p);
+                if (il) hipLaunchKernelGGL((dense_x3p_kernel<false, true>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<false, false>), dim3(g16), dim3(512), 0, s, p);
             }
         } else {
             if (p.rawW)

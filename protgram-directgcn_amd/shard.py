@@ -1241,12 +1241,13 @@ def reverse_exchange(mp: MiddlePartition, dX: torch.Tensor, comm) -> torch.Tenso
         comm.all_to_all(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_send[c], mp.chunk_recv[c])
         s0, r0 = s0 + ns, r0 + nr
     out = torch.zeros(mp.n_own, F_, dtype=torch.promote_types(dX.dtype, torch.float32), device=dX.device)
+    recv = recv.to(out.dtype)  # one widening pass (bf16 mode), then the per-source adds
     off = 0
     for c in range(mp.chunks):
         for q in range(len(mp.chunk_send[c])):
             k = mp.chunk_send[c][q]
             if k:
-                out.index_add_(0, mp.send_pos[off:off + k], recv[off:off + k].to(out.dtype))
+                out.index_add_(0, mp.send_pos[off:off + k], recv[off:off + k])
             off += k
     return out
 
@@ -1297,10 +1298,19 @@ class MiddleTrainer:
     model's full per-node parameters (rows owned elsewhere stay stale on this rank, as with ShardedTrainer)."""
 
     def __init__(self, model, mp: MiddlePartition, lr: float = 1e-3, l2_lambda: float = 1e-7, comm=None,
-                 optimizer_factory=None, **adam_kw):
+                 optimizer_factory=None, graphs: bool = False, **adam_kw):
         from . import train
         self.model, self.mp, self.l2_lambda = model, mp, float(l2_lambda)
         self.comm = comm if comm is not None else TorchComm()
+        # graphs: after WARM eager steps the whole step (forward, backward, collectives, optimizer) is captured once as
+        # a HIP graph and replayed: at a rank's share of the graph the eager step is bound by host-side launches, not
+        # by the GPU (profiles/r04_middle_train_rank0_breakdown.txt). Needs collectives that can be captured
+        # (comm.capturable: no-op / RCCL stream collectives; not gloo, which stages through host memory)
+        self.graphs = bool(graphs)
+        if self.graphs and not getattr(self.comm, "capturable", False):
+            raise ValueError("graphs=True needs a comm whose collectives can be captured (comm.capturable)")
+        self._graph = None
+        self._eager_steps = 0
         self.xchg = mp.world > 1 or mp.loopback
         self.own: List[dict] = []
         node_ids, dense, node_leaves = set(), [], []
@@ -1360,11 +1370,49 @@ class MiddleTrainer:
                 res_x = h_own
         return model.head(h_own)
 
+    WARM = 3
+
     def step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
-        """One step; y_own = the labels of the owned rows (y[mp.own]). Returns the global loss (device scalar)."""
+        """One step; y_own = the labels of the owned rows (y[mp.own]). Returns the global loss (device scalar; with
+        graphs, the graph's static output, overwritten by the next step)."""
+        if not self.graphs:
+            return self._step(x_full, y_own)
+        if self._graph is None:
+            if self._eager_steps < self.WARM:  # allocator pools, Adam state, descriptor lists, index checks
+                self._eager_steps += 1
+                return self._step(x_full, y_own)
+            self._capture(x_full, y_own)
+        if x_full is not self._x:
+            self._x.copy_(x_full)
+        if y_own is not self._y:
+            self._y.copy_(y_own)
+        self._graph.replay()
+        return self._loss
+
+    def _capture(self, x_full, y_own):
+        self._x, self._y = x_full, y_own
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            self._loss = self._step(self._x, self._y)
+        # everything the captured launches read by address stays alive with the graph: Adam's and the L2 sum's
+        # device descriptor lists (and their pinned staging copies, which captured uploads re-read)
+        self._keep = list(getattr(self.opt, "_tl_cache", {}).values()) + list(self._train._LISTS.values())
+        self._graph = g
+        g.replay()  # the step the capture recorded
+
+    def _step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
         mp, lam, train = self.mp, self.l2_lambda, self._train
-        for p in self.node:
-            p.grad = None
+        if self.graphs:  # persistent gradient buffers (autograd accumulates into them): fixed addresses, so the
+            # optimizer's descriptor lists built in the eager warm-up serve the capture and its replays
+            if not hasattr(self, "_node_grads"):
+                self._node_grads = [torch.zeros_like(p) for p in self.node]
+            for p, gb in zip(self.node, self._node_grads):
+                p.grad = gb
+            torch._foreach_zero_(self._node_grads)
+        else:
+            for p in self.node:
+                p.grad = None
         self.flat.zero_()
         off = 0
         for p in self.dense:

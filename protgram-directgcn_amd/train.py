@@ -27,9 +27,12 @@ import torch.nn.functional as F
 from ._lib import check, load_library
 
 
-def _upload(a: np.ndarray, dev) -> torch.Tensor:
-    """Host array -> device without a host sync (pinned staging, stream-ordered copy)."""
+def _upload(a: np.ndarray, dev, keep: Optional[list] = None) -> torch.Tensor:
+    """Host array -> device without a host sync (pinned staging, stream-ordered copy). `keep` receives the pinned
+    staging tensor: a copy captured into a HIP graph re-reads it at every replay, so its owner must keep it alive."""
     h = torch.from_numpy(a).pin_memory()
+    if keep is not None:
+        keep.append(h)
     return h.to(dev, non_blocking=True)
 
 
@@ -55,8 +58,9 @@ class TensorList:
             desc[i, -1] = x.numel()
             chunks[i + 1] = chunks[i] + lib.pg_multi_chunks(x.numel())
         self.fields = fields  # keep the tensors alive while the descriptors may be in use (dropped when cached)
-        self.desc = _upload(desc, dev)
-        self.chunk_ptr = _upload(chunks, dev)
+        self.host = []  # the pinned staging copies (see _upload)
+        self.desc = _upload(desc, dev, self.host)
+        self.chunk_ptr = _upload(chunks, dev, self.host)
         self.nchunks = int(chunks[-1])
         self.partial = torch.empty(max(self.nchunks, 1), dtype=torch.float32, device=dev)
 

@@ -69,6 +69,7 @@ struct DenseP {
     int map_res, map_y;
     int nt_a;  // pipelined kernels: A rows and the per-node constant (read once) by non-temporal LDS-DMA
                // (PG_FLAG_DENSE_A_CACHED clears)
+    int prio;  // pipelined kernel: waves 4-7 (the second-dispatched half) at s_setprio 1 (PG_FLAG_DENSE_PRIO)
     int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
 };
 
@@ -998,6 +999,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     float4 bq[4];
     if (ntl > 0) lds_ld4x4(&Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], &Bs[3][4 * ej], bq);
     bool y_pending = false;  // the previous epilogue left exactly one Y store per thread in flight
+    if (p.prio && !mfma_first) __builtin_amdgcn_s_setprio(1);
     for (int64_t i = 0; i <= ntl && ntl > 0; ++i) {
         const int ab = (int)(i & 1);
         [[maybe_unused]] const int si = (int)i;
@@ -1184,6 +1186,7 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.nt_a = (flags & PG_FLAG_DENSE_A_CACHED) ? 0 : 1;
+    p.prio = (flags & PG_FLAG_DENSE_PRIO) ? 1 : 0;
 #ifdef PG_DENSE_EXP
     p.exp = (int)((flags >> 24) & 31u);
 #endif

@@ -15,7 +15,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
-from protgram_directgcn_amd._lib import PG_FLAG_DENSE_DMA_IL  # noqa: E402
+from protgram_directgcn_amd._lib import PG_FLAG_DENSE_DMA_IL, PG_FLAG_DENSE_PRIO  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 n = int(args[0]) if args else 4
@@ -33,7 +33,8 @@ prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
 Z = ops.spmm3(g, x)
 Y = torch.empty(N, 128, device=dev)
 base = ops.default_flags()
-variants = {"x3p": base, "x3p_il": base | PG_FLAG_DENSE_DMA_IL}
+variants = {"x3p": base, "x3p_il": base | PG_FLAG_DENSE_DMA_IL, "x3p_prio": base | PG_FLAG_DENSE_PRIO,
+            "x3p_il_prio": base | PG_FLAG_DENSE_DMA_IL | PG_FLAG_DENSE_PRIO}
 
 
 def run(fl):
@@ -42,7 +43,7 @@ def run(fl):
 
 with torch.no_grad():
     outs = {k: run(fl).clone() for k, fl in variants.items()}
-    same = torch.equal(outs["x3p"], outs["x3p_il"])
+    same = all(torch.equal(outs["x3p"], v) for v in outs.values())
     times = {k: [] for k in variants}
     for _ in range(rounds):
         for k, fl in variants.items():

@@ -85,10 +85,9 @@ typedef struct pg_edge1 {
 #define PG_FLAG_MID_LOADER_SYNC (1u << 19) /* middle-tile kernels: the loader waits for chunk t+1's out / self rows
                                              before the in-phase barrier of chunk t (the round-3 protocol) instead of
                                              before the store-out barrier */
-#define PG_FLAG_DENSE_DMA_IL (1u << 13)   /* pipelined dense kernel: the next-but-one tile's A / gate LDS-DMA pieces
-                                             issued between the MFMA k-steps instead of at the top of the iteration;
-                                             same results */
-#define PG_FLAG_DENSE_PRIO (1u << 17)     /* pipelined dense kernel: the second half of the waves at s_setprio 1 */
+#define PG_FLAG_DENSE_NO_IL (1u << 13)    /* pipelined dense kernel: issue the next-but-one tile's A / gate LDS-DMA
+                                             pieces all at the top of the iteration (the round-3 schedule) instead of
+                                             between the MFMA k-steps (the default); same results */
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
 #define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernel

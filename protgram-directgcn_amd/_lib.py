@@ -25,8 +25,7 @@ PG_FLAG_MID_NO_PAIRS = 1 << 22
 PG_FLAG_MID_LOADER_SYNC = 1 << 19
 PG_FLAG_MID_TRANSPOSED = 1 << 23
 PG_FLAG_DENSE_A_CACHED = 1 << 12
-PG_FLAG_DENSE_DMA_IL = 1 << 13
-PG_FLAG_DENSE_PRIO = 1 << 17
+PG_FLAG_DENSE_NO_IL = 1 << 13
 
 c_i64, c_i32, c_u32, c_f32, c_vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 

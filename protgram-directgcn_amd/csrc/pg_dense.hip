@@ -69,7 +69,6 @@ struct DenseP {
     int map_res, map_y;
     int nt_a;  // pipelined kernels: A rows and the per-node constant (read once) by non-temporal LDS-DMA
                // (PG_FLAG_DENSE_A_CACHED clears)
-    int prio;  // pipelined kernel: waves 4-7 (the second-dispatched half) at s_setprio 1 (PG_FLAG_DENSE_PRIO)
     int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
 };
 
@@ -770,7 +769,7 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
 // LDS: Af 2 x 24 KB, As 2 x 36 KB, Cs/Rs 16 KB, Es 8.3 KB, gate inputs 4 x 512 B, bias sums 2 KB.
 __device__ __forceinline__ int a_unit16(int s, int r, int g) { return 64 * s + 4 * r + (g ^ ((-(r >> 2)) & 3)); }
 
-// IL (PG_FLAG_DENSE_DMA_IL): the A and gate-input LDS-DMA pieces of tile i + 2 are issued between the k-steps of
+// IL (the default; PG_FLAG_DENSE_NO_IL clears it): the A and gate-input LDS-DMA pieces of tile i + 2 are issued between the k-steps of
 // the wave's MFMA phase instead of all at the top of the iteration (stamps: issuing the five or seven pieces at once
 // took ~1,750 of an iteration's ~7,300 cycles, the memory pipeline pushing back); the constant / residual pieces stay
 // first, so the counted vmcnt waits are unchanged.
@@ -999,7 +998,6 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     float4 bq[4];
     if (ntl > 0) lds_ld4x4(&Bs[0][4 * ej], &Bs[1][4 * ej], &Bs[2][4 * ej], &Bs[3][4 * ej], bq);
     bool y_pending = false;  // the previous epilogue left exactly one Y store per thread in flight
-    if (p.prio && !mfma_first) __builtin_amdgcn_s_setprio(1);
     for (int64_t i = 0; i <= ntl && ntl > 0; ++i) {
         const int ab = (int)(i & 1);
         [[maybe_unused]] const int si = (int)i;
@@ -1186,7 +1184,6 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.nt_a = (flags & PG_FLAG_DENSE_A_CACHED) ? 0 : 1;
-    p.prio = (flags & PG_FLAG_DENSE_PRIO) ? 1 : 0;
 #ifdef PG_DENSE_EXP
     p.exp = (int)((flags >> 24) & 31u);
 #endif
@@ -1227,7 +1224,7 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
                 return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_f32: unpacked weights must be 16-B aligned");
             const int64_t T16 = (a->M + 15) / 16;
             const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
-            const bool il = (flags & PG_FLAG_DENSE_DMA_IL) != 0;
+            const bool il = (flags & PG_FLAG_DENSE_NO_IL) == 0;
             if (p.pregated) {
                 if (il) hipLaunchKernelGGL((dense_x3p_kernel<true, true>), dim3(g16), dim3(512), 0, s, p);
                 else hipLaunchKernelGGL((dense_x3p_kernel<true, false>), dim3(g16), dim3(512), 0, s, p);

@@ -1381,7 +1381,8 @@ class MiddleTrainer:
             if self._eager_steps < self.WARM:  # allocator pools, Adam state, descriptor lists, index checks
                 self._eager_steps += 1
                 return self._step(x_full, y_own)
-            self._capture(x_full, y_own)
+            self._capture(x_full, y_own)  # replays once: this step
+            return self._loss
         if x_full is not self._x:
             self._x.copy_(x_full)
         if y_own is not self._y:

@@ -487,11 +487,11 @@ def test_dense_kernel_variants_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, ro
 @pytest.mark.parametrize("M,vec", [(1, True), (5, True), (17, False), (700, True), (2050, True), (8200, False),
                                    (40_000, True)])
 def test_dense_dma_interleave_bitexact(pkg, cuda, M, vec):
-    """PG_FLAG_DENSE_DMA_IL (dense_x3p_kernel<.., IL>: the next-but-one tile's LDS-DMA pieces issued between the MFMA
-    k-steps) moves only instruction issue: the same bits, for full and partial tiles, vector and scalar gates,
+    """The default dense_x3p_kernel<.., IL = true> (the next-but-one tile's LDS-DMA pieces issued between the MFMA
+    k-steps) against PG_FLAG_DENSE_NO_IL (all at the top of the iteration) moves only instruction issue: the same bits, for full and partial tiles, vector and scalar gates,
     pre-gated operands, the identity residual and none, and the n-gram row map (pg_directgcn_dense_ngram_rows_f32)."""
     from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_DMA_IL
+    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_NO_IL
     Z, xres, prm, const, _, _, _, _ = _dense_case(M, 128, 128, False, vec, False, 1000 + M)
     dv = {k: v.to(cuda) for k, v in prm.items()}
     gate = 0 if vec else 1
@@ -500,7 +500,7 @@ def test_dense_dma_interleave_bitexact(pkg, cuda, M, vec):
     for pre in (False, True):
         for res in (xres.to(cuda), None):
             a = ops.layer_dense(Z.to(cuda), dv, gate, constant=c, res_x=res, act=True, flags=base, pregated=pre)
-            b = ops.layer_dense(Z.to(cuda), dv, gate, constant=c, res_x=res, act=True, flags=base | PG_FLAG_DENSE_DMA_IL,
+            b = ops.layer_dense(Z.to(cuda), dv, gate, constant=c, res_x=res, act=True, flags=base | PG_FLAG_DENSE_NO_IL,
                                 pregated=pre)
             assert torch.equal(a, b), (M, vec, pre, res is None)
     if vec and M % 400 == 0 or M == 40_000:
@@ -511,7 +511,7 @@ def test_dense_dma_interleave_bitexact(pkg, cuda, M, vec):
         cm = torch.randn(M, 128, generator=torch.Generator().manual_seed(4)).to(cuda)
         pm = {k: (v[:M] if v.dim() and v.size(0) >= M and k.startswith("C_") else v) for k, v in dv.items()}
         outs = []
-        for fl in (base, base | PG_FLAG_DENSE_DMA_IL):
+        for fl in (base, base | PG_FLAG_DENSE_NO_IL):
             Y = torch.full((N, 128), 7.0, device=cuda)
             ops.layer_dense_ngram_rows(Zm, pm, 0, Kn1, 0, constant=cm, res_x=X, map_res=True, out=Y, map_out=True,
                                        act=True, flags=fl)

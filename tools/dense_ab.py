@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of the dense layer kernels in the in-tree library on the bench's layer-1 shape (B(20,n), F = 128,
-vector gates, constant, identity residual): flags 0 (dense_x3p_kernel) against PG_FLAG_DENSE_DMA_IL
-(dense_x3p_kernel<.., IL>: interleaved LDS-DMA issue), interleaved rounds (min and median per launch, HIP events), and a bit-equality check.
+vector gates, constant, identity residual): the default (dense_x3p_kernel<.., IL>: interleaved LDS-DMA issue) against
+PG_FLAG_DENSE_NO_IL (all pieces at the top of the iteration), interleaved rounds (min and median per launch, HIP events), and a bit-equality check.
 usage: python tools/dense_ab.py [n=4] [rounds=20] [reps=20]"""
 import json
 import os
@@ -15,7 +15,7 @@ from __graft_entry__ import load_package  # noqa: E402
 
 pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
-from protgram_directgcn_amd._lib import PG_FLAG_DENSE_DMA_IL, PG_FLAG_DENSE_PRIO  # noqa: E402
+from protgram_directgcn_amd._lib import PG_FLAG_DENSE_NO_IL  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 n = int(args[0]) if args else 4
@@ -33,8 +33,7 @@ prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in layer._dense_params())))
 Z = ops.spmm3(g, x)
 Y = torch.empty(N, 128, device=dev)
 base = ops.default_flags()
-variants = {"x3p": base, "x3p_il": base | PG_FLAG_DENSE_DMA_IL, "x3p_prio": base | PG_FLAG_DENSE_PRIO,
-            "x3p_il_prio": base | PG_FLAG_DENSE_DMA_IL | PG_FLAG_DENSE_PRIO}
+variants = {"x3p_il": base, "x3p_no_il": base | PG_FLAG_DENSE_NO_IL}
 
 
 def run(fl):
@@ -43,7 +42,7 @@ def run(fl):
 
 with torch.no_grad():
     outs = {k: run(fl).clone() for k, fl in variants.items()}
-    same = all(torch.equal(outs["x3p"], v) for v in outs.values())
+    same = all(torch.equal(outs["x3p_il"], v) for v in outs.values())
     times = {k: [] for k in variants}
     for _ in range(rounds):
         for k, fl in variants.items():

@@ -53,7 +53,7 @@ a.Y, a.ldy = ops._p(Y), Y.stride(0)
 raw = [ops._f32c(prm[k].detach()) for k in ops._PACK_KEYS]
 (a.W_main_in, a.W_main_out, a.W_undirected, a.W_shared, a.b_main_in, a.b_dir_shared_in, a.b_main_out,
  a.b_dir_shared_out, a.b_undirected, a.b_undirected_shared) = [ops._p(t) for t in raw]
-base = (_lib.PG_FLAG_DENSE_PREGATED if pregated else 0) | (_lib.PG_FLAG_DENSE_DMA_IL if "--il" in sys.argv else 0)
+base = (_lib.PG_FLAG_DENSE_PREGATED if pregated else 0) | (_lib.PG_FLAG_DENSE_NO_IL if "--no-il" in sys.argv else 0)
 st = ops._stream(Z)
 
 

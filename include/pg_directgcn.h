@@ -90,8 +90,9 @@ typedef struct pg_edge1 {
                                              between the MFMA k-steps (the default); same results */
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
-#define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernel
-                                             (pg_spmm3t_ngram_mid_f32) instead of the 4x4-block one */
+#define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the off-diagonal transposed middle-tile kernel
+                                             (pg_spmm3t_ngram_mid_offdiag_f32) plus the diagonal term on the host,
+                                             instead of the 4x4-block kernel */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -291,14 +292,16 @@ int pg_spmm3_ngram_mid_map_f32(int K, int n, const float* plan, const int32_t* g
                                int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream);
 int pg_spmm3_resid_f32(int64_t n_list, const int64_t* rowptr, const int32_t* rows, const pg_edge3_t* edges,
                        const float* X, int64_t ldx, int64_t F, float* Z, int64_t ldz, uint32_t flags, void* stream);
-/* Transposed middle-tile kernel: dX (+)= sum_k A_k G[:, kF:(k+1)F] for the symmetric n-gram matrices (A_k^T = A_k;
- * the backward of the six propagates, protgram_directgcn.py:101-112, replacing pg_spmm3t_ngram_f32 / pg_spmm3t_f32
- * on graphs over all K^n n-grams). Same middle plan, stream and loader as the forward; per chunk three sub-chunks
- * (one per slice G_k) accumulate into one LDS partial, so dX is written once. K = 20, F a multiple of 16, 16-B
- * aligned G and dX rows; PG_ERR_UNSUPPORTED otherwise. Numerics as the forward: within fp32 rounding of the CSR
- * kernel; G must be finite. */
-int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
-                            float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+/* Transposed middle-tile kernel, off-diagonal part: dX (+)= sum_k (A_k - Diag_k) G[:, kF:(k+1)F] for the symmetric
+ * n-gram matrices (A_k^T = A_k; the backward of the six propagates, protgram_directgcn.py:101-112, replacing
+ * pg_spmm3t_ngram_f32 / pg_spmm3t_f32 on graphs over all K^n n-grams), where Diag_k holds the middle plan's diagonal
+ * slots (a self-loop of a constant n-gram sits in its out-slot and IS included). The caller adds
+ * sum_k Diag_k G_k: the dense backward while it holds G (pg_directgcn_dense_bwd_f32 with `diag`), or the host
+ * (ops.spmm3_t under PG_FLAG_MID_TRANSPOSED). Same middle plan and chunk stream as the forward; accumulate: dX +=.
+ * K = 20, F a multiple of 16, 16-B aligned G and dX rows, K^n * ldg and K^n * lddx < 2^32; PG_ERR_UNSUPPORTED
+ * otherwise. Numerics: within fp32 rounding of the CSR kernel; G must be finite. */
+int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg,
+                                    int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
  * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).

@@ -383,19 +383,25 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     float Ao[XTPW][XS], Ai[XTPW][XS];  // A fragments of this wave's out / in tiles (middle-resident)
     // A fragments of the next middle are prefetched where the registers are free: Ao after the last chunk's
     // out-phase (consumed by the next middle's first out-phase), Ai before its first chunk's out-phase
+    // (wave-uniform base + a 32-bit lane offset formed at each load: no 64-bit per-lane pointer stays live -- in the
+    // mapped kernel one was spilled, and its reload's vmcnt(0) waited for the chunk's Z stores at every middle change)
     auto load_Ao = [&](int M) {
-        const float* pm = p.plan + (int64_t)M * XMB + XPO + lane;
+        const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + XPO);
+        const uint32_t lo = (uint32_t)opaque((lane + (wb * 4 + mw) * XS * 64) * 4);
 #pragma unroll
         for (int j = 0; j < XTPW; ++j)
 #pragma unroll
-            for (int s = 0; s < XS; ++s) Ao[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+            for (int s = 0; s < XS; ++s)
+                Ao[j][s] = *reinterpret_cast<const float*>(pm + lo + (uint32_t)(((2 * j * 4) * XS + s) * 256));
     };
     auto load_Ai = [&](int M) {
-        const float* pm = p.plan + (int64_t)M * XMB + XPI + lane;
+        const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + XPI);
+        const uint32_t lo = (uint32_t)opaque((lane + (wb * 4 + mw) * XS * 64) * 4);
 #pragma unroll
         for (int j = 0; j < XTPW; ++j)
 #pragma unroll
-            for (int s = 0; s < XS; ++s) Ai[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+            for (int s = 0; s < XS; ++s)
+                Ai[j][s] = *reinterpret_cast<const float*>(pm + lo + (uint32_t)(((2 * j * 4) * XS + s) * 256));
     };
     // this lane's four accumulator rows i = 16 mw + 4 q4 + r: (k, a) in the out-phase, (k, b) in the in-phase. The
     // padding rows i = 60..63 repeat rows 56..59 (the plan holds their weights twice): their lanes compute the same
@@ -484,8 +490,6 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
         // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
-        ET* zso = reinterpret_cast<ET*>(p.Z) + (MAP ? 0 : ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz) +
-                  (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
         auto rd_in = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
@@ -523,7 +527,10 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         XSTAMP(ci, 4);
         // ---- store-out of chunk t, in the next out-phase's shadow (the out/self DMA of the in-phase is done; only
         // the smaller in-source DMA shares the CU's memory pipeline with these stores): every row of the partial
-        // buffer as 16-B pieces, then W(t) before the next out-phase overwrites it
+        // buffer as 16-B pieces, then W(t) before the next out-phase overwrites it. (The row address is formed here,
+        // not before the in-phase: it is not live across the in-phase's MFMAs, whose registers are the tightest.)
+        ET* zso = reinterpret_cast<ET*>(p.Z) + (MAP ? 0 : ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz) +
+                  (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
             const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);
@@ -563,280 +570,328 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Transposed middle-tile kernel: the backward of the forward above for the symmetric n-gram matrices (A_k^T = A_k;
-// the autograd of protgram_directgcn.py:101-112), with G_k = G[:, kF:(k+1)F]:
-//   dX[a.M.b, f] = sum_k ( sum_c Wout_k[a,b,c] G_k[M.b.c, f] + Wdiag_k[a,b] G_k[a.M.b, f] + sum_c Win_k[a,b,c] G_k[c.a.M, f] )
-// Same plan, same (middle, 16-feature chunk) stream and workgroup pairs, same LDS-DMA loader: each chunk runs three
-// sub-chunks k = 0, 1, 2, each an out-phase (per b) and an in-phase (per a) over the slice G_k, whose rows the loader
-// stages exactly as the forward stages X's. All six phases accumulate into ONE partial buffer P[a][b][16 f] in LDS
-// (each phase reads it as its MFMAs' initial accumulators and writes it back), which leaves for HBM once, after
-// k = 2: dX is written once per chunk, G_k's rows are read as out-sources, in-sources and own rows.
-// Sub-chunk k needs only the row tiles that hold rows (k, a) = 20 k .. 20 k + 19 of the plan's fragments (tiles
-// m = 20k / 16 and the next). The compute waves own fixed row tiles (their weights stay in registers per middle, as
-// in the forward): wave w owns tile m = (w & 1) + 2 (w >> 2) and the columns of parity (w >> 1) & 1, so the two waves
-// of every SIMD (w, w + 4) own tiles {0, 2} or {1, 3} and exactly one of them works in each phase. A lane row of an
-// active tile that belongs to another adjacency computes a value nobody reads: it reads and writes the pad dwords of
-// a P row (P rows are 20 dwords: 16 features + 4 pad, so both phases' lane patterns are bank-conflict free).
-constexpr int TPB = 20;                               // P row pitch (dwords)
-constexpr int TPA = XK * TPB + 4;                     // P a-block pitch (dwords)
-constexpr int TL_OUT = 0;                             // G_k out-sources [b][c][16 f]
-constexpr int TL_IN = TL_OUT + XR * 64;               // G_k in-sources  [c][a (+pad)][16 f]
-constexpr int TL_SELF = TL_IN + ML<false>::LINB;      // G_k own rows    [a][b][16 f]
-constexpr int TL_PART = TL_SELF + XR * 64;            // P [a][b][20]
-constexpr int TL_DIAG = TL_PART + XK * TPA * 4;       // diagonal weights [a][b][k]
-constexpr int TL_BYTES = TL_DIAG + XR * 3 * 4;        // 115,968 B
-static_assert(TL_BYTES <= 163840 && (TPB * 4) % 16 == 0 && (TPA * 4) % 16 == 0, "transposed LDS image");
+// Transposed middle-tile kernel, OFF-DIAGONAL part (pg_spmm3t_ngram_mid_offdiag_f32): the backward of the forward above
+// for the symmetric n-gram matrices (A_k^T = A_k; the autograd of protgram_directgcn.py:101-112) without its diagonal
+// term, with G_k = G[:, kF:(k+1)F]:
+//   dX[a.M.b, f] (+)= sum_k ( sum_c Wout_k[a,b,c] G_k[M.b.c, f] + sum_c Win_k[a,b,c] G_k[c.a.M, f] )
+// Why without the diagonal: the out-sources of middle M are the rows with prefix M, its in-sources the rows with
+// suffix M and its own rows those with middle M -- three disjoint sets, so the diagonal term sum_k Wdiag_k G_k[a.M.b]
+// would be a THIRD read of every G row (the 4x4-block kernel's 1,057 MB per launch). The dense backward adds it
+// instead, while it holds G in registers (pg_directgcn_dense_bwd_f32 with diagonal weights; ops.PropagateDense).
+//
+// Per (middle, 16-feature chunk) six sub-phases, one slice G_k each:
+//   out k = 0, 1, 2: tiles (b, m), rows a = 16 m + 0..15 (20 valid), K-dim (k, c): 5 MFMA k-steps per slice, the
+//                    accumulators kept across the three slices and handed over as P[a][b][16 f] (LDS) after k = 2;
+//   in  k = 0, 1, 2: tiles (a, m), rows b, started from P after k = 0's barrier; the finished rows go back to P and
+//                    leave for HBM (16-B pieces) in the next chunk's first sub-phase.
+// Every wave computes AND issues the LDS-DMA (no loader waves): one slice's source rows per sub-phase (out: 400 x 64 B,
+// in: 420 x 64 B with the pad rows) into a ring of four slots, three sub-phases ahead, one barrier per sub-phase. Wave w
+// owns the row tile m = w & 1 of the columns b (out) / a (in) = (w >> 1) + 4 j, j = 0..4; its A fragments, gathered
+// from the forward plan (rows (k, a) -> a, K-dim c -> (k, c)), stay in registers per middle: 75 out + 75 in per lane
+// (8 waves, 2 per SIMD: up to 256 VGPRs), the next middle's fetched a slice at a time three sub-phases before use.
+// The four slots and P are separate LDS objects, and the sub-phase loop is unrolled by 12 (= lcm of 6 sub-phases per
+// chunk and 4 slots), so every slot a DMA writes and every slot a read uses is known at compile time.
+constexpr int T2_SLOT = 27 * 1024;                     // ring slot: one slice's in-sources (420 rows x 64 B) rounded
+constexpr int T2_NOUT = XR * 64 / 1024;                // 25 wave-instructions of out-source pieces per slice
+constexpr int T2_NIN = (XK * XCB * 64 + 1023) / 1024;  // 27 of in-source pieces (the last one partly padding)
+constexpr int T2_PB = XFC, T2_PA = XK * T2_PB;        // P[a][b][16 f] (dwords; the 2-way conflicts of its 40 ops per
+                                                       // wave and chunk cost less than the padding's LDS)
+constexpr int T2_TPW = 5;                              // tiles per wave per sub-phase
+static_assert(T2_NIN * 1024 <= T2_SLOT && T2_NOUT * 1024 <= T2_SLOT && T2_NIN <= 32 && T2_NOUT <= 32, "ring slot");
+static_assert(4 * T2_SLOT + 2 * XR * 64 <= 163840, "LDS: four slots, P and the accumulate stage");
 
-struct TChunk {
-    int M, ch, k, first;  // middle, chunk, adjacency (sub-chunk), first sub-chunk of this middle in the range
-};
+// s_waitcnt vmcnt(min(n, 23)) for a wave-uniform n (a smaller bound than needed only waits longer)
+__device__ __forceinline__ void vm_wait(int n) {
+    switch (n < 0 ? 0 : n) {
+#define PG_VMW(k)                                              \
+    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); \
+        break;
+        PG_VMW(0) PG_VMW(1) PG_VMW(2) PG_VMW(3) PG_VMW(4) PG_VMW(5) PG_VMW(6) PG_VMW(7) PG_VMW(8) PG_VMW(9)
+        PG_VMW(10) PG_VMW(11) PG_VMW(12) PG_VMW(13) PG_VMW(14) PG_VMW(15) PG_VMW(16) PG_VMW(17) PG_VMW(18)
+        PG_VMW(19) PG_VMW(20) PG_VMW(21) PG_VMW(22)
+#undef PG_VMW
+        default: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    }
+}
 
-__global__ __launch_bounds__(XTHREADS) void ngram_midt_kernel(XP p, int accumulate) {
-    using C = ML<false>;
-    extern __shared__ __attribute__((aligned(16))) char L[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // the forward's chunk ranges and pairs (see ngram_mid_kernel); sub-chunk t = 3 g + k
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+// LDS-DMA piece (16 B per lane -> LDS byte address lds + 16 lane) in inline asm: hidden from the compiler's wait
+// bookkeeping, which otherwise drains every DMA in flight (vmcnt(0)) before LDS reads it cannot tell apart from them
+// (at control-flow joins); the kernel counts these operations itself (vm_wait). M0 saved and restored in the statement.
+__device__ __forceinline__ void glds16_asm(const float* src, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+
+__global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) {
+    __shared__ __attribute__((aligned(16))) float S0[T2_SLOT / 4];
+    __shared__ __attribute__((aligned(16))) float S1[T2_SLOT / 4];
+    __shared__ __attribute__((aligned(16))) float S2[T2_SLOT / 4];
+    __shared__ __attribute__((aligned(16))) float S3[T2_SLOT / 4];
+    __shared__ __attribute__((aligned(16))) float Pb[XK * T2_PA];
+    __shared__ __attribute__((aligned(16))) float SX[XR * XFC];  // accumulate: the chunk's dX rows, staged by LDS-DMA
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the forward's chunk ranges and workgroup pairs (see ngram_mid_kernel)
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
     const int half = p.cstride == 2 ? (int)(lb & 1) : 0;
     const int64_t lu = p.cstride == 2 ? lb >> 1 : lb, nu = p.cstride == 2 ? gridDim.x >> 1 : gridDim.x;
     const int g0 = (int)(lu * p.chunks / nu), g1 = (int)((lu + 1) * p.chunks / nu);
+    if (g0 >= g1) return;
     const int nchu = p.nch / p.cstride;
-    const int t0 = 3 * g0, t1 = 3 * g1;
-    auto sub_at = [&](int t) -> TChunk {
-        const int g = t / 3, k = t - 3 * g;
-        const int Mr = g / nchu;
-        const int j = g - Mr * nchu;
-        return TChunk{(int)p.m0 + Mr, j * p.cstride + half, k, (g == g0 || j == 0) && k == 0};
+    const int nc = g1 - g0;  // chunks of this workgroup, sub-phases u = 6 c + j
+    const int U = 6 * nc;
+    auto mid_of = [&](int c) { return (int)p.m0 + (g0 + c) / nchu; };
+    auto ch_of = [&](int c) { return ((g0 + c) % nchu) * p.cstride + half; };
+    const int q = lane >> 4, fl = lane & 15;
+    const int mt = wave & 1, grp = wave >> 1;
+    const int64_t ldg = p.ldx;
+    const float* __restrict__ G = reinterpret_cast<const float*>(p.X);
+
+    // LDS-DMA: wave-instruction it = wave + 8 t of a slice (piece it * 64 + lane, lane-linear in the slot); the per-lane
+    // element offsets do not depend on the middle, chunk or slice
+    // element offsets < 2^32 (the host checks n_rows * ldg): 32-bit per lane, added to a wave-uniform base
+    uint32_t off_o[4], off_i[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int pc = (wave + 8 * t) * 64 + lane, rl = pc >> 2, qq = pc & 3;
+        off_o[t] = (uint32_t)(rl < XR ? rl : 0) * (uint32_t)ldg + 4 * qq;  // out: row M K^2 + rl (= M.b.c)
+        const int c = rl / XCB, a = rl - c * XCB;                          // in: row c.a.M; pad pieces read row M
+        off_i[t] = (a >= XK || c >= XK) ? 4 * qq
+                                        : (uint32_t)(c * (uint32_t)p.Kn1 + a * (uint32_t)p.Kn2) * (uint32_t)ldg + 4 * qq;
+    }
+    const int n_out = wave < T2_NOUT - 24 ? 4 : 3, n_in = wave < T2_NIN - 24 ? 4 : 3;
+    // accumulate: the dX pieces of a chunk (row a.M.b, 16-B piece q4), in the store-out's order
+    uint32_t off_x[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int pc = min((wave + 8 * t) * 64 + lane, XR * 4 - 1), row = pc >> 2, a = row / XK, b = row - a * XK;
+        off_x[t] = (uint32_t)(a * (uint32_t)p.zsa + b) * (uint32_t)p.ldz + 4 * (pc & 3);
+    }
+    auto dma_x = [&](int c) {
+        const float* base = reinterpret_cast<const float*>(p.Z) + (int64_t)(mid_of(c) - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (t < n_out) glds16_asm(base + off_x[t], lds_addr(SX) + (wave + 8 * t) * 1024);
+    };
+    auto slot = [&](auto sc) -> float* {
+        constexpr int S = decltype(sc)::value;
+        if constexpr (S == 0) return S0;
+        else if constexpr (S == 1) return S1;
+        else if constexpr (S == 2) return S2;
+        else return S3;
+    };
+    auto dma = [&](float* dst, int c, int j) {  // sub-phase (chunk c, j): slice k = j mod 3 of the out / in sources
+        const int M = mid_of(c), k = j < 3 ? j : j - 3;
+        const float* base = G + (int64_t)k * p.F + ch_of(c) * XFC;
+        if (j < 3) {
+            base += (int64_t)M * XR * ldg;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t < n_out) glds16_asm(base + off_o[t], lds_addr(dst) + (wave + 8 * t) * 1024);
+        } else {
+            base += (int64_t)M * ldg;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t < n_in) glds16_asm(base + off_i[t], lds_addr(dst) + (wave + 8 * t) * 1024);
+        }
     };
 
-    if (wave >= XCW) {  // ---------------- loader waves (the forward's, on the columns of G_k)
-        const int lw = wave - XCW;
-        constexpr int NO = (C::NOI + XLW - 1) / XLW, NI = (C::NII + XLW - 1) / XLW;
-        int64_t off_o[NO], off_i[NI], off_s[NO];
-        const int64_t ldx = p.ldx;
+    // A fragments: Wo[j][5 k + s] (tile b = grp + 4 j, m = mt): lane holds A[a = 16 mt + fl][c = 4 s + q] of slice k
+    // = Wout_k[a, b, c], in the forward plan at out fragment (b, row (k, a) = 20 k + a, c). Wi likewise with (a, b)
+    // exchanged (tile a = grp + 4 j, rows b = 16 mt + fl). Rows past 19 load row 19's weights: an MFMA row only feeds
+    // its own accumulator row, and those rows are never handed over or stored.
+    float Wo[T2_TPW][15], Wi[T2_TPW][15];
+    const int rrc = min(16 * mt + fl, XK - 1);
+    auto gather = [&](auto kc, auto inc, int M) {
+        constexpr int k = decltype(kc)::value;
+        constexpr bool IN = decltype(inc)::value != 0;
+        const int i_f = XK * k + rrc;
+        const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + (IN ? XPI : XPO));  // wave-uniform
+        // per-lane byte offset, recomputed at every gather (opaque: not hoisted into 25 live copies per slice)
+        const uint32_t lo = (uint32_t)opaque(((q << 4) + (i_f & 15) + ((grp * 4 + (i_f >> 4)) * XS) * 64) * 4);
 #pragma unroll
-        for (int t = 0; t < NO; ++t) {
-            const int it = lw + t * XLW;
-            const int rl = (int)((unsigned)(it * 64 + lane) / C::PPR), q = lane & (C::PPR - 1);
-            off_o[t] = (int64_t)rl * ldx + q * C::EPP;
-            const int a = rl / XK, b = rl - a * XK;
-            off_s[t] = (a * p.Kn1 + b) * ldx + q * C::EPP;
-        }
+        for (int j = 0; j < T2_TPW; ++j)
 #pragma unroll
-        for (int t = 0; t < NI; ++t) {
-            const int it = lw + t * XLW;
-            const int rl = (int)((unsigned)(it * 64 + lane) / C::PPR), q = lane & (C::PPR - 1);
-            const int c = rl / XCB, a = rl - c * XCB;
-            off_i[t] = (a >= XK || c >= XK) ? q * C::EPP : (c * p.Kn1 + a * p.Kn2) * ldx + q * C::EPP;
-        }
-        auto dma_rows = [&](int region, int kind, const TChunk& c) {
-            const float* xc = reinterpret_cast<const float*>(p.X) + (int64_t)c.k * p.F + c.ch * XFC;
-            if (kind == 0) {
-                const float* base = xc + (int64_t)c.M * XR * ldx;
-#pragma unroll
-                for (int t = 0; t < NO; ++t)
-                    if (lw + t * XLW < C::NOI) glds16(base + off_o[t], L + region + (lw + t * XLW) * 1024);
-            } else if (kind == 1) {
-                const float* base = xc + (int64_t)c.M * ldx;
-#pragma unroll
-                for (int t = 0; t < NI; ++t)
-                    if (lw + t * XLW < C::NII) glds16(base + off_i[t], L + region + (lw + t * XLW) * 1024);
-            } else {
-                const float* base = xc + (int64_t)c.M * XK * ldx;
-#pragma unroll
-                for (int t = 0; t < NO; ++t)
-                    if (lw + t * XLW < C::NOI) glds16(base + off_s[t], L + region + (lw + t * XLW) * 1024);
+            for (int s = 0; s < XS; ++s) {
+                const float v = *reinterpret_cast<const float*>(pm + lo + (uint32_t)((16 * j * XS + s) * 256));
+                if constexpr (IN) Wi[j][5 * k + s] = v;
+                else Wo[j][5 * k + s] = v;
             }
-        };
-        auto dma_diag = [&](int M) {
-            const float* d = p.plan + (int64_t)M * XMB + XPD;
-#pragma unroll 1
-            for (int it = lw; it < 5; it += XLW) {
-                const int P = it * 64 + lane;
-                if (P < XR * 3 / 4) glds16(d + P * 4, L + TL_DIAG + it * 1024);
-            }
-        };
-        if (t0 < t1) {
-            const TChunk c0 = sub_at(t0);
-            dma_rows(TL_OUT, 0, c0);
-            dma_rows(TL_IN, 1, c0);
-            dma_rows(TL_SELF, 2, c0);
-            dma_diag(c0.M);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_barrier" ::: "memory");  // S(-1)
-#pragma unroll 1
-        for (int t = t0; t < t1; ++t) {
-            const bool more = t + 1 < t1;
-            const TChunk nx = more ? sub_at(t + 1) : TChunk{0, 0, 0, 0};
-            asm volatile("s_barrier" ::: "memory");  // M(t): out-phase done; out / self / diag free
-            if (more) {
-                dma_rows(TL_OUT, 0, nx);
-                dma_rows(TL_SELF, 2, nx);
-                if (nx.first) dma_diag(nx.M);
-            }
-            if (!p.early_in) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            asm volatile("s_barrier" ::: "memory");  // S(t): in-phase done; in-region free
-            if (more) dma_rows(TL_IN, 1, nx);
-            wait_all_but_in<C::NII>(lw);             // out / self (+ diagonal) of t + 1 have landed
-            asm volatile("s_barrier" ::: "memory");  // W(t)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        return;
-    }
+    };
 
-    // ---------------- compute waves
-    const int q4 = lane >> 4, fl = lane & 15;
-    const int mw = (wave & 1) + 2 * (wave >> 2);  // row tile
-    const int wb = (wave >> 1) & 1;               // column parity: b (out) / a (in) = 2 j + wb
-    float Ao[XTPW][XS], Ai[XTPW][XS];
-    auto load_Ao = [&](int M) {
-        const float* pm = p.plan + (int64_t)M * XMB + XPO + lane;
+    f4_t acc[T2_TPW];
+    const bool prow = mt == 0 || q == 0;  // accumulator rows 16 mt + 4 q + r < 20
+    const int p_out = opaque((((16 * mt + 4 * q) * T2_PA + grp * T2_PB + fl) * 4));  // P[a][b]: + (r T2_PA + 4 j T2_PB) 4
+    const int p_in = opaque(((grp * T2_PA + (16 * mt + 4 * q) * T2_PB + fl) * 4));   // P[a][b]: + (4 j T2_PA + r T2_PB) 4
+    const int b_out = opaque(((grp * XK + q) * XFC + fl) * 4);   // out-source (b = grp + 4j, c = 4 s + q): + (4 j K + 4 s) 64
+    const int b_in = opaque(((q * XCB + grp) * XFC + fl) * 4);   // in-source (c = 4 s + q, a = grp + 4j): + (4 s XCB + 4 j) 64
+    char* const P8 = reinterpret_cast<char*>(Pb);
+    auto out_sub = [&](const float* sl, auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const char* sb = reinterpret_cast<const char*>(sl) + b_out;
+        if constexpr (k == 0) {
 #pragma unroll
-        for (int j = 0; j < XTPW; ++j)
+            for (int j = 0; j < T2_TPW; ++j) acc[j] = f4_t{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-            for (int s = 0; s < XS; ++s) Ao[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+        for (int s = 0; s < XS; ++s) {
+            float bv[T2_TPW];
+#pragma unroll
+            for (int j = 0; j < T2_TPW; ++j) bv[j] = *reinterpret_cast<const float*>(sb + (4 * j * XK + 4 * s) * 64);
+#pragma unroll
+            for (int j = 0; j < T2_TPW; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wo[j][5 * k + s], bv[j], acc[j], 0, 0, 0);
+        }
+        if constexpr (k == 2) {
+            if (prow) {
+#pragma unroll
+                for (int j = 0; j < T2_TPW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        *reinterpret_cast<float*>(P8 + p_out + (r * T2_PA + 4 * j * T2_PB) * 4) = acc[j][r];
+            }
+        }
     };
-    auto load_Ai = [&](int M) {
-        const float* pm = p.plan + (int64_t)M * XMB + XPI + lane;
+    auto in_sub = [&](const float* sl, auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const char* sb = reinterpret_cast<const char*>(sl) + b_in;
+        if constexpr (k == 0) {
 #pragma unroll
-        for (int j = 0; j < XTPW; ++j)
+            for (int j = 0; j < T2_TPW; ++j) {
+                acc[j] = f4_t{0.f, 0.f, 0.f, 0.f};
+                if (prow)
 #pragma unroll
-            for (int s = 0; s < XS; ++s) Ai[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+                    for (int r = 0; r < 4; ++r)
+                        acc[j][r] = *reinterpret_cast<const float*>(P8 + p_in + (4 * j * T2_PA + r * T2_PB) * 4);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < XS; ++s) {
+            float bv[T2_TPW];
+#pragma unroll
+            for (int j = 0; j < T2_TPW; ++j) bv[j] = *reinterpret_cast<const float*>(sb + (4 * s * XCB + 4 * j) * 64);
+#pragma unroll
+            for (int j = 0; j < T2_TPW; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wi[j][5 * k + s], bv[j], acc[j], 0, 0, 0);
+        }
+        if constexpr (k == 2) {
+            if (prow) {
+#pragma unroll
+                for (int j = 0; j < T2_TPW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        *reinterpret_cast<float*>(P8 + p_in + (4 * j * T2_PA + r * T2_PB) * 4) = acc[j][r];
+            }
+        }
     };
-    // this lane's accumulator rows i = 16 mw + 4 q4 + r, r = 0..3: (k, a) in the out-phase, (k, b) in the in-phase
-    // (padding rows 60..63 repeat 56..59, as in the forward). The four rows are consecutive and of one adjacency rk
-    // (20 and 40 are multiples of 4): rv + r. Per-row LDS offsets are the base's plus compile-time immediates.
-    const int i0 = 16 * mw + 4 * q4 - (16 * mw + 4 * q4 >= 3 * XK ? 4 : 0);
-    const int rk = i0 / XK, rv = i0 - rk * XK;
-    const int self_b = opaque(TL_SELF + ((rv * XK + wb) * XFC + fl) * 4);  // + r * K * 64 + 2 j * 64
-    const int col_v = fl * 4, col_j = (16 + (fl & 3)) * 4;  // a valid row's feature dword / a pad dword
-    const int src_lane = (q4 * XFC + fl) * 4;
-    const int in_lane = (q4 * XCB * XFC + fl) * 4;
-    if (t0 < t1) {
-        load_Ao(sub_at(t0).M);
-        load_Ai(sub_at(t0).M);
+    // store-out of chunk c: P's 400 rows as 1,600 16-B pieces over the 512 threads (wave 0: 4, the others 3), plus the
+    // staged dX rows when accumulating
+    const int n_st = wave == 0 ? 4 : 3;  // vector-memory operations it issues
+    auto store_out = [&](int c) {
+        const int M = mid_of(c);
+        float* dx = reinterpret_cast<float*>(p.Z) + (int64_t)(M - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+            const int pc = tid + 512 * tt;
+            if (tt < 3 || wave == 0) {  // pc < 1,600
+                const int row = pc >> 2, a = row / XK, b = row - a * XK, q4 = pc & 3;
+                f4_t v = *reinterpret_cast<const f4_t*>(P8 + (a * T2_PA + b * T2_PB + 4 * q4) * 4);
+                if (accumulate) v += *reinterpret_cast<const f4_t*>(reinterpret_cast<const char*>(SX) + pc * 16);
+                *reinterpret_cast<f4_t*>(dx + ((int64_t)a * p.zsa + b) * p.ldz + 4 * q4) = v;
+            }
+        }
+    };
+
+    // prologue: the first middle's weights and the first three sub-phases' slices, all landed
+    {
+        const int M = mid_of(0);
+        gather(ic<0>{}, ic<0>{}, M);
+        gather(ic<1>{}, ic<0>{}, M);
+        gather(ic<2>{}, ic<0>{}, M);
+        gather(ic<0>{}, ic<1>{}, M);
+        gather(ic<1>{}, ic<1>{}, M);
+        gather(ic<2>{}, ic<1>{}, M);
+        dma(S0, 0, 0);
+        dma(S1, 0, 1);
+        dma(S2, 0, 2);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights (hipcc sees this wait) and the DMA
     }
-    asm volatile("s_barrier" ::: "memory");  // S(-1)
+    // vector-memory operations per sub-phase block, in issue order: [accumulate stage pieces] [DMA of sub-phase u + 3]
+    // [stores, weights]; blk = all of them, aft = those after the DMA
+    int blk[4] = {0, 0, 0, 0}, aft[4] = {0, 0, 0, 0};
+    auto sub = [&](auto jjc, int u) {
+        constexpr int JJ = decltype(jjc)::value, S = JJ % 4, J = JJ % 6;
+        const int c = u / 6;
+        // this wave's pieces of sub-phase u were issued in block u - 3 (and the stage pieces of chunk c - 1 before
+        // them); wait for them, then for everyone's
+        vm_wait(aft[(S + 1) % 4] + blk[(S + 2) % 4] + blk[(S + 3) % 4]);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        int n = 0, o = 0;
+        if constexpr (J == 3) {  // stage this chunk's dX rows (read at the next chunk's store-out)
+            if (accumulate) {
+                dma_x(c);
+                n += n_out;
+            }
+        }
+        // slot (S + 3) % 4 was read by sub-phase u - 1, which every wave has finished: sub-phase u + 3's slice
+        if (u + 3 < U) {
+            dma(slot(ic<(S + 3) % 4>{}), (u + 3) / 6, (J + 3) % 6);
+            n += (J + 3) % 6 < 3 ? n_out : n_in;
+        }
+        asm volatile("" ::: "memory");  // nothing below moves above the DMA
+        if constexpr (J == 0) {
+            if (c > 0) {
+                store_out(c - 1);
+                o += n_st;
+                const int M = mid_of(c);
+                if (mid_of(c - 1) != M) {  // a new middle: its weights (the previous middle's last use was u - 1),
+                    // waited for here (vmcnt(0), which hipcc's bookkeeping sees): one drain per middle change
+                    gather(ic<0>{}, ic<0>{}, M);
+                    gather(ic<1>{}, ic<0>{}, M);
+                    gather(ic<2>{}, ic<0>{}, M);
+                    gather(ic<0>{}, ic<1>{}, M);
+                    gather(ic<1>{}, ic<1>{}, M);
+                    gather(ic<2>{}, ic<1>{}, M);
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+                }
+            }
+        }
+        asm volatile("" ::: "memory");
+        blk[S] = n + o;
+        aft[S] = o;
+        if constexpr (J < 3) out_sub(slot(ic<S>{}), ic<J>{});
+        else in_sub(slot(ic<S>{}), ic<J - 3>{});
+    };
 #pragma unroll 1
-    for (int t = t0; t < t1; ++t) {
-        const TChunk cu = sub_at(t);
-        const int k = cu.k;
-        const int mlo = (XK * k) >> 4;
-        const bool active = mw == mlo || mw == mlo + 1;  // wave-uniform
-        const bool next_mid = k == 2 && t + 1 < t1 && ((t + 1) / 3) % nchu == 0;
-        const int cv = rk == k ? col_v : col_j;
-        const int po = opaque(TL_PART + (rv * TPA + wb * TPB) * 4 + cv);  // out: P[a = rv + r][b = wb]; + r TPA 4 + 2 j TPB 4
-        const int dg = opaque(TL_DIAG + ((rv * XK + wb) * 3 + k) * 4);     // + r K 12 + 2 j 12
-        if (active) {
-            // ---- out-phase: tiles (b = 2 j + wb, m = mw); P[a][b] (+)= sum_c Wout_k G_k[M.b.c] + Wdiag_k G_k[a.M.b]
-            auto rd_out = [&](int j, float (&x)[2][XS]) {
-#pragma unroll
-                for (int s = 0; s < XS; ++s) {
-                    x[0][s] = *reinterpret_cast<const float*>(L + TL_OUT + src_lane + ((2 * j + wb) * XK + 4 * s) * 64);
-                    x[1][s] =
-                        *reinterpret_cast<const float*>(L + TL_OUT + src_lane + ((2 * j + 2 + wb) * XK + 4 * s) * 64);
-                }
-            };
-            float xo[2][2][XS];
-            rd_out(0, xo[0]);
-#pragma unroll
-            for (int j = 0; j < XTPW; j += 2) {
-                float(&xc)[2][XS] = xo[(j >> 1) & 1];
-                if (j + 2 < XTPW) rd_out(j + 2, xo[((j >> 1) + 1) & 1]);
-                float w0[4], w1[4], s0[4], s1[4];
-                f4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    w0[r] = *reinterpret_cast<const float*>(L + dg + r * XK * 12 + 2 * j * 12);
-                    w1[r] = *reinterpret_cast<const float*>(L + dg + r * XK * 12 + (2 * j + 2) * 12);
-                    s0[r] = *reinterpret_cast<const float*>(L + self_b + r * XK * 64 + 2 * j * 64);
-                    s1[r] = *reinterpret_cast<const float*>(L + self_b + r * XK * 64 + (2 * j + 2) * 64);
-                }
-                if (k) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        acc0[r] = *reinterpret_cast<const float*>(L + po + r * TPA * 4 + 2 * j * TPB * 4);
-                        acc1[r] = *reinterpret_cast<const float*>(L + po + r * TPA * 4 + (2 * j + 2) * TPB * 4);
-                    }
-                }
-                asm volatile("" ::: "memory");  // the reads above are issued before the MFMAs below
-#pragma unroll
-                for (int s = 0; s < XS; ++s) {
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j][s], xc[0][s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ao[j + 1][s], xc[1][s], acc1, 0, 0, 0);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    *reinterpret_cast<float*>(L + po + r * TPA * 4 + 2 * j * TPB * 4) = __builtin_fmaf(w0[r], s0[r], acc0[r]);
-                    *reinterpret_cast<float*>(L + po + r * TPA * 4 + (2 * j + 2) * TPB * 4) =
-                        __builtin_fmaf(w1[r], s1[r], acc1[r]);
-                }
-                asm volatile("" ::: "memory");
-            }
-        }
-        if (next_mid) load_Ao(cu.M + 1);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // M(t)
-        if (active) {
-            // ---- in-phase: tiles (a = 2 j + wb, m = mw); P[a][b] += sum_c Win_k G_k[c.a.M]
-            const int pi = opaque(TL_PART + (wb * TPA + rv * TPB) * 4 + cv);  // P[a = wb][b = rv + r]; + r TPB 4 + 2 j TPA 4
-            auto rd_in = [&](int j, float (&x)[2][XS]) {
-#pragma unroll
-                for (int s = 0; s < XS; ++s) {
-                    x[0][s] = *reinterpret_cast<const float*>(L + TL_IN + in_lane + (4 * s * XCB + 2 * j + wb) * 64);
-                    x[1][s] = *reinterpret_cast<const float*>(L + TL_IN + in_lane + (4 * s * XCB + 2 * j + 2 + wb) * 64);
-                }
-            };
-            float xi[2][2][XS];
-            rd_in(0, xi[0]);
-#pragma unroll
-            for (int j = 0; j < XTPW; j += 2) {
-                float(&xc)[2][XS] = xi[(j >> 1) & 1];
-                f4_t acc0, acc1;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    acc0[r] = *reinterpret_cast<const float*>(L + pi + r * TPB * 4 + 2 * j * TPA * 4);
-                    acc1[r] = *reinterpret_cast<const float*>(L + pi + r * TPB * 4 + (2 * j + 2) * TPA * 4);
-                }
-                if (j + 2 < XTPW) rd_in(j + 2, xi[((j >> 1) + 1) & 1]);
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int s = 0; s < XS; ++s) {
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j][s], xc[0][s], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Ai[j + 1][s], xc[1][s], acc1, 0, 0, 0);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    *reinterpret_cast<float*>(L + pi + r * TPB * 4 + 2 * j * TPA * 4) = acc0[r];
-                    *reinterpret_cast<float*>(L + pi + r * TPB * 4 + (2 * j + 2) * TPA * 4) = acc1[r];
-                }
-                asm volatile("" ::: "memory");
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // S(t)
-        if (k == 2) {
-            // ---- store-out: the 400 rows of P as 16-B pieces (1,600 pieces over the 512 compute lanes)
-            const int64_t mrow = (int64_t)(cu.M - p.m0) * p.zsm;
-            float* dxc = reinterpret_cast<float*>(p.Z) + cu.ch * XFC;
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                const int pc = (int)threadIdx.x + 512 * tt;
-                if (pc < XR * 4) {  // tt < 3: every lane; tt = 3: wave 0
-                    const int row = pc >> 2, q = pc & 3;
-                    const int a = row / XK, b = row - a * XK;
-                    f4_t v = *reinterpret_cast<const f4_t*>(L + TL_PART + (a * TPA + b * TPB + 4 * q) * 4);
-                    f4_t* dst = reinterpret_cast<f4_t*>(dxc + ((int64_t)a * p.zsa + mrow + b) * p.ldz + 4 * q);
-                    if (accumulate) v += *dst;
-                    *dst = v;
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // W(t): P read out before the next out-phase
-        if (next_mid) load_Ai(cu.M + 1);
+    for (int u0 = 0; u0 < U; u0 += 12) {
+        sub(ic<0>{}, u0);
+        sub(ic<1>{}, u0 + 1);
+        sub(ic<2>{}, u0 + 2);
+        sub(ic<3>{}, u0 + 3);
+        sub(ic<4>{}, u0 + 4);
+        sub(ic<5>{}, u0 + 5);
+        if (u0 + 6 >= U) break;
+        sub(ic<6>{}, u0 + 6);
+        sub(ic<7>{}, u0 + 7);
+        sub(ic<8>{}, u0 + 8);
+        sub(ic<9>{}, u0 + 9);
+        sub(ic<10>{}, u0 + 10);
+        sub(ic<11>{}, u0 + 11);
     }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the last chunk's rows in P (and SX)
+    store_out(nc - 1);
 }
 
+// ---------------------------------------------------------------------------------------------------------
 // Plan construction: one thread per CSR row scatters its entries into the fragment-ordered slots.
 __global__ __launch_bounds__(256) void ngram_mplan_kernel(int64_t Kn1, int64_t n_rows, const int64_t* rowptr,
                                                           const int4* edges, float* plan, int* bad) {
@@ -1171,9 +1226,9 @@ int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan
                       stream);
 }
 
-int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg, int64_t F,
-                            float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
-    const char* name = "pg_spmm3t_ngram_mid_f32";
+int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg,
+                                    int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+    const char* name = "pg_spmm3t_ngram_mid_offdiag_f32";
     int64_t Kn1 = 0, Kn2 = 0;
     PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
     PG_REQUIRE(plan && G && dX, "null pointer");
@@ -1181,7 +1236,9 @@ int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, con
     if (F <= 0 || F % XFC) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be a multiple of %d", name, XFC);
     if (!pg::aligned16(G) || !pg::aligned16(dX) || !pg::aligned16(plan) || (ldg * 4) % 16 || (lddx * 4) % 16)
         return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned G and dX rows", name);
-    PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 29), "too many column chunks");
+    PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 28), "too many column chunks");
+    if (n_rows * ldg >= (int64_t(1) << 32) || n_rows * lddx >= (int64_t(1) << 32))
+        return pg::set_error(PG_ERR_UNSUPPORTED, "%s: 32-bit per-lane element offsets", name);
     XP p{};
     p.Kn1 = Kn1;
     p.Kn2 = Kn2;
@@ -1199,18 +1256,10 @@ int pg_spmm3t_ngram_mid_f32(int K, int n, int64_t n_rows, const float* plan, con
     const int64_t total = Kn2 * p.nch;
     p.cstride = (p.nch % 2 == 0 && p.remap && total >= 2 && !(flags & PG_FLAG_MID_NO_PAIRS)) ? 2 : 1;
     p.chunks = (int)(total / p.cstride);
-    p.early_in = (flags & PG_FLAG_MID_LOADER_SYNC) ? 0 : 1;
     const int64_t cap = grid_cap();
     unsigned grid = (unsigned)(total < cap ? total : cap);
     if (p.cstride == 2) grid &= ~1u;
-    static bool attr_set = false;
-    if (!attr_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(ngram_midt_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, TL_BYTES) != hipSuccess)
-            return pg::set_error(PG_ERR_HIP, "%s: cannot raise the LDS limit", name);
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(ngram_midt_kernel, dim3(grid), dim3(XTHREADS), TL_BYTES, (hipStream_t)stream, p, accumulate ? 1 : 0);
+    hipLaunchKernelGGL(ngram_midt2_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p, accumulate ? 1 : 0);
     return pg::check_launch(name);
 }
 

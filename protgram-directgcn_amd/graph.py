@@ -56,6 +56,23 @@ class NgramPlan:
     n: int
     plan: torch.Tensor  # fp32 [pg_ngram_plan_floats(K, n, K^n)]: 4x4-block layout (transposed kernels, block-4 forward)
     mplan: Optional[torch.Tensor] = None  # fp32 [pg_ngram_mplan_floats(K, n, K^n)]: middle layout (middle-tile forward)
+    _diag3: Optional[torch.Tensor] = field(default=None, repr=False, compare=False)
+
+    def diag3(self) -> torch.Tensor:
+        """The middle plan's diagonal slots as fp32 [K^n, 3] (row i = a.M.b: Wdiag_k[a, b] of middle M, k = in, out,
+        undirected) -- the term pg_spmm3t_ngram_mid_offdiag_f32 leaves to its caller. A self-loop that is also an
+        out-neighbour (a constant n-gram) sits in its out-slot, not here. Computed once (a view of the plan)."""
+        if self._diag3 is None:
+            K = self.K
+            Kn2 = K ** (self.n - 2)
+            d = self.mplan.view(Kn2, MPLAN_FLOATS)[:, MPLAN_DIAG:MPLAN_DIAG + 3 * K * K].view(Kn2, K, K, 3)  # [M][a][b]
+            self._diag3 = d.permute(1, 0, 2, 3).reshape(K ** self.n, 3).contiguous()  # row a K^(n-1) + M K + b
+        return self._diag3
+
+
+# middle-plan layout (pg_ngram_mid.hip): floats per middle, offset of the diagonal slots [a][b][k]
+MPLAN_FLOATS = 52_400
+MPLAN_DIAG = 51_200
 
 
 # The K = 20 grid of the mapped plan: the standard amino-acid letters (any other character -- the builder's padding

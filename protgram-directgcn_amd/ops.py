@@ -351,9 +351,9 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
 
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
     """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX.
-    Same numerics note as spmm3: the n-gram tile kernels (symmetric graphs with a plan: the transposed middle-tile
-    kernel under PG_FLAG_MID_TRANSPOSED, else the 4x4-block one for F in {64, 128, 256}) need finite G and match the
-    CSR kernel within fp32 rounding; PG_FLAG_NO_NGRAM selects the CSR kernel (under AMP, GradScaler's scaled
+    Same numerics note as spmm3: the n-gram tile kernels (symmetric graphs with a plan: the off-diagonal transposed
+    middle-tile kernel + the diagonal term under PG_FLAG_MID_TRANSPOSED, else the 4x4-block one for F in
+    {64, 128, 256}) need finite G and match the CSR kernel within fp32 rounding; PG_FLAG_NO_NGRAM selects the CSR kernel (under AMP, GradScaler's scaled
     gradients can overflow to inf: the step is skipped either way, but the skipped values differ)."""
     lib = load_library()
     if _is_bf16(G):
@@ -386,11 +386,13 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     fl = default_flags() if flags is None else flags
     s = _stream(G)
     if g.shared and g.symmetric and G.size(0) == g.n_rows and (fl & _lib.PG_FLAG_MID_TRANSPOSED) and _mid_ok(g, dX, fl):
-        ng = g.ngram  # the transposed middle-tile kernel (opt-in: slower than the 4x4-block kernel)
-        rc = lib.pg_spmm3t_ngram_mid_f32(ng.K, ng.n, N, _p(ng.mplan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,
-                                         fl, s)
+        # the off-diagonal middle-tile kernel + the diagonal term here (opt-in: the extra pass over G costs what the
+        # kernel saves; training folds the diagonal into the dense backward instead, PropagateDense)
+        rc = _offdiag(lib, g, G, dX, False, fl, s)
         if rc != _lib.PG_ERR_UNSUPPORTED:
-            check(rc, "pg_spmm3t_ngram_mid_f32")
+            check(rc, "pg_spmm3t_ngram_mid_offdiag_f32")
+            d3 = g.ngram.diag3()
+            dX += (G[:, :3 * F].view(N, 3, F) * d3.unsqueeze(2)).sum(1)
             return dX
     if g.shared and g.symmetric and G.size(0) == g.n_rows and _ngram_ok(g, dX, fl, (64, 128, 256)):
         ng = g.ngram
@@ -406,6 +408,37 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
         for k, a in enumerate(g.adj):
             check(lib.pg_spmm1_f32(N, _p(a.rowptr_t), None, _p(a.edges_t), _p(G[:, k * F:]), G.stride(0), F, _p(dX),
                                    dX.stride(0), 1 if k else 0, fl, s), "pg_spmm1_f32")
+    return dX
+
+
+def _offdiag(lib, g: CSRGraph, G, dX, accumulate: bool, fl: int, s) -> int:
+    ng = g.ngram
+    return lib.pg_spmm3t_ngram_mid_offdiag_f32(ng.K, ng.n, g.n_rows, _p(ng.mplan), _p(G), G.stride(0), G.size(1) // 3,
+                                               _p(dX), dX.stride(0), 1 if accumulate else 0, fl, s)
+
+
+def spmm3t_offdiag(g: CSRGraph, G: torch.Tensor, out: Optional[torch.Tensor] = None, flags: Optional[int] = None):
+    """dX = sum_k (A_k - Diag_k) G_k (+ out when given: accumulated into it) by the off-diagonal transposed middle-tile
+    kernel (pg_spmm3t_ngram_mid_offdiag_f32; fp32, a complete n-gram graph with a middle plan, F % 16 == 0);
+    Diag_k = g.ngram.diag3()[:, k]. None when the kernel does not take the call (the caller then runs spmm3_t)."""
+    lib = load_library()
+    if _is_bf16(G) or not (g.shared and g.symmetric and g.ngram is not None and g.ngram.mplan is not None):
+        return None
+    G = _f32c(G)
+    _require_gpu(G)
+    _require_graph_on(g, G)
+    N, F = g.n_rows, G.size(1) // 3
+    if G.size(0) != N or F % 16:
+        return None
+    acc = out is not None
+    dX = out if acc else torch.empty(N, F, device=G.device, dtype=torch.float32)
+    if dX.dtype != torch.float32 or dX.shape != (N, F) or dX.stride(1) != 1:
+        raise ValueError("spmm3t_offdiag: out must be fp32 [N, F] with unit column stride")
+    fl = default_flags() if flags is None else flags
+    rc = _offdiag(lib, g, G, dX, acc, fl, _stream(G))
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_spmm3t_ngram_mid_offdiag_f32")
     return dX
 
 

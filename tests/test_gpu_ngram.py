@@ -77,32 +77,37 @@ def test_ngram_spmm3_vs_csr(pkg, cuda, n, keep, F):
 @pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
 @pytest.mark.parametrize("F", [16, 48, 64, 128, 256])
 def test_ngram_spmm3t_vs_csr(pkg, cuda, n, keep, F):
-    """The transposed middle-tile kernel (PG_FLAG_MID_TRANSPOSED; F % 16 == 0, odd chunk counts run without
-    workgroup pairs; both loader protocols) and the 4x4-block transposed kernel (default) against the CSR kernel; the
-    middle-tile kernel's accumulate mode."""
+    """The off-diagonal transposed middle-tile kernel (F % 16 == 0; odd chunk counts run without workgroup pairs) plus
+    the plan's diagonal term (PG_FLAG_MID_TRANSPOSED), and the 4x4-block transposed kernel (default), against the CSR
+    kernel; the off-diagonal kernel alone against the CSR result minus the diagonal term, its accumulate mode on a
+    strided G view, and determinism."""
     from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_MID_LOADER_SYNC, PG_FLAG_MID_TRANSPOSED, load_library
+    from protgram_directgcn_amd._lib import PG_FLAG_MID_NO_PAIRS, PG_FLAG_MID_TRANSPOSED
     g = _graph(pkg, cuda, n, keep)
     assert g.ngram is not None and g.symmetric
-    G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(F)).to(cuda)
+    N = g.n_rows
+    G = torch.randn(N, 3 * F, generator=torch.Generator().manual_seed(F)).to(cuda)
     ref = ops.spmm3_t(g, G, flags=_csr_flag())
     mid = ops.default_flags() | PG_FLAG_MID_TRANSPOSED
     got = ops.spmm3_t(g, G, flags=mid)
     assert_close(got, ref, f"transposed middle-tile n={n} F={F}")
-    assert torch.equal(ops.spmm3_t(g, G, flags=mid), got)  # deterministic
-    assert torch.equal(ops.spmm3_t(g, G, flags=mid | PG_FLAG_MID_LOADER_SYNC), got)  # loader protocol: speed only
     if F in (64, 128, 256):
         assert_close(ops.spmm3_t(g, G), ref, f"block4 (default) n={n} F={F}")
-    # accumulate: dX += A^T G through the C ABI, on a strided G view
-    lib = load_library()
-    Gw = torch.randn(g.n_rows, 3 * F + 16, generator=torch.Generator().manual_seed(7)).to(cuda)
+    # the off-diagonal part alone: ref minus sum_k Diag_k G_k
+    d3 = g.ngram.diag3()
+    assert d3.shape == (N, 3)
+    diag = (G.view(N, 3, F) * d3.unsqueeze(2)).sum(1)
+    off = ops.spmm3t_offdiag(g, G)
+    assert off is not None
+    assert_close(off + diag, ref, f"off-diagonal + diagonal n={n} F={F}")
+    assert torch.equal(ops.spmm3t_offdiag(g, G), off)  # deterministic
+    assert torch.equal(ops.spmm3t_offdiag(g, G, flags=ops.default_flags() | PG_FLAG_MID_NO_PAIRS), off)  # schedule only
+    # accumulate on a strided G view: out += offdiag
+    Gw = torch.randn(N, 3 * F + 16, generator=torch.Generator().manual_seed(7)).to(cuda)
     Gw[:, :3 * F] = G
-    dX = torch.randn(g.n_rows, F, generator=torch.Generator().manual_seed(8)).to(cuda)
-    want = dX + ref
-    ng = g.ngram
-    rc = lib.pg_spmm3t_ngram_mid_f32(ng.K, ng.n, g.n_rows, ng.mplan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
-                                     dX.data_ptr(), dX.stride(0), 1, ops.default_flags(), ops._stream(dX))
-    assert rc == 0
+    dX = torch.randn(N, F, generator=torch.Generator().manual_seed(8)).to(cuda)
+    want = dX + off
+    assert ops.spmm3t_offdiag(g, Gw[:, :3 * F], out=dX) is dX
     assert_close(dX, want, f"accumulate n={n} F={F}")
 
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Time the propagation kernels at B(20,n), F: n-gram tile forward (default / LDS-weight variant), the CSR window
 kernel, and the transposed kernels (min of interleaved rounds, HIP events), plus a max-|d| check vs the CSR result.
+Transposed: the 4x4-block kernel (default), the off-diagonal middle-tile kernel (alone, accumulating, and with the
+diagonal term on the host under PG_FLAG_MID_TRANSPOSED) and the CSR kernel.
 usage: python tools/ngram_probe_k.py [n=4] [F=128] [reps=20]"""
 import os
 import sys
@@ -25,6 +27,7 @@ g = pkg.build_propagation_csr(N, s, d, c, device=dev)
 assert g.ngram is not None
 x = torch.randn(N, F, device=dev)
 G = torch.randn(N, 3 * F, device=dev)
+dXa = torch.zeros(N, F, device=dev)
 
 
 def timeit(fn):
@@ -50,8 +53,8 @@ cases = {"fwd_ngram": lambda: ops.spmm3(g, x), "gated_ngram": lambda: ops.spmm3_
          "fwd_sync": lambda: ops.spmm3(g, x, flags=ops.default_flags() | PG_FLAG_MID_LOADER_SYNC),
          "bwd_ngram": lambda: ops.spmm3_t(g, G),
          "bwd_mid": lambda: ops.spmm3_t(g, G, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED),
-         "bwd_mid_sync": lambda: ops.spmm3_t(g, G, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED
-                                             | PG_FLAG_MID_LOADER_SYNC),
+         "bwd_offdiag": lambda: ops.spmm3t_offdiag(g, G),
+         "bwd_offdiag_acc": lambda: ops.spmm3t_offdiag(g, G, out=dXa),
          "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
 for a in ALT:
     cases[f"fwd_alt{a:#x}"] = (lambda a: lambda: ops.spmm3(g, x, flags=a))(a)
@@ -78,3 +81,7 @@ for k in [c for c in ("gated_ngram", "gated_block4") if c in cases]:
 comp = g.compulsory_bytes(F)
 print(" ".join(f"{k}={v:.4f}ms" for k, v in best.items()), f"compulsory_fwd={comp / 1e6:.1f}MB "
       f"-> {comp / best['fwd_ngram'] / 1e6:.0f} GB/s")
+if "bwd_offdiag" in best:  # its algorithmic bytes: G read twice (out- and in-sources), dX written, the plan once
+    ob = 2 * N * 3 * F * 4 + N * F * 4 + g.ngram.mplan.numel() * 4
+    print(f"offdiag bytes {ob / 1e6:.1f}MB -> {ob / best['bwd_offdiag'] / 1e6:.0f} GB/s; "
+          f"with accumulate +{N * F * 4 / 1e6:.1f}MB")

@@ -231,3 +231,23 @@ def test_protein_sequences_seeded(pkg):
     assert a == pkg.synth.protein_sequences(5, 40, seed=3, rare=0.2)
     assert all(20 <= len(s) <= 60 for s in a)
     assert set("".join(a)) <= set(pkg.synth.ALPHABET + "XUBZ") and set("".join(a)) & set("XUBZ")
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_ngram_plan_diag3_layout(pkg, n):
+    """NgramPlan.diag3: row i = a K^(n-1) + M K + b of the [K^n, 3] result is the middle plan's diagonal slot
+    [a][b][k] of middle M (the layout pg_ngram_mplan_f32 writes, offset MPLAN_DIAG of each MPLAN_FLOATS block)."""
+    from protgram_directgcn_amd import graph as gr
+    K = 20
+    Kn2, Kn1 = K ** (n - 2), K ** (n - 1)
+    plan = torch.full((Kn2, gr.MPLAN_FLOATS), -1.0)
+    M, a, b, k = np.meshgrid(np.arange(Kn2), np.arange(K), np.arange(K), np.arange(3), indexing="ij")
+    code = torch.from_numpy((((M * K + a) * K + b) * 3 + k).astype(np.float32))  # exact in fp32 up to 2^24
+    plan[:, gr.MPLAN_DIAG:gr.MPLAN_DIAG + 3 * K * K] = code.reshape(Kn2, 3 * K * K)
+    d3 = gr.NgramPlan(K, n, torch.zeros(1), plan.reshape(-1)).diag3()
+    assert d3.shape == (K ** n, 3)
+    rng = np.random.default_rng(n)
+    for i in rng.integers(0, K ** n, 200).tolist() + [0, K ** n - 1]:
+        ai, Mi, bi = i // Kn1, (i % Kn1) // K, i % K
+        for kk in range(3):
+            assert d3[i, kk].item() == ((Mi * K + ai) * K + bi) * 3 + kk, (i, kk)

@@ -90,9 +90,9 @@ typedef struct pg_edge1 {
                                              between the MFMA k-steps (the default); same results */
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
-#define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the off-diagonal transposed middle-tile kernel
-                                             (pg_spmm3t_ngram_mid_offdiag_f32) plus the diagonal term on the host,
-                                             instead of the 4x4-block kernel */
+#define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernels instead of the
+                                             4x4-block ones: fp32 pg_spmm3t_ngram_mid_offdiag_f32 plus the diagonal
+                                             term on the host, bf16 pg_spmm3t_ngram_mid_bf16 */
 
 /* `row_order` (all SpMM entry points): optional int32 [n_rows] permutation giving the order in which
  * destination rows are processed (position p handles row row_order[p]; NULL = 0..n_rows-1). It changes
@@ -302,6 +302,13 @@ int pg_spmm3_resid_f32(int64_t n_list, const int64_t* rowptr, const int32_t* row
  * otherwise. Numerics: within fp32 rounding of the CSR kernel; G must be finite. */
 int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg,
                                     int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+/* bf16 transposed middle-tile kernel, the FULL product (diagonal included): dX (+)= sum_k A_k G[:, kF:(k+1)F] on bf16
+ * G and dX rows (fp32 weights and sums, dX rounded once, RNE; the same product as pg_spmm3t_ngram_bf16 on graphs over
+ * all K^n n-grams, which stays ops.spmm3_t's default: this kernel measured slower). The half-size rows leave
+ * LDS room for each slice's own rows, so the diagonal term costs a third read of G but no caller work. Same shape /
+ * alignment rules as the fp32 kernel (16-B aligned bf16 rows). */
+int pg_spmm3t_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
+                             uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
 /* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
  * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).

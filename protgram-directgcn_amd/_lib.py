@@ -97,6 +97,8 @@ SIGNATURES = {
                                            ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_mid_offdiag_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,
                                                        c_vp, c_i64, ctypes.c_int, c_u32, c_vp]),
+    "pg_spmm3t_ngram_mid_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                                ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                             ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,

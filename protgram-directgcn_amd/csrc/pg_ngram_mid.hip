@@ -570,30 +570,45 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Transposed middle-tile kernel, OFF-DIAGONAL part (pg_spmm3t_ngram_mid_offdiag_f32): the backward of the forward above
-// for the symmetric n-gram matrices (A_k^T = A_k; the autograd of protgram_directgcn.py:101-112) without its diagonal
-// term, with G_k = G[:, kF:(k+1)F]:
-//   dX[a.M.b, f] (+)= sum_k ( sum_c Wout_k[a,b,c] G_k[M.b.c, f] + sum_c Win_k[a,b,c] G_k[c.a.M, f] )
-// Why without the diagonal: the out-sources of middle M are the rows with prefix M, its in-sources the rows with
-// suffix M and its own rows those with middle M -- three disjoint sets, so the diagonal term sum_k Wdiag_k G_k[a.M.b]
-// would be a THIRD read of every G row (the 4x4-block kernel's 1,057 MB per launch). The dense backward adds it
-// instead, while it holds G in registers (pg_directgcn_dense_bwd_f32 with diagonal weights; ops.PropagateDense).
+// Transposed middle-tile kernel: the backward of the forward above for the symmetric n-gram matrices (A_k^T = A_k; the
+// autograd of protgram_directgcn.py:101-112), with G_k = G[:, kF:(k+1)F]:
+//   dX[a.M.b, f] (+)= sum_k ( sum_c Wout_k[a,b,c] G_k[M.b.c, f] + sum_c Win_k[a,b,c] G_k[c.a.M, f]
+//                             [+ Wdiag_k[a,b] G_k[a.M.b, f]] )
+// fp32 (pg_spmm3t_ngram_mid_offdiag_f32): WITHOUT the bracketed diagonal term. The out-sources of middle M are the rows
+// with prefix M, its in-sources the rows with suffix M and its own rows those with middle M -- three disjoint sets, so
+// the diagonal term is a THIRD read of every G row (the 4x4-block kernel's 1,057 MB per launch), and at fp32 one
+// slice's own rows (25.6 KB) do not fit beside the ring; the caller adds it (NgramPlan.diag3).
+// bf16 (pg_spmm3t_ngram_mid_bf16: bf16 G and dX rows, fp32 weights and sums, dX rounded once): the full product. Half-
+// size rows leave room for slice k's own rows in the out-sub-phase's slot beside its out-sources; they are added
+// after that slice's out-MFMAs with the middle's diagonal weights (LDS, loaded at each middle change).
 //
 // Per (middle, 16-feature chunk) six sub-phases, one slice G_k each:
 //   out k = 0, 1, 2: tiles (b, m), rows a = 16 m + 0..15 (20 valid), K-dim (k, c): 5 MFMA k-steps per slice, the
 //                    accumulators kept across the three slices and handed over as P[a][b][16 f] (LDS) after k = 2;
 //   in  k = 0, 1, 2: tiles (a, m), rows b, started from P after k = 0's barrier; the finished rows go back to P and
 //                    leave for HBM (16-B pieces) in the next chunk's first sub-phase.
-// Every wave computes AND issues the LDS-DMA (no loader waves): one slice's source rows per sub-phase (out: 400 x 64 B,
-// in: 420 x 64 B with the pad rows) into a ring of four slots, three sub-phases ahead, one barrier per sub-phase. Wave w
-// owns the row tile m = w & 1 of the columns b (out) / a (in) = (w >> 1) + 4 j, j = 0..4; its A fragments, gathered
-// from the forward plan (rows (k, a) -> a, K-dim c -> (k, c)), stay in registers per middle: 75 out + 75 in per lane
-// (8 waves, 2 per SIMD: up to 256 VGPRs), the next middle's fetched a slice at a time three sub-phases before use.
+// Every wave computes AND issues the LDS-DMA (no loader waves): one slice's source rows per sub-phase (out: 400 rows,
+// in: 420 with the pad rows; 64-B row chunks fp32, 32-B bf16) into a ring of four slots, three sub-phases ahead, one
+// barrier per sub-phase. Wave w owns the row tile m = w & 1 of the columns b (out) / a (in) = (w >> 1) + 4 j, j = 0..4;
+// its A fragments, gathered from the forward plan (rows (k, a) -> a, K-dim c -> (k, c)), stay in registers per middle:
+// 75 out + 75 in per lane (8 waves, 2 per SIMD: up to 256 VGPRs), reloaded at a middle change.
 // The four slots and P are separate LDS objects, and the sub-phase loop is unrolled by 12 (= lcm of 6 sub-phases per
 // chunk and 4 slots), so every slot a DMA writes and every slot a read uses is known at compile time.
-constexpr int T2_SLOT = 27 * 1024;                     // ring slot: one slice's in-sources (420 rows x 64 B) rounded
-constexpr int T2_NOUT = XR * 64 / 1024;                // 25 wave-instructions of out-source pieces per slice
+constexpr int T2_SLOT = 27 * 1024;                     // ring slot: fp32 one slice's in-sources (420 rows x 64 B);
+                                                       // bf16 out-sources (13 KiB) + own rows (13 KiB) of a slice
+constexpr int T2_NOUT = XR * 64 / 1024;                // fp32: 25 wave-instructions of out-source pieces per slice
 constexpr int T2_NIN = (XK * XCB * 64 + 1023) / 1024;  // 27 of in-source pieces (the last one partly padding)
+template <bool BF>
+struct T2L {
+    static constexpr int ES = BF ? 2 : 4;                       // bytes per G / dX element
+    static constexpr int RB = XFC * ES;                         // bytes per row chunk
+    static constexpr int PPR = RB / 16, EPP = 16 / ES;          // 16-B pieces per row chunk, elements per piece
+    static constexpr int NO = (XR * RB + 1023) / 1024;          // wave-instructions per out / own-row / stage slice
+    static constexpr int NI = (XK * XCB * RB + 1023) / 1024;    // per in slice
+    static constexpr int SELF = NO * 1024;                      // bf16: own rows after the out-sources in the slot
+};
+static_assert(T2L<true>::NO == 13 && T2L<true>::NI == 14 && 2 * T2L<true>::SELF <= T2_SLOT, "bf16 slot");
+static_assert(T2L<false>::NO == T2_NOUT && T2L<false>::NI == T2_NIN, "fp32 slot");
 constexpr int T2_PB = XFC, T2_PA = XK * T2_PB;        // P[a][b][16 f] (dwords; the 2-way conflicts of its 40 ops per
                                                        // wave and chunk cost less than the padding's LDS)
 constexpr int T2_TPW = 5;                              // tiles per wave per sub-phase
@@ -631,13 +646,18 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
 }
 
+template <bool BF>
 __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) {
+    using C = T2L<BF>;
+    constexpr int ES = C::ES, RB = C::RB, PPR = C::PPR, EPP = C::EPP;
+    using ET = std::conditional_t<BF, uint16_t, float>;
     __shared__ __attribute__((aligned(16))) float S0[T2_SLOT / 4];
     __shared__ __attribute__((aligned(16))) float S1[T2_SLOT / 4];
     __shared__ __attribute__((aligned(16))) float S2[T2_SLOT / 4];
     __shared__ __attribute__((aligned(16))) float S3[T2_SLOT / 4];
     __shared__ __attribute__((aligned(16))) float Pb[XK * T2_PA];
-    __shared__ __attribute__((aligned(16))) float SX[XR * XFC];  // accumulate: the chunk's dX rows, staged by LDS-DMA
+    __shared__ __attribute__((aligned(16))) float SX[C::NO * 256];  // accumulate: the chunk's dX rows (LDS-DMA, whole instructions)
+    __shared__ __attribute__((aligned(16))) float Dg[BF ? XR * 3 : 4];  // bf16: the middle's diagonal weights [a][b][k]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // the forward's chunk ranges and workgroup pairs (see ngram_mid_kernel)
@@ -654,33 +674,30 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
     const int q = lane >> 4, fl = lane & 15;
     const int mt = wave & 1, grp = wave >> 1;
     const int64_t ldg = p.ldx;
-    const float* __restrict__ G = reinterpret_cast<const float*>(p.X);
+    const ET* __restrict__ G = reinterpret_cast<const ET*>(p.X);
 
     // LDS-DMA: wave-instruction it = wave + 8 t of a slice (piece it * 64 + lane, lane-linear in the slot); the per-lane
-    // element offsets do not depend on the middle, chunk or slice
-    // element offsets < 2^32 (the host checks n_rows * ldg): 32-bit per lane, added to a wave-uniform base
-    uint32_t off_o[4], off_i[4];
+    // element offsets do not depend on the middle, chunk or slice; < 2^32 (the host checks n_rows * ldg): 32-bit per
+    // lane, added to a wave-uniform base. Pieces past a slice's last row read a valid row into the slot's padding.
+    uint32_t off_o[4], off_i[4], off_s[4], off_x[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const int pc = (wave + 8 * t) * 64 + lane, rl = pc >> 2, qq = pc & 3;
-        off_o[t] = (uint32_t)(rl < XR ? rl : 0) * (uint32_t)ldg + 4 * qq;  // out: row M K^2 + rl (= M.b.c)
-        const int c = rl / XCB, a = rl - c * XCB;                          // in: row c.a.M; pad pieces read row M
-        off_i[t] = (a >= XK || c >= XK) ? 4 * qq
-                                        : (uint32_t)(c * (uint32_t)p.Kn1 + a * (uint32_t)p.Kn2) * (uint32_t)ldg + 4 * qq;
+        const int pc = (wave + 8 * t) * 64 + lane, rl = pc / PPR, qq = (pc % PPR) * EPP;
+        const int ro = rl < XR ? rl : 0;
+        off_o[t] = (uint32_t)ro * (uint32_t)ldg + qq;                              // out: row M K^2 + rl (= M.b.c)
+        const int c = rl / XCB, a = rl - c * XCB;                                  // in: row c.a.M; pad pieces: row M
+        off_i[t] = (a >= XK || c >= XK) ? qq
+                                        : (uint32_t)(c * (uint32_t)p.Kn1 + a * (uint32_t)p.Kn2) * (uint32_t)ldg + qq;
+        const int sa = ro / XK, sb = ro - sa * XK;                                 // own: row a.M.b (bf16)
+        off_s[t] = (uint32_t)(sa * (uint32_t)p.Kn1 + sb) * (uint32_t)ldg + qq;
+        off_x[t] = (uint32_t)(sa * (uint32_t)p.zsa + sb) * (uint32_t)p.ldz + qq;   // accumulate: dX row a.M.b
     }
-    const int n_out = wave < T2_NOUT - 24 ? 4 : 3, n_in = wave < T2_NIN - 24 ? 4 : 3;
-    // accumulate: the dX pieces of a chunk (row a.M.b, 16-B piece q4), in the store-out's order
-    uint32_t off_x[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const int pc = min((wave + 8 * t) * 64 + lane, XR * 4 - 1), row = pc >> 2, a = row / XK, b = row - a * XK;
-        off_x[t] = (uint32_t)(a * (uint32_t)p.zsa + b) * (uint32_t)p.ldz + 4 * (pc & 3);
-    }
+    const int n_out = (C::NO - wave + 7) / 8, n_in = (C::NI - wave + 7) / 8;      // this wave's instructions per slice
     auto dma_x = [&](int c) {
-        const float* base = reinterpret_cast<const float*>(p.Z) + (int64_t)(mid_of(c) - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
+        const ET* base = reinterpret_cast<const ET*>(p.Z) + (int64_t)(mid_of(c) - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-            if (t < n_out) glds16_asm(base + off_x[t], lds_addr(SX) + (wave + 8 * t) * 1024);
+            if (t < n_out) glds16_asm(reinterpret_cast<const float*>(base + off_x[t]), lds_addr(SX) + (wave + 8 * t) * 1024);
     };
     auto slot = [&](auto sc) -> float* {
         constexpr int S = decltype(sc)::value;
@@ -691,20 +708,29 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
     };
     auto dma = [&](float* dst, int c, int j) {  // sub-phase (chunk c, j): slice k = j mod 3 of the out / in sources
         const int M = mid_of(c), k = j < 3 ? j : j - 3;
-        const float* base = G + (int64_t)k * p.F + ch_of(c) * XFC;
+        const ET* base = G + (int64_t)k * p.F + ch_of(c) * XFC;
         if (j < 3) {
-            base += (int64_t)M * XR * ldg;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (t < n_out) glds16_asm(base + off_o[t], lds_addr(dst) + (wave + 8 * t) * 1024);
+                if (t < n_out)
+                    glds16_asm(reinterpret_cast<const float*>(base + (int64_t)M * XR * ldg + off_o[t]),
+                               lds_addr(dst) + (wave + 8 * t) * 1024);
+            if constexpr (BF) {  // the slice's own rows a.M.b beside them
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (t < n_out)
+                        glds16_asm(reinterpret_cast<const float*>(base + (int64_t)M * XK * ldg + off_s[t]),
+                                   lds_addr(dst) + C::SELF + (wave + 8 * t) * 1024);
+            }
         } else {
-            base += (int64_t)M * ldg;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (t < n_in) glds16_asm(base + off_i[t], lds_addr(dst) + (wave + 8 * t) * 1024);
+                if (t < n_in)
+                    glds16_asm(reinterpret_cast<const float*>(base + (int64_t)M * ldg + off_i[t]),
+                               lds_addr(dst) + (wave + 8 * t) * 1024);
         }
     };
-
+    const int n_dma_out = (BF ? 2 : 1) * n_out;  // pieces of an out-sub-phase's DMA (bf16: + the own rows)
     // A fragments: Wo[j][5 k + s] (tile b = grp + 4 j, m = mt): lane holds A[a = 16 mt + fl][c = 4 s + q] of slice k
     // = Wout_k[a, b, c], in the forward plan at out fragment (b, row (k, a) = 20 k + a, c). Wi likewise with (a, b)
     // exchanged (tile a = grp + 4 j, rows b = 16 mt + fl). Rows past 19 load row 19's weights: an MFMA row only feeds
@@ -732,8 +758,12 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
     const bool prow = mt == 0 || q == 0;  // accumulator rows 16 mt + 4 q + r < 20
     const int p_out = opaque((((16 * mt + 4 * q) * T2_PA + grp * T2_PB + fl) * 4));  // P[a][b]: + (r T2_PA + 4 j T2_PB) 4
     const int p_in = opaque(((grp * T2_PA + (16 * mt + 4 * q) * T2_PB + fl) * 4));   // P[a][b]: + (4 j T2_PA + r T2_PB) 4
-    const int b_out = opaque(((grp * XK + q) * XFC + fl) * 4);   // out-source (b = grp + 4j, c = 4 s + q): + (4 j K + 4 s) 64
-    const int b_in = opaque(((q * XCB + grp) * XFC + fl) * 4);   // in-source (c = 4 s + q, a = grp + 4j): + (4 s XCB + 4 j) 64
+    const int b_out = opaque(((grp * XK + q) * XFC + fl) * ES);  // out-source (b = grp + 4j, c = 4 s + q): + (4 j K + 4 s) RB
+    const int b_in = opaque(((q * XCB + grp) * XFC + fl) * ES);  // in-source (c = 4 s + q, a = grp + 4j): + (4 s XCB + 4 j) RB
+    // bf16 own-row term: own row (a = 16 mt + 4 q + r, b = grp + 4 j) of the slot's second half, + (r K + 4 j) RB; its
+    // diagonal weight Dg[(a K + b) 3 + k], + ((r K + 4 j) 3 + k) 4
+    [[maybe_unused]] const int b_self = opaque(C::SELF + (((16 * mt + 4 * q) * XK + grp) * XFC + fl) * ES);
+    [[maybe_unused]] const int d_self = opaque((((16 * mt + 4 * q) * XK + grp) * 3) * 4);
     char* const P8 = reinterpret_cast<char*>(Pb);
     auto out_sub = [&](const float* sl, auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -746,10 +776,22 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
         for (int s = 0; s < XS; ++s) {
             float bv[T2_TPW];
 #pragma unroll
-            for (int j = 0; j < T2_TPW; ++j) bv[j] = *reinterpret_cast<const float*>(sb + (4 * j * XK + 4 * s) * 64);
+            for (int j = 0; j < T2_TPW; ++j) bv[j] = lds_src<BF>(sb + (4 * j * XK + 4 * s) * RB);
 #pragma unroll
             for (int j = 0; j < T2_TPW; ++j)
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wo[j][5 * k + s], bv[j], acc[j], 0, 0, 0);
+        }
+        if constexpr (BF) {  // + Wdiag_k[a, b] G_k[a.M.b, f] (rows a < 20)
+            if (prow) {
+                const char* ss = reinterpret_cast<const char*>(sl) + b_self;
+                const char* dd = reinterpret_cast<const char*>(Dg) + d_self;
+#pragma unroll
+                for (int j = 0; j < T2_TPW; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[j][r] = __builtin_fmaf(*reinterpret_cast<const float*>(dd + ((r * XK + 4 * j) * 3 + k) * 4),
+                                                   lds_src<true>(ss + (r * XK + 4 * j) * RB), acc[j][r]);
+            }
         }
         if constexpr (k == 2) {
             if (prow) {
@@ -778,7 +820,7 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
         for (int s = 0; s < XS; ++s) {
             float bv[T2_TPW];
 #pragma unroll
-            for (int j = 0; j < T2_TPW; ++j) bv[j] = *reinterpret_cast<const float*>(sb + (4 * s * XCB + 4 * j) * 64);
+            for (int j = 0; j < T2_TPW; ++j) bv[j] = lds_src<BF>(sb + (4 * s * XCB + 4 * j) * RB);
 #pragma unroll
             for (int j = 0; j < T2_TPW; ++j)
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Wi[j][5 * k + s], bv[j], acc[j], 0, 0, 0);
@@ -798,16 +840,35 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
     const int n_st = wave == 0 ? 4 : 3;  // vector-memory operations it issues
     auto store_out = [&](int c) {
         const int M = mid_of(c);
-        float* dx = reinterpret_cast<float*>(p.Z) + (int64_t)(M - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
+        ET* dx = reinterpret_cast<ET*>(p.Z) + (int64_t)(M - p.m0) * p.zsm * p.ldz + ch_of(c) * XFC;
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) {
             const int pc = tid + 512 * tt;
             if (tt < 3 || wave == 0) {  // pc < 1,600
                 const int row = pc >> 2, a = row / XK, b = row - a * XK, q4 = pc & 3;
                 f4_t v = *reinterpret_cast<const f4_t*>(P8 + (a * T2_PA + b * T2_PB + 4 * q4) * 4);
-                if (accumulate) v += *reinterpret_cast<const f4_t*>(reinterpret_cast<const char*>(SX) + pc * 16);
-                *reinterpret_cast<f4_t*>(dx + ((int64_t)a * p.zsa + b) * p.ldz + 4 * q4) = v;
+                ET* dst = dx + ((int64_t)a * p.zsa + b) * p.ldz + 4 * q4;
+                if constexpr (BF) {  // fp32 sums, one rounding (RNE)
+                    if (accumulate) {
+                        const uint2 o = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(SX) + pc * 8);
+                        v[0] += pgbf::lo(o.x);
+                        v[1] += pgbf::hi(o.x);
+                        v[2] += pgbf::lo(o.y);
+                        v[3] += pgbf::hi(o.y);
+                    }
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(pgbf::pack2(v[0], v[1]), pgbf::pack2(v[2], v[3]));
+                } else {
+                    if (accumulate) v += *reinterpret_cast<const f4_t*>(reinterpret_cast<const char*>(SX) + pc * 16);
+                    *reinterpret_cast<f4_t*>(dst) = v;
+                }
             }
+        }
+    };
+    // bf16: the middle's diagonal weights into Dg (1,200 floats = 300 16-B pieces; plain loads, waited for by the caller)
+    auto load_diag = [&](int M) {
+        if constexpr (BF) {
+            if (tid < XR * 3 / 4)
+                reinterpret_cast<float4*>(Dg)[tid] = reinterpret_cast<const float4*>(p.plan + (int64_t)M * XMB + XPD)[tid];
         }
     };
 
@@ -820,11 +881,12 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
         gather(ic<0>{}, ic<1>{}, M);
         gather(ic<1>{}, ic<1>{}, M);
         gather(ic<2>{}, ic<1>{}, M);
+        load_diag(M);
         dma(S0, 0, 0);
         dma(S1, 0, 1);
         dma(S2, 0, 2);
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights (hipcc sees this wait) and the DMA
-    }
+    }  // (Dg is published by the first sub-phase's barrier)
     // vector-memory operations per sub-phase block, in issue order: [accumulate stage pieces] [DMA of sub-phase u + 3]
     // [stores, weights]; blk = all of them, aft = those after the DMA
     int blk[4] = {0, 0, 0, 0}, aft[4] = {0, 0, 0, 0};
@@ -845,7 +907,7 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
         // slot (S + 3) % 4 was read by sub-phase u - 1, which every wave has finished: sub-phase u + 3's slice
         if (u + 3 < U) {
             dma(slot(ic<(S + 3) % 4>{}), (u + 3) / 6, (J + 3) % 6);
-            n += (J + 3) % 6 < 3 ? n_out : n_in;
+            n += (J + 3) % 6 < 3 ? n_dma_out : n_in;
         }
         asm volatile("" ::: "memory");  // nothing below moves above the DMA
         if constexpr (J == 0) {
@@ -861,7 +923,13 @@ __global__ __launch_bounds__(512) void ngram_midt2_kernel(XP p, int accumulate) 
                     gather(ic<0>{}, ic<1>{}, M);
                     gather(ic<1>{}, ic<1>{}, M);
                     gather(ic<2>{}, ic<1>{}, M);
-                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+                    if constexpr (BF) {  // the new middle's diagonal weights (the old ones' last use was u - 1)
+                        load_diag(M);
+                        __builtin_amdgcn_s_waitcnt(0x0F70);
+                        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // uniform branch
+                    } else {
+                        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+                    }
                 }
             }
         }
@@ -1226,15 +1294,19 @@ int pg_spmm3_ngram_mid_rows_bf16(int K, int n, int64_t n_rows, const float* plan
                       stream);
 }
 
-int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg,
-                                    int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
-    const char* name = "pg_spmm3t_ngram_mid_offdiag_f32";
+}  // extern "C"
+
+// the transposed middle-tile launch (fp32: off-diagonal part; bf16: the full product)
+static int midt_launch(int K, int n, int64_t n_rows, const float* plan, const void* G, int64_t ldg, int64_t F, void* dX,
+                       int64_t lddx, int accumulate, uint32_t flags, void* stream, bool bf) {
+    const char* name = bf ? "pg_spmm3t_ngram_mid_bf16" : "pg_spmm3t_ngram_mid_offdiag_f32";
     int64_t Kn1 = 0, Kn2 = 0;
     PG_REQUIRE(mid_shape(K, n, n_rows, Kn1, Kn2), "bad n-gram shape (K must be %d, n_rows = K^n)", XK);
     PG_REQUIRE(plan && G && dX, "null pointer");
     PG_REQUIRE(ldg >= 3 * F && lddx >= F, "leading dimensions too small");
     if (F <= 0 || F % XFC) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: F must be a multiple of %d", name, XFC);
-    if (!pg::aligned16(G) || !pg::aligned16(dX) || !pg::aligned16(plan) || (ldg * 4) % 16 || (lddx * 4) % 16)
+    const int64_t es = bf ? 2 : 4;
+    if (!pg::aligned16(G) || !pg::aligned16(dX) || !pg::aligned16(plan) || (ldg * es) % 16 || (lddx * es) % 16)
         return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned G and dX rows", name);
     PG_REQUIRE(Kn2 * (F / XFC) < (int64_t(1) << 28), "too many column chunks");
     if (n_rows * ldg >= (int64_t(1) << 32) || n_rows * lddx >= (int64_t(1) << 32))
@@ -1259,8 +1331,22 @@ int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* p
     const int64_t cap = grid_cap();
     unsigned grid = (unsigned)(total < cap ? total : cap);
     if (p.cstride == 2) grid &= ~1u;
-    hipLaunchKernelGGL(ngram_midt2_kernel, dim3(grid), dim3(512), 0, (hipStream_t)stream, p, accumulate ? 1 : 0);
+    const int acc = accumulate ? 1 : 0;
+    if (bf) hipLaunchKernelGGL(ngram_midt2_kernel<true>, dim3(grid), dim3(512), 0, (hipStream_t)stream, p, acc);
+    else hipLaunchKernelGGL(ngram_midt2_kernel<false>, dim3(grid), dim3(512), 0, (hipStream_t)stream, p, acc);
     return pg::check_launch(name);
+}
+
+extern "C" {
+
+int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* plan, const float* G, int64_t ldg,
+                                    int64_t F, float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+    return midt_launch(K, n, n_rows, plan, G, ldg, F, dX, lddx, accumulate, flags, stream, false);
+}
+
+int pg_spmm3t_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
+                             uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream) {
+    return midt_launch(K, n, n_rows, plan, G, ldg, F, dX, lddx, accumulate, flags, stream, true);
 }
 
 #ifdef PG_MID_STAMPS

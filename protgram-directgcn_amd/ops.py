@@ -365,6 +365,15 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
             dX = torch.empty(N, F, device=G.device, dtype=torch.bfloat16)
             ro = g.row_order if g.symmetric else None
             fl = default_flags() if flags is None else flags
+            if g.symmetric and G.size(0) == g.n_rows and (fl & _lib.PG_FLAG_MID_TRANSPOSED) and _mid_ok(g, dX, fl):
+                # the transposed middle-tile kernel, diagonal included (bf16 rows leave it room); opt-in: slower than the
+                # 4x4-block bf16 kernel (0.164 vs 0.112 ms at B(20,4), F = 128)
+                ng = g.ngram
+                rc = lib.pg_spmm3t_ngram_mid_bf16(ng.K, ng.n, N, _p(ng.mplan), _p(G), G.stride(0), F, _p(dX),
+                                                  dX.stride(0), 0, fl, _stream(G))
+                if rc != _lib.PG_ERR_UNSUPPORTED:
+                    check(rc, "pg_spmm3t_ngram_mid_bf16")
+                    return dX
             if g.symmetric and G.size(0) == g.n_rows and _ngram_ok(g, dX, fl, (64, 128, 256), torch.bfloat16):
                 ng = g.ngram
                 rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, N, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 0,

@@ -132,18 +132,41 @@ def test_ngram_spmm3_vs_oracle_and_fallback_widths(pkg, cuda):
                 assert_close(Z[:, j * F:(j + 1) * F], ref, f"oracle {j}")
 
 
-@pytest.mark.parametrize("n,keep", [(3, 1.0), (3, 0.5), (4, 1.0)])
-@pytest.mark.parametrize("F", [64, 128, 256])
-def test_ngram_transposed_bf16(pkg, cuda, n, keep, F):
-    """pg_spmm3t_ngram_bf16 (bf16 rows, fp32 sums, one rounding) against the fp32 kernel on the widened bf16 input
-    and against the bf16 CSR kernel: within one bf16 ulp (|d| <= 2^-7 |ref| + 1e-6)."""
+@pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
+@pytest.mark.parametrize("F", [16, 48, 64, 128, 256])
+@pytest.mark.parametrize("kernel", ["mid", "block4"])
+def test_ngram_transposed_bf16(pkg, cuda, n, keep, F, kernel):
+    """bf16 transposed tile kernels (bf16 rows, fp32 sums, one rounding): the middle-tile kernel with the diagonal term
+    in-kernel (pg_spmm3t_ngram_mid_bf16, PG_FLAG_MID_TRANSPOSED; F % 16 == 0) and the 4x4-block one
+    (pg_spmm3t_ngram_bf16, the default; F in {64, 128, 256}), against the fp32 kernel on the widened bf16 input and against the bf16
+    CSR kernel: within one bf16 ulp (|d| <= 2^-7 |ref| + 1e-6); the middle kernel's accumulate mode on a strided G,
+    and determinism."""
     from protgram_directgcn_amd import ops
+    from protgram_directgcn_amd._lib import PG_FLAG_MID_TRANSPOSED, load_library
+    if kernel == "block4" and F not in (64, 128, 256):
+        pytest.skip("the 4x4-block kernel takes F in {64, 128, 256}")
     g = _graph(pkg, cuda, n, keep)
-    G = torch.randn(g.n_rows, 3 * F, generator=torch.Generator().manual_seed(n * 10 + F)).to(cuda).to(torch.bfloat16)
-    got = ops.spmm3_t(g, G)
+    N = g.n_rows
+    G = torch.randn(N, 3 * F, generator=torch.Generator().manual_seed(n * 10 + F)).to(cuda).to(torch.bfloat16)
+    fl = ops.default_flags() | (PG_FLAG_MID_TRANSPOSED if kernel == "mid" else 0)
+    got = ops.spmm3_t(g, G, flags=fl)
     assert got.dtype == torch.bfloat16
-    for other, tag in ((ops.spmm3_t(g, G.float(), flags=_csr_flag()), "fp32"),
-                       (ops.spmm3_t(g, G, flags=_csr_flag()).float(), "bf16 CSR")):
+    assert torch.equal(ops.spmm3_t(g, G, flags=fl), got)
+    ref32 = ops.spmm3_t(g, G.float(), flags=_csr_flag())
+    for other, tag in ((ref32, "fp32"), (ops.spmm3_t(g, G, flags=_csr_flag()).float(), "bf16 CSR")):
         d = (got.float() - other).abs()
         bad = d > 2.0 ** -7 * other.abs() + 1e-6
         assert not bool(bad.any()), (tag, int(bad.sum()), float(d.max()))
+    if kernel == "mid":  # accumulate through the C ABI: dX += A^T G (fp32 sum, one rounding)
+        lib = load_library()
+        Gw = torch.zeros(N, 3 * F + 8, dtype=torch.bfloat16, device=cuda)
+        Gw[:, :3 * F] = G
+        dX = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda).to(torch.bfloat16)
+        want = dX.float() + ref32
+        ng = g.ngram
+        rc = lib.pg_spmm3t_ngram_mid_bf16(ng.K, ng.n, N, ng.mplan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
+                                          dX.data_ptr(), dX.stride(0), 1, ops.default_flags(), ops._stream(dX))
+        assert rc == 0
+        d = (dX.float() - want).abs()
+        bad = d > 2.0 ** -7 * want.abs() + 2.0 ** -7 * ref32.abs() + 1e-6
+        assert not bool(bad.any()), ("accumulate", int(bad.sum()), float(d.max()))

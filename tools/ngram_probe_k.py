@@ -28,6 +28,7 @@ assert g.ngram is not None
 x = torch.randn(N, F, device=dev)
 G = torch.randn(N, 3 * F, device=dev)
 dXa = torch.zeros(N, F, device=dev)
+Gb = G.to(torch.bfloat16)
 
 
 def timeit(fn):
@@ -55,7 +56,9 @@ cases = {"fwd_ngram": lambda: ops.spmm3(g, x), "gated_ngram": lambda: ops.spmm3_
          "bwd_mid": lambda: ops.spmm3_t(g, G, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED),
          "bwd_offdiag": lambda: ops.spmm3t_offdiag(g, G),
          "bwd_offdiag_acc": lambda: ops.spmm3t_offdiag(g, G, out=dXa),
-         "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM)}
+         "bwd_csr": lambda: ops.spmm3_t(g, G, flags=PG_FLAG_NO_NGRAM),
+         "bwd_bf16_mid": lambda: ops.spmm3_t(g, Gb, flags=ops.default_flags() | PG_FLAG_MID_TRANSPOSED),
+         "bwd_bf16_block4": lambda: ops.spmm3_t(g, Gb)}
 for a in ALT:
     cases[f"fwd_alt{a:#x}"] = (lambda a: lambda: ops.spmm3(g, x, flags=a))(a)
     cases[f"gated_alt{a:#x}"] = (lambda a: lambda: ops.spmm3_gated(g, x, prm, 0, flags=a))(a)
@@ -81,6 +84,9 @@ for k in [c for c in ("gated_ngram", "gated_block4") if c in cases]:
 comp = g.compulsory_bytes(F)
 print(" ".join(f"{k}={v:.4f}ms" for k, v in best.items()), f"compulsory_fwd={comp / 1e6:.1f}MB "
       f"-> {comp / best['fwd_ngram'] / 1e6:.0f} GB/s")
+if "bwd_bf16_mid" in best:  # bf16 full product: G read three times (out, in, own rows), dX written, the plan once
+    bb = 3 * N * 3 * F * 2 + N * F * 2 + g.ngram.mplan.numel() * 4
+    print(f"bf16 mid bytes {bb / 1e6:.1f}MB -> {bb / best['bwd_bf16_mid'] / 1e6:.0f} GB/s")
 if "bwd_offdiag" in best:  # its algorithmic bytes: G read twice (out- and in-sources), dX written, the plan once
     ob = 2 * N * 3 * F * 4 + N * F * 4 + g.ngram.mplan.numel() * 4
     print(f"offdiag bytes {ob / 1e6:.1f}MB -> {ob / best['bwd_offdiag'] / 1e6:.0f} GB/s; "

@@ -383,26 +383,28 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
     float Ao[XTPW][XS], Ai[XTPW][XS];  // A fragments of this wave's out / in tiles (middle-resident)
     // A fragments of the next middle are prefetched where the registers are free: Ao after the last chunk's
     // out-phase (consumed by the next middle's first out-phase), Ai before its first chunk's out-phase
-    // (wave-uniform base + a 32-bit lane offset formed at each load: no 64-bit per-lane pointer stays live -- in the
-    // mapped kernel one was spilled, and its reload's vmcnt(0) waited for the chunk's Z stores at every middle change)
-    auto load_Ao = [&](int M) {
-        const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + XPO);
-        const uint32_t lo = (uint32_t)opaque((lane + (wb * 4 + mw) * XS * 64) * 4);
+    // MAP: wave-uniform base + a 32-bit lane offset formed at each load, so no 64-bit per-lane pointer stays live (one
+    // was spilled, and its reload's vmcnt(0) waited for the chunk's Z stores at every middle change); the plain kernel
+    // keeps the pointer form, under which its registers allocate best (measured: the opaque form cost it ~7 us)
+    auto load_W = [&](float (&W)[XTPW][XS], int M, int region) {
+        if constexpr (MAP) {
+            const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + region);
+            const uint32_t lo = (uint32_t)opaque((lane + (wb * 4 + mw) * XS * 64) * 4);
 #pragma unroll
-        for (int j = 0; j < XTPW; ++j)
+            for (int j = 0; j < XTPW; ++j)
 #pragma unroll
-            for (int s = 0; s < XS; ++s)
-                Ao[j][s] = *reinterpret_cast<const float*>(pm + lo + (uint32_t)(((2 * j * 4) * XS + s) * 256));
+                for (int s = 0; s < XS; ++s)
+                    W[j][s] = *reinterpret_cast<const float*>(pm + lo + (uint32_t)(((2 * j * 4) * XS + s) * 256));
+        } else {
+            const float* pm = p.plan + (int64_t)M * XMB + region + lane;
+#pragma unroll
+            for (int j = 0; j < XTPW; ++j)
+#pragma unroll
+                for (int s = 0; s < XS; ++s) W[j][s] = pm[(((2 * j + wb) * 4 + mw) * XS + s) * 64];
+        }
     };
-    auto load_Ai = [&](int M) {
-        const char* pm = reinterpret_cast<const char*>(p.plan + (int64_t)M * XMB + XPI);
-        const uint32_t lo = (uint32_t)opaque((lane + (wb * 4 + mw) * XS * 64) * 4);
-#pragma unroll
-        for (int j = 0; j < XTPW; ++j)
-#pragma unroll
-            for (int s = 0; s < XS; ++s)
-                Ai[j][s] = *reinterpret_cast<const float*>(pm + lo + (uint32_t)(((2 * j * 4) * XS + s) * 256));
-    };
+    auto load_Ao = [&](int M) { load_W(Ao, M, XPO); };
+    auto load_Ai = [&](int M) { load_W(Ai, M, XPI); };
     // this lane's four accumulator rows i = 16 mw + 4 q4 + r: (k, a) in the out-phase, (k, b) in the in-phase. The
     // padding rows i = 60..63 repeat rows 56..59 (the plan holds their weights twice): their lanes compute the same
     // values and write them to the same places as the lanes of rows 56..59, so no lane needs a branch
@@ -490,6 +492,10 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         // ---- in-phase: tiles (a = 2 j + wb, m = mw): rows (k, b); initial accumulators from the partial buffer; the
         // finished values go back into the partial buffer and leave it as 16-B row pieces
         const int M = cu.M;
+        [[maybe_unused]] ET* zso = nullptr;
+        if constexpr (!MAP)  // (the mapped kernel forms its store address after the in-phase: fewer live registers)
+            zso = reinterpret_cast<ET*>(p.Z) + ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz +
+                  (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
         auto rd_in = [&](int j, float (&x)[2][XS]) {
 #pragma unroll
             for (int s = 0; s < XS; ++s) {
@@ -527,10 +533,8 @@ __global__ __launch_bounds__(XTHREADS) void ngram_mid_kernel(XP p) {
         XSTAMP(ci, 4);
         // ---- store-out of chunk t, in the next out-phase's shadow (the out/self DMA of the in-phase is done; only
         // the smaller in-source DMA shares the CU's memory pipeline with these stores): every row of the partial
-        // buffer as 16-B pieces, then W(t) before the next out-phase overwrites it. (The row address is formed here,
-        // not before the in-phase: it is not live across the in-phase's MFMAs, whose registers are the tightest.)
-        ET* zso = reinterpret_cast<ET*>(p.Z) + (MAP ? 0 : ((int64_t)wb * p.zsa + (M - p.m0) * p.zsm + so_b) * p.ldz) +
-                  (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
+        // buffer as 16-B pieces, then W(t) before the next out-phase overwrites it
+        if constexpr (MAP) zso = reinterpret_cast<ET*>(p.Z) + (int64_t)so_k * p.F + cu.ch * XFC + 4 * (lane & 3);
 #pragma unroll
         for (int j = 0; j < XTPW; j += 2) {
             const f4_t v0 = *reinterpret_cast<const f4_t*>(L + so_lds + 2 * j * 3 * XK * 64);

@@ -395,8 +395,8 @@ def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.
     fl = default_flags() if flags is None else flags
     s = _stream(G)
     if g.shared and g.symmetric and G.size(0) == g.n_rows and (fl & _lib.PG_FLAG_MID_TRANSPOSED) and _mid_ok(g, dX, fl):
-        # the off-diagonal middle-tile kernel + the diagonal term here (opt-in: the extra pass over G costs what the
-        # kernel saves; training folds the diagonal into the dense backward instead, PropagateDense)
+        # the off-diagonal middle-tile kernel + the diagonal term here (opt-in: the extra pass over G costs more than
+        # the kernel saves against the 4x4-block kernel)
         rc = _offdiag(lib, g, G, dX, False, fl, s)
         if rc != _lib.PG_ERR_UNSUPPORTED:
             check(rc, "pg_spmm3t_ngram_mid_offdiag_f32")

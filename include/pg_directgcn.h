@@ -90,6 +90,8 @@ typedef struct pg_edge1 {
                                              between the MFMA k-steps (the default); same results */
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
+#define PG_FLAG_SCATTER_CPW_SHIFT 24    /* scatter kernel (pg_spmm3t_ngram_scatter_*): bits 24..28 = 16-feature chunks per
+                                           workgroup (1..31, clamped to F / 16; 0 = chosen from the grid size) */
 #define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernels instead of the
                                              4x4-block ones: fp32 pg_spmm3t_ngram_mid_offdiag_f32 plus the diagonal
                                              term on the host, bf16 pg_spmm3t_ngram_mid_bf16 */
@@ -310,6 +312,24 @@ int pg_spmm3t_ngram_mid_offdiag_f32(int K, int n, int64_t n_rows, const float* p
 int pg_spmm3t_ngram_mid_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
                              uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 
+/* Transposed middle-tile propagation of ONE middle-partition rank (shard.MiddleTrainer's backward, replacing the
+ * transposed CSR pass pg_spmm3t_f32 / pg_spmm3t_bf16 over the rank's column block): G = dZ [n_mid * 400, ldg] of
+ * the rank's owned rows a.M.b (middles M = m0 .. m0 + n_mid - 1, middle-major, (a, b) inside, the order
+ * pg_spmm3_ngram_mid_rows_* writes), T [3 * n_mid * 400, ldt] fp32 = the three parts of sum_k A_k^T G_k that the
+ * owned middles send to their row sets, each row written once (no accumulation, deterministic):
+ *   D: row          l*400 + a*20 + b  <- row a.M.b   sum_k Wdiag_k[a,b] G_k[a.M.b]
+ *   P: n_own  +     l*400 + b*20 + c  <- row M.b.c   sum_{k,a} Wout_k[a,b,c] G_k[a.M.b]
+ *   S: 2 n_own +    l*400 + c*20 + a  <- row c.a.M   sum_{k,b} Win_k[a,b,c] G_k[a.M.b]
+ * (l = M - m0, n_own = n_mid * 400). The caller sums the parts of each global row (pg_rows_gather_sum). `splan` =
+ * pg_ngram_scatter_plan of the same middles (78,000 floats per middle). F a multiple of 16; 16-B aligned G (ldg a
+ * multiple of 8 bf16 / 4 fp32 elements) and T. Numerics: fp32 MFMA sums of the same w*g terms (bf16 G widened
+ * exactly): within fp32 rounding of the CSR transposed kernel. */
+int pg_ngram_scatter_plan(int K, int n, const float* mplan, int64_t m0, int64_t n_mid, float* splan, void* stream);
+int pg_spmm3t_ngram_scatter_f32(const float* splan, int64_t n_mid, const float* G, int64_t ldg, int64_t F, float* T,
+                                int64_t ldt, uint32_t flags, void* stream);
+int pg_spmm3t_ngram_scatter_bf16(const float* splan, int64_t n_mid, const uint16_t* G, int64_t ldg, int64_t F,
+                                 float* T, int64_t ldt, uint32_t flags, void* stream);
+
 /* Row gather / scatter by an int64 index list (shard.py's ghost-row exchange; replaces the torch index gather /
  * index_copy_ around the RCCL all_to_all, which have no reference counterpart: the reference is single-device).
  * Byte-generic rows of row_bytes (a multiple of 4; 16-B pieces when rows, strides and pointers allow); strides in
@@ -318,6 +338,13 @@ int pg_rows_gather(const void* src, int64_t ld_src, const int64_t* idx, int64_t 
                    int64_t ld_dst, void* stream);
 int pg_rows_scatter(const void* src, int64_t ld_src, const int64_t* idx, int64_t n, int64_t row_bytes, void* dst,
                     int64_t ld_dst, void* stream);
+/* out[i] = sum of the rows listed for i, in list order, in fp32: entry idx[e] >= 0 is row idx[e] of A (fp32,
+ * stride lda elements), idx[e] < 0 row -1 - idx[e] of B (bf16 if b_bf16 else fp32, stride ldb); entries of row i
+ * are rowptr[i] .. rowptr[i+1]-1; out [n_out, F] fp32, or bf16 (one rounding) if out_bf16. F a multiple of 4. (The
+ * middle partition's backward: a row's scatter parts plus the rows received for it from the other ranks.) */
+int pg_rows_gather_sum(const float* A, int64_t lda, const void* B, int64_t ldb, int b_bf16, const int64_t* rowptr,
+                       const int32_t* idx, int64_t n_out, int64_t F, void* out, int64_t ldo, int out_bf16,
+                       void* stream);
 
 /* Backward of pg_directgcn_dense_f32 (the autograd of protgram_directgcn.py:100-133 and the fused
  * residual / leaky_relu of :213-215). `args` is the forward's argument block, with Y = the forward output

@@ -24,6 +24,7 @@ PG_FLAG_NGRAM_BLOCK4 = 1 << 21
 PG_FLAG_MID_NO_PAIRS = 1 << 22
 PG_FLAG_MID_LOADER_SYNC = 1 << 19
 PG_FLAG_MID_TRANSPOSED = 1 << 23
+PG_FLAG_SCATTER_CPW_SHIFT = 24
 PG_FLAG_DENSE_A_CACHED = 1 << 12
 PG_FLAG_DENSE_NO_IL = 1 << 13
 
@@ -93,6 +94,11 @@ SIGNATURES = {
     "pg_spmm3_resid_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_rows_gather": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "pg_rows_scatter": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "pg_rows_gather_sum": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, ctypes.c_int, c_vp, c_vp, c_i64, c_i64, c_vp,
+                                          c_i64, ctypes.c_int, c_vp]),
+    "pg_ngram_scatter_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "pg_spmm3t_ngram_scatter_f32": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
+    "pg_spmm3t_ngram_scatter_bf16": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_ngram_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                            ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_mid_offdiag_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64,

@@ -282,6 +282,74 @@ def rows_scatter(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor, check_
     return dst
 
 
+def rows_gather_sum(A: Optional[torch.Tensor], rowptr: torch.Tensor, idx: torch.Tensor, n_out: int, F: int,
+                    B: Optional[torch.Tensor] = None, out_dtype=torch.float32) -> torch.Tensor:
+    """pg_rows_gather_sum: out[i] = sum over e in [rowptr[i], rowptr[i+1]) of (A[idx[e]] if idx[e] >= 0 else
+    B[-1 - idx[e]]), in entry order, in fp32; A fp32, B fp32 or bf16, out fp32 or bf16 (one rounding). rowptr int64
+    [n_out + 1], idx int32 -- lists built and range-checked by their owner (shard.middle_scatter)."""
+    lib = load_library()
+    ref = A if A is not None else B
+    _require_gpu(ref)
+    for t in (A, B):
+        if t is not None and (t.dim() != 2 or t.stride(1) != 1 or t.size(1) < F):
+            raise ValueError("rows_gather_sum: 2-D sources with unit column stride and >= F columns")
+    if A is not None and A.dtype != torch.float32:
+        raise ValueError("rows_gather_sum: A must be fp32")
+    b_bf = B is not None and _is_bf16(B)
+    if B is not None and not b_bf and B.dtype != torch.float32:
+        raise ValueError("rows_gather_sum: B must be fp32 or bf16")
+    if rowptr.dtype != torch.int64 or idx.dtype != torch.int32 or rowptr.numel() != n_out + 1:
+        raise ValueError("rows_gather_sum: int64 rowptr of n_out + 1 entries and int32 idx")
+    o_bf = out_dtype == torch.bfloat16
+    if not o_bf and out_dtype != torch.float32:
+        raise ValueError("rows_gather_sum: out_dtype fp32 or bf16")
+    out = torch.empty(n_out, F, device=ref.device, dtype=out_dtype)
+    check(lib.pg_rows_gather_sum(_p(A), A.stride(0) if A is not None else F, _p(B),
+                                 B.stride(0) if B is not None else F, int(b_bf), _p(rowptr), _p(idx), n_out, F,
+                                 _p(out), out.stride(0), int(o_bf), _stream(ref)), "pg_rows_gather_sum")
+    return out
+
+
+def ngram_scatter_plan(g: CSRGraph, m_begin: int, m_end: int) -> torch.Tensor:
+    """pg_ngram_scatter_plan: the transposed-fragment plan [m_end - m_begin, 78,000] fp32 of the middles
+    [m_begin, m_end) (from g.ngram's middle plan; setup work, once per partition)."""
+    lib = load_library()
+    ng = g.ngram
+    if ng is None or ng.mplan is None:
+        raise ValueError("ngram_scatter_plan needs a graph with a middle plan")
+    _require_gpu(ng.mplan)
+    sp = torch.empty(m_end - m_begin, SCATTER_PLAN_FLOATS, device=ng.mplan.device, dtype=torch.float32)
+    check(lib.pg_ngram_scatter_plan(ng.K, ng.n, _p(ng.mplan), m_begin, m_end - m_begin, _p(sp), _stream(sp)),
+          "pg_ngram_scatter_plan")
+    return sp
+
+
+SCATTER_PLAN_FLOATS = 78_000
+
+
+def spmm3t_scatter(splan: torch.Tensor, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
+    """pg_spmm3t_ngram_scatter_f32 / _bf16: T [3 n_own, F] fp32 = the D / P / S parts of sum_k A_k^T G_k that a
+    middle-partition rank's owned rows send (include/pg_directgcn.h); G [n_own, 3F] (fp32 or bf16, owned rows in
+    middle-major order), n_own = 400 * splan.size(0), F % 16 == 0."""
+    lib = load_library()
+    bf = _is_bf16(G)
+    G = _bf16c(G) if bf else _f32c(G)
+    _require_gpu(G, splan)
+    n_mid = splan.size(0)
+    if splan.dim() != 2 or splan.size(1) != SCATTER_PLAN_FLOATS or splan.dtype != torch.float32:
+        raise ValueError("spmm3t_scatter: splan must be [n_mid, 78000] fp32 (ngram_scatter_plan)")
+    n_own = 400 * n_mid
+    if G.dim() != 2 or G.size(0) != n_own or G.size(1) % 48:
+        raise ValueError("spmm3t_scatter: G must be [400 n_mid, 3F] with F % 16 == 0")
+    F = G.size(1) // 3
+    T = torch.empty(3 * n_own, F, device=G.device, dtype=torch.float32)
+    fl = default_flags() if flags is None else flags
+    fn = lib.pg_spmm3t_ngram_scatter_bf16 if bf else lib.pg_spmm3t_ngram_scatter_f32
+    check(fn(_p(splan), n_mid, _p(G), G.stride(0), F, _p(T), T.stride(0), fl, _stream(G)),
+          "pg_spmm3t_ngram_scatter_" + ("bf16" if bf else "f32"))
+    return T
+
+
 def _spmm3_bf16(lib, g: CSRGraph, x, out, fused, flags):
     x = _bf16c(x)
     _require_gpu(x)

@@ -1288,6 +1288,113 @@ class _MidExchange(torch.autograd.Function):
         return d.to(dX.dtype), None, None
 
 
+@dataclass
+class MiddleScatter:
+    """The middle partition's scatter-form backward (pg_spmm3t_ngram_scatter_*): the rank's scatter plan and, over the
+    kernel's part rows T (D | P | S, include/pg_directgcn.h), the per-row lists pg_rows_gather_sum sums: the ghost rows
+    sent back (recv_ids order) and the owned rows (their own parts, unless loopback, then the rows received for them,
+    as -1 - position in the receive buffer)."""
+    splan: torch.Tensor
+    send_ptr: torch.Tensor
+    send_idx: torch.Tensor
+    own_ptr: torch.Tensor
+    own_idx: torch.Tensor
+
+
+def _csr_lists(counts: torch.Tensor):
+    ptr = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=counts.device)
+    ptr[1:] = torch.cumsum(counts, 0)
+    return ptr
+
+
+def middle_scatter(mp: MiddlePartition) -> Optional[MiddleScatter]:
+    """Setup of the scatter-form backward, once per partition (cached); None without a middle plan (K = 20)."""
+    if "scatter" in mp.cache:
+        return mp.cache["scatter"]
+    ng = mp.graph.ngram
+    if ng is None or getattr(ng, "mplan", None) is None or mp.K != 20 or not mp.own.is_cuda:
+        mp.cache["scatter"] = None
+        return None
+    dev = mp.own.device
+    K, n = mp.K, mp.ngram
+    Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
+    M = torch.arange(mp.m0, mp.m1, dtype=torch.int64, device=dev).view(-1, 1, 1)
+    x = torch.arange(K, dtype=torch.int64, device=dev).view(1, -1, 1)
+    y = torch.arange(K, dtype=torch.int64, device=dev).view(1, 1, -1)
+    tgt = torch.cat([(x * Kn1 + M * K + y).reshape(-1),         # D: (a, b) -> a.M.b
+                     (M * (K * K) + x * K + y).reshape(-1),     # P: (b, c) -> M.b.c
+                     (x * Kn1 + y * Kn2 + M).reshape(-1)])      # S: (c, a) -> c.a.M
+    order = torch.sort(tgt, stable=True).indices                # T rows by global row, ascending T row within
+    cnt = torch.bincount(tgt, minlength=mp.n)
+    gptr = _csr_lists(cnt)
+
+    def t_rows(rows: torch.Tensor, counts: torch.Tensor):
+        p = _csr_lists(counts)
+        tot = int(p[-1])
+        k = torch.arange(tot, dtype=torch.int64, device=dev) - torch.repeat_interleave(p[:-1], counts)
+        return order[torch.repeat_interleave(gptr[rows], counts) + k]
+
+    # ghost rows sent back: their parts (every ghost row is read by an owned middle: at least one part)
+    c_send = cnt[mp.recv_ids]
+    send_ptr = _csr_lists(c_send)
+    send_idx = t_rows(mp.recv_ids, c_send).to(torch.int32)
+    # owned rows: own parts (the received copies replace them in loopback mode), then the received rows in order
+    c_own = torch.zeros(mp.n_own, dtype=torch.int64, device=dev) if mp.loopback else cnt[mp.own]
+    c_rcv = torch.bincount(mp.send_pos, minlength=mp.n_own) if mp.send_pos.numel() else torch.zeros_like(c_own)
+    own_ptr = _csr_lists(c_own + c_rcv)
+    own_idx = torch.empty(int(own_ptr[-1]), dtype=torch.int64, device=dev)
+    if int(c_own.sum()):
+        k = torch.arange(int(c_own.sum()), dtype=torch.int64, device=dev) - torch.repeat_interleave(
+            _csr_lists(c_own)[:-1], c_own)
+        own_idx[torch.repeat_interleave(own_ptr[:-1], c_own) + k] = t_rows(mp.own, c_own)
+    if mp.send_pos.numel():
+        e = torch.sort(mp.send_pos, stable=True).indices        # receive-buffer entries by owned row, in order
+        k = torch.arange(e.numel(), dtype=torch.int64, device=dev) - torch.repeat_interleave(_csr_lists(c_rcv)[:-1], c_rcv)
+        own_idx[torch.repeat_interleave(own_ptr[:-1] + c_own, c_rcv) + k] = -1 - e
+    if own_idx.numel() >= 2 ** 31 or 3 * mp.n_own >= 2 ** 31:
+        raise ValueError("middle_scatter: lists exceed int32")
+    sc = MiddleScatter(ops.ngram_scatter_plan(mp.graph, mp.m0, mp.m1), send_ptr, send_idx, own_ptr,
+                       own_idx.to(torch.int32))
+    mp.cache["scatter"] = sc
+    return sc
+
+
+def _scatter_ok(mp: MiddlePartition, h_own: torch.Tensor) -> bool:
+    return h_own.is_cuda and h_own.size(1) % 16 == 0 and middle_scatter(mp) is not None
+
+
+class _MidExchangePropagate(torch.autograd.Function):
+    """h_own (owned rows) -> Z of the owned rows [n_own, 3F]: the ghost-row exchange (forward_exchange), then the
+    owned-middle propagation. Backward in scatter form: the owned middles' gradient dZ goes to the rows they read
+    (pg_spmm3t_ngram_scatter_*: D / P / S parts, no CSR pass over the rank's column block); the ghost rows' sums go
+    back to their owners (one pg_rows_gather_sum, the all_to_all per chunk), and each owned row sums its own parts
+    and the rows received for it (one pg_rows_gather_sum, fp32, one rounding to h_own's dtype)."""
+
+    @staticmethod
+    def forward(ctx, h_own, mp: MiddlePartition, comm):
+        ctx.mp, ctx.comm, ctx.hdtype = mp, comm, h_own.dtype
+        return _owned_spmm3(mp, forward_exchange(mp, h_own, comm))
+
+    @staticmethod
+    def backward(ctx, dZ):
+        mp, comm = ctx.mp, ctx.comm
+        sc = middle_scatter(mp)
+        T = ops.spmm3t_scatter(sc.splan, dZ.contiguous())
+        F_ = T.size(1)
+        recv = None
+        if mp.world > 1 or mp.loopback:
+            send = ops.rows_gather_sum(T, sc.send_ptr, sc.send_idx, int(mp.recv_ids.numel()), F_,
+                                       out_dtype=ctx.hdtype)
+            recv = send.new_empty(int(mp.send_pos.numel()), F_)
+            s0 = r0 = 0
+            for c in range(mp.chunks):
+                ns, nr = sum(mp.chunk_recv[c]), sum(mp.chunk_send[c])
+                comm.all_to_all(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_send[c], mp.chunk_recv[c])
+                s0, r0 = s0 + ns, r0 + nr
+        d = ops.rows_gather_sum(T, sc.own_ptr, sc.own_idx, mp.n_own, F_, B=recv, out_dtype=ctx.hdtype)
+        return d, None, None
+
+
 class MiddleTrainer:
     """ShardedTrainer's step (the reference's full-batch loop, protgram_directgcn_trainer.py:91-100: zero_grad ->
     forward -> nll_loss (mean over all N nodes) + l2_lambda * sum_p ||p||^2 -> backward -> Adam step) on the middle
@@ -1339,6 +1446,7 @@ class MiddleTrainer:
         for prm in self.params:
             prm.register_post_accumulate_grad_hook(lambda t: self._touched.add(id(t)))
         middle_transpose(mp)  # setup work, outside the steps
+        middle_scatter(mp)
 
     def forward(self, x_full: torch.Tensor):
         """(log_probs, emb) of the owned rows (middle-major) with autograd."""
@@ -1352,7 +1460,12 @@ class MiddleTrainer:
         L = len(model.convs)
         h_own = None
         for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
-            Z = _MidPropagate.apply(X, mp)
+            if i == 0:
+                Z = _MidPropagate.apply(X, mp)  # the input carries no gradient
+            elif _scatter_ok(mp, h_own):
+                Z = _MidExchangePropagate.apply(h_own, mp, self.comm)
+            else:
+                Z = _MidPropagate.apply(_MidExchange.apply(h_own, mp, self.comm), mp)
             vec = conv.use_vector_coeffs
             params = conv._dense_params()
             own = self.own[i]
@@ -1365,9 +1478,7 @@ class MiddleTrainer:
             h_own = ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, None, 0 if vec else 1, True,
                                          ops.LEAKY_SLOPE, *params)
             h_own = F.dropout(h_own, p=model.dropout, training=model.training)
-            if i + 1 < L:
-                X = _MidExchange.apply(h_own, mp, self.comm)
-                res_x = h_own
+            res_x = h_own
         return model.head(h_own)
 
     WARM = 3

@@ -91,7 +91,7 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_A_CACHED (1u << 12) /* pipelined dense kernels: default cache policy for the LDS-DMA of the
                                              A rows and the per-node constant instead of non-temporal (speed only) */
 #define PG_FLAG_SCATTER_CPW_SHIFT 24    /* scatter kernel (pg_spmm3t_ngram_scatter_*): bits 24..28 = 16-feature chunks per
-                                           workgroup (1..31, clamped to F / 16; 0 = chosen from the grid size) */
+                                           workgroup (1..31, clamped to F / 16; 0 = chosen from the CU count) */
 #define PG_FLAG_MID_TRANSPOSED (1u << 23) /* host-side: spmm3_t runs the transposed middle-tile kernels instead of the
                                              4x4-block ones: fp32 pg_spmm3t_ngram_mid_offdiag_f32 plus the diagonal
                                              term on the host, bf16 pg_spmm3t_ngram_mid_bf16 */

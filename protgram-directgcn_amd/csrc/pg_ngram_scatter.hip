@@ -283,6 +283,18 @@ int pg_ngram_scatter_plan(int K, int n, const float* mplan, int64_t m0, int64_t 
 
 namespace {
 
+int grid_cap() {  // CUs of the current device (cached; immutable once read)
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev] = v;
+    }
+    return cus[dev];
+}
+
 template <bool BF>
 int scatter_launch(const float* splan, int64_t n_mid, const void* G, int64_t ldg, int64_t F, float* T, int64_t ldt,
                    uint32_t flags, void* stream, const char* name) {
@@ -304,8 +316,16 @@ int scatter_launch(const float* splan, int64_t n_mid, const void* G, int64_t ldg
     p.n_own = n_mid * SR;
     p.F = (int)F;
     p.nch = (int)(F / 16);
-    const int64_t items = n_mid * 2 * p.nch;  // (middle, direction, chunk)
-    int64_t cpw = items / 600;                // >= ~600 workgroups; weights reused over cpw chunks
+    // chunks per workgroup: the (middle, direction) pairs' chunks split into as many equal groups as one round of
+    // workgroups (one per CU: the kernel's registers allow one) holds, at least one group per pair (more pairs than
+    // CUs: whole pairs, several rounds). A workgroup loads its pair's weights once, so fewer, longer groups amortise
+    // them; measured at config 5's rank shapes (50 middles, F = 256): 8 chunks (200 workgroups) 49.6 us, 4 chunks
+    // 54.3, 2 chunks 60.2, 16 chunks (100 workgroups) 76.2, a persistent walker over the item stream with weight
+    // reloads at pair changes (256 workgroups) 59.0
+    const int64_t pairs = n_mid * 2;
+    int64_t groups = grid_cap() / pairs;
+    groups = groups < 1 ? 1 : (groups > p.nch ? p.nch : groups);
+    int64_t cpw = (p.nch + groups - 1) / groups;
     int64_t forced = (flags >> PG_FLAG_SCATTER_CPW_SHIFT) & 31;
 #ifdef PG_SCATTER_EXP
     p.exp = (int)forced;  // the diagnostics build reads bits 24..28 as phase skips, at 8 chunks per workgroup

@@ -21,21 +21,36 @@ __global__ __launch_bounds__(256) void gather_sum_kernel(const float* A, int64_t
         const int q = (int)(t - i * q4);
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         const int64_t e1 = rowptr[i + 1];
-        for (int64_t e = rowptr[i]; e < e1; ++e) {
-            const int32_t v = idx[e];
-            float4 x;
-            if (v >= 0) {
-                x = *reinterpret_cast<const float4*>(A + (int64_t)v * lda + 4 * q);
-            } else if constexpr (BBF) {
-                x = pgbf::unpack4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(B) +
-                                                                   (int64_t)(-1 - v) * ldb + 4 * q));
-            } else {
-                x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(B) + (int64_t)(-1 - v) * ldb + 4 * q);
+        // entries in batches of 4: the index loads, then the row loads, are issued together (not one dependent
+        // pair per entry); the adds keep the entry order
+        for (int64_t e = rowptr[i]; e < e1; e += 4) {
+            int32_t v[4];
+            float4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = e + u < e1 ? idx[e + u] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (e + u < e1) {
+                    if (v[u] >= 0) {
+                        x[u] = *reinterpret_cast<const float4*>(A + (int64_t)v[u] * lda + 4 * q);
+                    } else if constexpr (BBF) {
+                        x[u] = pgbf::unpack4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(B) +
+                                                                          (int64_t)(-1 - v[u]) * ldb + 4 * q));
+                    } else {
+                        x[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(B) +
+                                                                (int64_t)(-1 - v[u]) * ldb + 4 * q);
+                    }
+                }
             }
-            acc.x += x.x;
-            acc.y += x.y;
-            acc.z += x.z;
-            acc.w += x.w;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (e + u < e1) {
+                    acc.x += x[u].x;
+                    acc.y += x[u].y;
+                    acc.z += x[u].z;
+                    acc.w += x[u].w;
+                }
+            }
         }
         if constexpr (OBF)
             *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + i * ldo + 4 * q) = pgbf::pack4(acc);

@@ -1515,26 +1515,36 @@ class MiddleTrainer:
 
     def _step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
         mp, lam, train = self.mp, self.l2_lambda, self._train
-        if self.graphs:  # persistent gradient buffers (autograd accumulates into them): fixed addresses, so the
-            # optimizer's descriptor lists built in the eager warm-up serve the capture and its replays
-            if not hasattr(self, "_node_grads"):
-                self._node_grads = [torch.zeros_like(p) for p in self.node]
-            for p, gb in zip(self.node, self._node_grads):
-                p.grad = gb
-            torch._foreach_zero_(self._node_grads)
-        else:
-            for p in self.node:
-                p.grad = None
+        # autograd assigns each parameter's gradient (no .grad preset: a preset one costs an add kernel per parameter
+        # per step, ~0.3 ms at config 5); then one multi-tensor copy moves them into their fixed homes: the flat
+        # buffer of the replicated parameters (one all-reduce) and, with graphs, persistent per-node buffers (fixed
+        # addresses: the optimizer's descriptor lists built in the eager warm-up serve the capture and its replays)
+        if self.graphs and not hasattr(self, "_node_grads"):
+            self._node_grads = [torch.zeros_like(p) for p in self.node]
+        if not hasattr(self, "_flat_views"):
+            views, off = [], 0
+            for p in self.dense:
+                k = p.numel()
+                views.append(self.flat[off:off + k].view_as(p))
+                off += k
+            self._flat_views = views
+        for p in self.dense + self.node:
+            p.grad = None
         self.flat.zero_()
-        off = 0
-        for p in self.dense:
-            k = p.numel()
-            p.grad = self.flat[off:off + k].view_as(p)
-            off += k
         lp, _ = self.forward(x_full)
         nll = -lp.float().gather(1, y_own.view(-1, 1)).sum() / mp.n
         self._touched = set()
         nll.backward()
+        homes = [(p, h, False) for p, h in zip(self.dense, self._flat_views)]
+        if self.graphs:
+            homes += [(p, h, True) for p, h in zip(self.node, self._node_grads)]
+        have = [(p, h) for p, h, _ in homes if p.grad is not None]
+        if have:
+            torch._foreach_copy_([h for _, h in have], [p.grad for p, _ in have])
+        for p, h, node in homes:
+            if p.grad is None and node:
+                h.zero_()  # an unused per-node parameter: its persistent buffer holds zeros (the flat one is zeroed)
+            p.grad = h
         if lam:
             for p in self.node:
                 if p.requires_grad and p.grad is None:

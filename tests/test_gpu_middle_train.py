@@ -106,6 +106,33 @@ def _worker(rank, world, port, out_q, bf16):
         dist.destroy_process_group()
 
 
+def _collect(q, procs, n, limit):
+    """The n ranks' results; fails fast (terminating the others) when a rank reports an error or dies, instead of
+    leaving the surviving ranks blocked in a collective until the time limit."""
+    import queue
+    import time
+    res, t0 = [], time.time()
+    while len(res) < n:
+        try:
+            r = q.get(timeout=5)
+        except queue.Empty:
+            r = None
+        if r is not None:
+            res.append(r)
+            if not r[3] and r[1] == 0:  # an exception in the rank (see _worker)
+                break
+        dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+        if dead or time.time() - t0 > limit:
+            break
+    if len(res) < n or any(not r[3] and r[1] == 0 for r in res):
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+        pytest.fail(f"ranks incomplete: {len(res)} of {n} results, exit codes {[p.exitcode for p in procs]}, "
+                    f"errors {[r[4] for r in res if not r[3]]}")
+    return res
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("bf16", [False, True])
 def test_config5_middle_trainer_p8_one_gpu(cuda, bf16):
@@ -116,7 +143,7 @@ def test_config5_middle_trainer_p8_one_gpu(cuda, bf16):
     procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, bf16)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=840) for _ in range(WORLD))
+    res = sorted(_collect(q, procs, WORLD, 840))
     for p in procs:
         p.join(timeout=120)
     assert env_keep is None or os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") == env_keep

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timing of the middle partition's backward propagation at config 5's rank shapes (4-gram, P = 8, rank 0, F = 256,
-bf16 dZ): the scatter kernel (pg_spmm3t_ngram_scatter_bf16) per chunks-per-workgroup setting, the two gather-sums
+bf16 dZ): the scatter kernel (pg_spmm3t_ngram_scatter_bf16) per chunks-per-workgroup setting (0: the library's choice), the two gather-sums
 that follow it, and the transposed CSR kernel over the rank's column block it replaces. HIP events, median of reps.
   python tools/scatter_probe.py [--F 256] [--world 8] [--rank 0] [--fp32]"""
 import argparse
@@ -41,7 +41,7 @@ ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--n", type=int, default=4)
 ap.add_argument("--fp32", action="store_true")
-ap.add_argument("--cpw", type=int, nargs="*", default=[0, 1, 2, 4, 8, 16])
+ap.add_argument("--cpw", type=int, nargs="*", default=[0, 2, 4, 8, 16])
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--no-csr", action="store_true")
 a = ap.parse_args()

@@ -1257,16 +1257,26 @@ def forward_exchange(mp: MiddlePartition, h_own: torch.Tensor, comm) -> torch.Te
     rows unwritten); per chunk one all_to_all (the lists are grouped by (chunk, rank))."""
     F_ = h_own.size(1)
     X = h_own.new_empty(mp.n, F_)
-    X.index_copy_(0, mp.own, h_own)
+    # on the device the row moves are pg_rows_scatter / pg_rows_gather (16-B pieces; the lists are the partition's
+    # closed form, checked when it was built); host tensors (the gloo rehearsals) take torch's index ops
+    dev = h_own.is_cuda
+    h_own = h_own.contiguous()
+    if dev:
+        ops.rows_scatter(h_own, mp.own, X, check_idx=False)
+    else:
+        X.index_copy_(0, mp.own, h_own)
     if mp.world > 1 or mp.loopback:
-        send = h_own.index_select(0, mp.send_pos)
+        send = ops.rows_gather(h_own, mp.send_pos, check_idx=False) if dev else h_own.index_select(0, mp.send_pos)
         recv = send.new_empty(int(mp.recv_ids.numel()), F_)
         s0 = r0 = 0
         for c in range(mp.chunks):
             ns, nr = sum(mp.chunk_send[c]), sum(mp.chunk_recv[c])
             comm.all_to_all(recv[r0:r0 + nr], send[s0:s0 + ns], mp.chunk_recv[c], mp.chunk_send[c])
             s0, r0 = s0 + ns, r0 + nr
-        X.index_copy_(0, mp.recv_ids, recv)
+        if dev:
+            ops.rows_scatter(recv, mp.recv_ids, X, check_idx=False)
+        else:
+            X.index_copy_(0, mp.recv_ids, recv)
     return X
 
 
@@ -1439,8 +1449,17 @@ class MiddleTrainer:
         dev = dense[0].device if dense else mp.own.device
         self.flat = torch.zeros(sum(p.numel() for p in dense), dtype=torch.float32, device=dev)
         self.params = dense + [p for p in node_leaves if p.requires_grad]
-        self.opt = (train.Adam(self.params, lr=lr, **adam_kw) if optimizer_factory is None
-                    else optimizer_factory(self.params))
+        # train.Adam over two groups (replicated, per-node): its launches also return each group's L2 value of the
+        # pre-update parameters (the loss's two L2 terms, one of them all-reduced), so no separate sums are launched
+        node_req = [p for p in node_leaves if p.requires_grad]
+        self._sq_groups = None
+        if optimizer_factory is None:
+            groups = [g for g in ({"params": dense}, {"params": node_req}) if g["params"]]
+            self.opt = train.Adam(groups, lr=lr, **adam_kw)
+            if len(node_req) == len(node_leaves):
+                self._sq_groups = (0 if dense else None, (1 if dense else 0) if node_req else None)
+        else:
+            self.opt = optimizer_factory(self.params)
         self._train = train
         self._touched: set = set()
         for prm in self.params:
@@ -1545,33 +1564,43 @@ class MiddleTrainer:
             if p.grad is None and node:
                 h.zero_()  # an unused per-node parameter: its persistent buffer holds zeros (the flat one is zeroed)
             p.grad = h
+        fold = bool(lam) and isinstance(self.opt, train.Adam)
+        fused = fold and self._sq_groups is not None  # the L2 values come out of the Adam launches
+        zero = nll.new_zeros(())
         if lam:
             for p in self.node:
                 if p.requires_grad and p.grad is None:
                     p.grad = torch.zeros_like(p)
-            l2_rep = train.l2_sqsum(self.dense) if self.dense else nll.new_zeros(())
-            l2_own = train.l2_sqsum(self.node) if self.node else nll.new_zeros(())
+            if not fused:
+                l2_rep = train.l2_sqsum(self.dense) if self.dense else zero
+                l2_own = train.l2_sqsum(self.node) if self.node else zero
         else:
             for p in self.params:
                 if id(p) not in self._touched:
                     p.grad = None
-            l2_rep = l2_own = nll.new_zeros(())
-        parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
-        if self.xchg and mp.world > 1:
-            if self.flat.numel():
-                self.comm.all_reduce(self.flat)
-            self.comm.all_reduce(parts)
-        fold = bool(lam) and isinstance(self.opt, train.Adam)
+            l2_rep = l2_own = zero
+        if self.xchg and mp.world > 1 and self.flat.numel():
+            self.comm.all_reduce(self.flat)
         if lam and not fold:
             ps = [p for p in self.params if p.grad is not None]
             torch._foreach_add_([p.grad for p in ps], [p.detach() for p in ps], alpha=2.0 * lam)
         if fold:
             self.opt._l2_extra = 2.0 * lam
+            self.opt._want_sqsum = "groups" if fused else False
         try:
             self.opt.step()
         finally:
             if fold:
                 self.opt._l2_extra = 0.0
+                self.opt._want_sqsum = False
+        if fused:
+            sums = self.opt._last_sqsum_groups
+            gd, gn = self._sq_groups
+            l2_rep = sums[gd] if gd is not None and sums[gd] is not None else zero
+            l2_own = sums[gn] if gn is not None and sums[gn] is not None else zero
+        parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
+        if self.xchg and mp.world > 1:
+            self.comm.all_reduce(parts)
         return parts.sum() + lam * l2_rep
 
     @torch.no_grad()

@@ -201,9 +201,12 @@ class Adam(torch.optim.Optimizer):
         found_inf = getattr(self, "found_inf", None)
         lib = load_library()
         # train_step's fused L2 value: per-chunk sums of p^2 (pre-update) from every launch, added at the end
+        # (_want_sqsum == "groups": one value per parameter group, in _last_sqsum_groups)
         want_sq = getattr(self, "_want_sqsum", False)
         sq_parts = []
+        group_parts: List[list] = []
         for group in self.param_groups:
+            group_parts.append([])
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -230,6 +233,7 @@ class Adam(torch.optim.Optimizer):
                                         [self.state[p]["exp_avg_sq"] for p in members]))
                 if want_sq:
                     sq_parts.append(tl.partial[:tl.nchunks])
+                    group_parts[-1].append(tl.partial[:tl.nchunks])
                 check(lib.pg_adam_f32(len(members), ctypes.c_void_p(tl.desc.data_ptr()),
                                       ctypes.c_void_p(tl.chunk_ptr.data_ptr()), tl.nchunks, float(group["lr"]),
                                       float(b1), float(b2), float(group["eps"]),
@@ -241,12 +245,17 @@ class Adam(torch.optim.Optimizer):
                       "pg_adam_f32")
             for p in ps:  # written in place by the kernel: let autograd / version-keyed caches see it
                 torch.autograd.graph.increment_version(p)
-        if want_sq:
-            parts = torch.cat(sq_parts) if len(sq_parts) > 1 else sq_parts[0]
+        def fixed_order_sum(chunks):
+            parts = torch.cat(chunks) if len(chunks) > 1 else chunks[0]
             out = torch.empty((), dtype=torch.float32, device=parts.device)
             check(lib.pg_multi_sum_f32(parts.numel(), ctypes.c_void_p(parts.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                        _stream(parts.device)), "pg_multi_sum_f32")
-            self._last_sqsum = out
+            return out
+
+        if want_sq == "groups":
+            self._last_sqsum_groups = [fixed_order_sum(gp) if gp else None for gp in group_parts]
+        elif want_sq and sq_parts:
+            self._last_sqsum = fixed_order_sum(sq_parts)
         return loss
 
 

@@ -1318,13 +1318,28 @@ def _csr_lists(counts: torch.Tensor):
 
 
 def middle_scatter(mp: MiddlePartition) -> Optional[MiddleScatter]:
-    """Setup of the scatter-form backward, once per partition (cached); None without a middle plan (K = 20)."""
+    """Setup of the scatter-form backward, once per partition (cached): the scatter plan of the rank's middles and
+    the row lists (scatter_lists); None without a middle plan on the device (K = 20)."""
     if "scatter" in mp.cache:
         return mp.cache["scatter"]
     ng = mp.graph.ngram
     if ng is None or getattr(ng, "mplan", None) is None or mp.K != 20 or not mp.own.is_cuda:
         mp.cache["scatter"] = None
         return None
+    sc = MiddleScatter(ops.ngram_scatter_plan(mp.graph, mp.m0, mp.m1), *scatter_lists(mp))
+    mp.cache["scatter"] = sc
+    return sc
+
+
+def scatter_lists(mp: MiddlePartition):
+    """(send_ptr, send_idx, own_ptr, own_idx) of the scatter-form backward (MiddleScatter), on mp's device. Part row t
+    of T (D | P | S, include/pg_directgcn.h) targets one global row; a row's list holds its part rows in T-row order;
+    the ghost rows' lists come in recv_ids order (what goes back to each owner), the owned rows' lists hold their own
+    parts (none in loopback mode: the received copies replaced the own rows), then -1 - e for each receive-buffer
+    entry e of that row, in order."""
+    hit = mp.cache.get("scatter_lists")
+    if hit is not None:
+        return hit
     dev = mp.own.device
     K, n = mp.K, mp.ngram
     Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
@@ -1363,10 +1378,9 @@ def middle_scatter(mp: MiddlePartition) -> Optional[MiddleScatter]:
         own_idx[torch.repeat_interleave(own_ptr[:-1] + c_own, c_rcv) + k] = -1 - e
     if own_idx.numel() >= 2 ** 31 or 3 * mp.n_own >= 2 ** 31:
         raise ValueError("middle_scatter: lists exceed int32")
-    sc = MiddleScatter(ops.ngram_scatter_plan(mp.graph, mp.m0, mp.m1), send_ptr, send_idx, own_ptr,
-                       own_idx.to(torch.int32))
-    mp.cache["scatter"] = sc
-    return sc
+    lists = (send_ptr, send_idx, own_ptr, own_idx.to(torch.int32))
+    mp.cache["scatter_lists"] = lists
+    return lists
 
 
 def _scatter_ok(mp: MiddlePartition, h_own: torch.Tensor) -> bool:

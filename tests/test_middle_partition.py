@@ -311,3 +311,109 @@ def test_middle_trainer_gloo(world, chunks, bf16):
     assert sum(r[1] for r in res) == 8000
     for r in res:
         assert r[2], f"rank {r[0]}: {r[3]}"
+
+
+def _cpu_scatter_parts(mp_):
+    """CPU stand-in for ops.spmm3t_scatter on partition mp_: T [3 n_own, F] (D | P | S) from the owned rows' CSR,
+    each entry (i = a.M.b <- j) to the part row of j that the kernel writes (prefix M: P, suffix M: S, else D = i)."""
+    def fn(splan, G, flags=None):
+        oc = mp_.own_csr
+        K, n = mp_.K, mp_.ngram
+        Kn1, Kn2 = K ** (n - 1), K ** (n - 2)
+        n_own, F = mp_.n_own, G.size(1) // 3
+        ipos = torch.repeat_interleave(torch.arange(n_own), oc.rowptr[1:] - oc.rowptr[:-1])
+        j = oc.edges3[:, 0].long()
+        l = ipos // (K * K)
+        M = mp_.m0 + l
+        P_row = n_own + l * K * K + ((j // K) % K) * K + j % K
+        S_row = 2 * n_own + l * K * K + (j // Kn1) * K + (j // Kn2) % K
+        t = torch.where(j // (K * K) == M, P_row, torch.where(j % Kn2 == M, S_row, ipos))
+        d_ok = (j // (K * K) == M) | (j % Kn2 == M) | (j == mp_.own[ipos])
+        assert bool(d_ok.all()), "an entry outside the out / in / diagonal slots"
+        T = torch.zeros(3 * n_own, F, dtype=torch.float64)
+        Gd = G.double()
+        for k in range(3):
+            w = oc.edges3[:, 1 + k].contiguous().view(torch.float32).double()
+            T.index_add_(0, t, w[:, None] * Gd[ipos, k * F:(k + 1) * F])
+        return T.float()
+    return fn
+
+
+def _cpu_gather_sum(A, rowptr, idx, n_out, F, B=None, out_dtype=torch.float32):
+    """CPU stand-in for ops.rows_gather_sum (fp32 sum in entry order)."""
+    out = torch.zeros(n_out, F)
+    cnt = rowptr[1:] - rowptr[:-1]
+    rows = torch.repeat_interleave(torch.arange(n_out), cnt)
+    k_of = torch.arange(int(rowptr[-1])) - torch.repeat_interleave(rowptr[:-1], cnt)
+    v = idx.long()
+    for k in range(int(cnt.max()) + 1 if n_out and cnt.numel() and int(cnt.max()) > 0 else 0):
+        sel = k_of == k
+        vv = v[sel]
+        src = A[vv.clamp(min=0)].float()
+        if B is not None:
+            src = torch.where((vv >= 0).view(-1, 1), src, B[(-1 - vv).clamp(min=0)].float())
+        out[rows[sel]] += src[:, :F]
+    return out.to(out_dtype)
+
+
+def _scatter_bwd_worker(rank, world, port, out_q, chunks):
+    """The scatter-form backward (_MidExchangePropagate: part rows, ghost sums sent back, owned rows summed with the
+    rows received) against the CSR composition (_MidExchange -> _MidPropagate) on the same rank, the kernels replaced
+    by CPU stand-ins; the lists (shard.scatter_lists) and the exchange are the product's."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [REPO, HERE]
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    from protgram_directgcn_amd import ops, shard
+    from test_shard_gloo import _cpu_spmm3
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bad = []
+    try:
+        N, m, g = _graph(pkg, 3)
+        g.symmetric = True
+        mp_ = shard.middle_partition(g, rank, world, chunks=chunks)
+        comm = shard.TorchComm()
+        ops.spmm3 = _cpu_spmm3
+        ops.spmm3t_rows = _cpu_spmm3t_rows
+        ops.spmm3t_scatter = _cpu_scatter_parts(mp_)
+        ops.rows_gather_sum = _cpu_gather_sum
+        shard.middle_scatter = lambda mp: shard.MiddleScatter(None, *shard.scatter_lists(mp))
+        F = 8
+        gen = torch.Generator().manual_seed(50 + rank)
+        h = torch.randn(mp_.n_own, F, generator=gen)
+        w = torch.randn(mp_.n_own, 3 * F, generator=gen)
+        grads = []
+        for fused in (True, False):
+            hh = h.clone().requires_grad_(True)
+            if fused:
+                Z = shard._MidExchangePropagate.apply(hh, mp_, comm)
+            else:
+                Z = shard._MidPropagate.apply(shard._MidExchange.apply(hh, mp_, comm), mp_)
+            (Z * w).sum().backward()
+            grads.append(hh.grad)
+        err = float((grads[0] - grads[1]).abs().max())
+        if err > 1e-5 * float(grads[1].abs().max()) + 1e-6:
+            bad.append(("grad", err))
+        out_q.put((rank, not bad, str(bad)))
+    except Exception as e:
+        out_q.put((rank, False, repr(e)[:300]))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,chunks", [(3, 1), (3, 2)])
+def test_scatter_backward_gloo(world, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_bwd_worker, args=(r, world, port, q, chunks)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=280) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in res:
+        assert r[1], f"rank {r[0]}: {r[2]}"

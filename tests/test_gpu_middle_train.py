@@ -31,6 +31,8 @@ def _free_port():
 
 
 def _worker(rank, world, port, out_q, bf16):
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=True)  # a stuck rank prints where it is and exits (the parent fails)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [REPO, HERE]
     import torch.distributed as dist
@@ -98,6 +100,7 @@ def _worker(rank, world, port, out_q, bf16):
                 err = (gg - r).abs()
                 if bool((err > 1e-4 * float(r.abs().max()) + 1e-4 * r.abs()).any()):
                     bad.append((name, "grad", float(err.max()), float(r.abs().max())))
+        faulthandler.cancel_dump_traceback_later()
         out_q.put((rank, mp_.n_own, int(mp_.recv_ids.numel()), not bad, str(bad[:4]), loss, loss_r))
     except Exception as e:  # report instead of hanging the parent
         out_q.put((rank, 0, 0, False, repr(e)[:400], 0.0, 0.0))

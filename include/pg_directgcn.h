@@ -425,7 +425,7 @@ int pg_ngram_keys(int64_t nseq, const int64_t* offsets, const uint8_t* bytes, co
 
 /* ---- training-step helpers (the trainer's L2 term over all parameters, trainer :96 / :136) ---------
  * A tensor list is a device array of descriptors; tensor t is split into pg_multi_chunks(numel_t) chunks of
- * 64K elements and chunk_ptr[t] = the first chunk of tensor t (exclusive prefix sum, chunk_ptr[ntens] =
+ * 16K elements and chunk_ptr[t] = the first chunk of tensor t (exclusive prefix sum, chunk_ptr[ntens] =
  * nchunks). */
 typedef struct pg_tensor_desc {
     const float* x;  /* read */

@@ -8,12 +8,15 @@
 //                         2*lambda*p added to p.grad);
 //   pg_adam_f32        -- Adam over the list in one launch, optionally with the L2 value of the pre-update
 //                         parameters as per-chunk partials (pg_multi_sum_f32 adds them in fixed order).
-// A list is a device array of pg_tensor_desc_t; work is split into fixed 64K-element chunks.
+// A list is a device array of pg_tensor_desc_t; work is split into fixed 16K-element chunks.
 #include "pg_common.h"
 
 namespace {
 
-constexpr int64_t CHUNK = 65536;
+// 16K elements per chunk (one 256-thread block each): a 16M-element parameter list gives ~1000 blocks, four per
+// CU, whose loads overlap (at 64K, one block of four waves per CU walked its chunk one latency at a time: Adam over
+// config 5's per-node state took 2x its bytes' time)
+constexpr int64_t CHUNK = 16384;
 
 __global__ __launch_bounds__(256) void sqsum_chunks_kernel(int ntens, const pg_tensor_desc_t* d,
                                                            const int64_t* chunk_ptr, float* partial) {
@@ -29,7 +32,7 @@ __global__ __launch_bounds__(256) void sqsum_chunks_kernel(int ntens, const pg_t
     const int64_t beg = (b - chunk_ptr[lo]) * CHUNK;
     const int64_t end = min(beg + CHUNK, t.numel);
     float s = 0.f;
-    if ((reinterpret_cast<uintptr_t>(t.x) & 15) == 0) {  // float4 body (chunks start at multiples of 64K)
+    if ((reinterpret_cast<uintptr_t>(t.x) & 15) == 0) {  // float4 body (chunks start at multiples of 16K)
         const int64_t end4 = beg + ((end - beg) & ~int64_t(3));
         const float4* x4 = reinterpret_cast<const float4*>(t.x);
         for (int64_t i = beg / 4 + threadIdx.x; i < end4 / 4; i += 256) {

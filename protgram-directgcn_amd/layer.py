@@ -265,10 +265,11 @@ class ProtGramDirectGCN(nn.Module):
             h = F.dropout(h, p=self.dropout, training=self.training)
         return self.head(h)
 
-    def head(self, h):
+    def head(self, h, need_emb: bool = True):
         """decoder_fc -> log_softmax, and l2_normalize (protgram_directgcn.py:218-222). Inference (eval, no
         autograd) runs the fused pg_directgcn_head_f32 kernel; training runs the decoder Linears through
-        ops.row_linear (weight gradients in pg_gemm_at_b_f32)."""
+        ops.row_linear (weight gradients in pg_gemm_at_b_f32). need_emb=False (a trainer whose loss reads only the
+        log-probs) returns (log_probs, None) on the training path: the embeddings take no part in the loss."""
         dec = self.decoder_fc
         if not self.training and not torch.is_grad_enabled() and h.is_cuda:
             return ops.head(h, dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias, self.l2_eps)
@@ -278,5 +279,7 @@ class ProtGramDirectGCN(nn.Module):
             logits = ops.row_linear(a, dec[3].weight, dec[3].bias)
         else:
             logits = dec(h)
+        if not need_emb:
+            return F.log_softmax(logits, dim=-1), None
         emb = h / (torch.norm(h, p=2, dim=1, keepdim=True) + self.l2_eps)  # models_utils.py:139-147
         return F.log_softmax(logits, dim=-1), emb

@@ -972,14 +972,20 @@ class LayerDense(torch.autograd.Function):
                     out[k] = out[k].to(torch.bfloat16)
         dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]
         M, F_in = Z.size(0), Z.size(1) // 3
-        g = {}
-        g["W_main_in"] = dB[:, :F_in]
-        g["W_main_out"] = dB[:, F_in:2 * F_in]
-        g["W_undirected"] = dB[:, 2 * F_in:3 * F_in]
-        g["W_shared"] = g["W_main_in"] + g["W_main_out"] + g["W_undirected"]
-        g["b_main_in"] = g["b_dir_shared_in"] = dbsum[0]
-        g["b_main_out"] = g["b_dir_shared_out"] = dbsum[1]
-        g["b_undirected"] = g["b_undirected_shared"] = dbsum[2]
+        F_out = dB.size(0)
+        # Every weight and bias gradient is handed to autograd as its own contiguous tensor, so AccumulateGrad keeps it
+        # instead of copying it: column slices of dB break the parameters' layout contract (one strided copy each), and
+        # a bias sum shared by two parameters is copied for one of them. One copy lays dB out by segment
+        # ([segments, F_out, F_in]); W_shared = (W_in' + W_out') + W_und' as before; one copy doubles the bias sums.
+        Wg = dB.view(F_out, dB.size(1) // F_in, F_in).transpose(0, 1).contiguous()
+        g = {"W_main_in": Wg[0], "W_main_out": Wg[1], "W_undirected": Wg[2]}
+        ws = Wg[0] + Wg[1]
+        ws += Wg[2]
+        g["W_shared"] = ws
+        bb = dbsum[:3].unsqueeze(0).expand(2, 3, F_out).contiguous()
+        g["b_main_in"], g["b_dir_shared_in"] = bb[0, 0], bb[1, 0]
+        g["b_main_out"], g["b_dir_shared_out"] = bb[0, 1], bb[1, 1]
+        g["b_undirected"], g["b_undirected_shared"] = bb[0, 2], bb[1, 2]
         for q, name in enumerate(("C_in", "C_out", "C_directed", "C_undirected", "C_all")):
             v = prm[name]
             if not ctx.needs_input_grad[9 + _DENSE_KEYS.index(name)]:
@@ -1011,7 +1017,7 @@ class LayerDense(torch.autograd.Function):
                 d_res = dpre
             else:
                 d_res = out["dres"]
-                d_wres = dB[:, 3 * F_in:4 * F_in]
+                d_wres = Wg[3]
                 d_bres = dbsum[3]
         grads = [g[k] if ctx.needs_input_grad[9 + i] else None for i, k in enumerate(_DENSE_KEYS)]
         return (dZ, d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)

@@ -133,8 +133,8 @@ def test_ngram_spmm3_vs_oracle_and_fallback_widths(pkg, cuda):
 
 
 @pytest.mark.parametrize("n,keep", [(2, 1.0), (3, 1.0), (3, 0.5), (4, 1.0)])
-@pytest.mark.parametrize("F", [16, 48, 64, 128, 256])
-@pytest.mark.parametrize("kernel", ["mid", "block4"])
+@pytest.mark.parametrize("kernel,F", [("mid", F) for F in (16, 48, 64, 128, 256)]
+                         + [("block4", F) for F in (64, 128, 256)])  # the 4x4-block kernel takes F in {64, 128, 256}
 def test_ngram_transposed_bf16(pkg, cuda, n, keep, F, kernel):
     """bf16 transposed tile kernels (bf16 rows, fp32 sums, one rounding): the middle-tile kernel with the diagonal term
     in-kernel (pg_spmm3t_ngram_mid_bf16, PG_FLAG_MID_TRANSPOSED; F % 16 == 0) and the 4x4-block one
@@ -143,8 +143,6 @@ def test_ngram_transposed_bf16(pkg, cuda, n, keep, F, kernel):
     and determinism."""
     from protgram_directgcn_amd import ops
     from protgram_directgcn_amd._lib import PG_FLAG_MID_TRANSPOSED, load_library
-    if kernel == "block4" and F not in (64, 128, 256):
-        pytest.skip("the 4x4-block kernel takes F in {64, 128, 256}")
     g = _graph(pkg, cuda, n, keep)
     N = g.n_rows
     G = torch.randn(N, 3 * F, generator=torch.Generator().manual_seed(n * 10 + F)).to(cuda).to(torch.bfloat16)

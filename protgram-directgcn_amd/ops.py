@@ -653,13 +653,14 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
                 act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                out: Optional[torch.Tensor] = None, pregated: bool = False) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, pregated: bool = False, packs: Optional[list] = None) -> torch.Tensor:
     """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header). bf16 Z ->
-    pg_directgcn_dense_bf16 (bf16 output)."""
+    pg_directgcn_dense_bf16 (bf16 output; `packs`, when given, receives its packed weights (fp32, bf16) so that the
+    backward of the same step reuses them)."""
     lib = load_library()
     _require_gpu(Z)
     if _is_bf16(Z):
-        Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags)
+        Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs)
         if Y is None:
             Y = layer_dense(Z.float(), prm, gate_mode, rows, constant, None if res_x is None else res_x.float(),
                             W_res, b_res, act, slope, flags).to(torch.bfloat16)
@@ -744,9 +745,11 @@ def layer_dense_ngram_rows(Z, prm: dict, gate_mode: int, Kn1: int, m0: int, cons
     return Y
 
 
-def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags):
+def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs=None):
     lib = load_library()
     packed, p16 = pack_weights_bf16(prm, W_res, b_res)
+    if packs is not None:
+        packs[:] = [packed, p16]
     M = Z.size(0)
     F_out = prm["W_main_in"].size(0)
     Y = torch.empty(M, F_out, device=Z.device, dtype=torch.bfloat16)
@@ -765,12 +768,14 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
 
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
                          act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                         need_dZ: bool = True):
+                         need_dZ: bool = True, packs: Optional[list] = None):
     """pg_directgcn_dense_bwd_f32 (any shape; bf16 operands: pg_directgcn_dense_bwd_bf16, None when F_in / F_out
     are not multiples of 8 -- the caller then runs the fp32 kernels on widened copies). Returns a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
       dgate [5, M] (per-row grads of c_in, c_out, c_directed, c_undirected, c_all),
-      dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out]."""
+      dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out].
+    packs: the bf16 forward's packed weights of the same parameters (LayerDense: saved by its forward), else packed
+    here."""
     lib = load_library()
     _require_gpu(dY, Z, Y)
     M, F_in = Z.size(0), Z.size(1) // 3
@@ -779,7 +784,7 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     if bf and (F_in % 8 or F_out % 8):
         return None
     if bf:
-        packed, p16 = pack_weights_bf16(prm, W_res, b_res)
+        packed, p16 = packs if packs else pack_weights_bf16(prm, W_res, b_res)
         Y = _bf16c(Y)
     else:
         packed = pack_weights(prm, W_res, b_res)
@@ -941,8 +946,11 @@ class LayerDense(torch.autograd.Function):
     @_fwd32
     def forward(ctx, Z, res_x, constant, W_res, b_res, rows, gate_mode, act, slope, *params):
         prm = dict(zip(_DENSE_KEYS, params))
+        # the bf16 kernels' packed weights are kept for the backward (the parameters are saved tensors: autograd
+        # refuses a backward after an in-place change to them, so the packed copies cannot go stale before it)
+        ctx.packs = []
         Y = layer_dense(Z, prm, gate_mode, rows=rows, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
-                        act=act, slope=slope)
+                        act=act, slope=slope, packs=ctx.packs)
         ctx.gate_mode, ctx.act, ctx.slope = gate_mode, act, slope
         ctx.has_res, ctx.has_const = res_x is not None, constant is not None
         ctx.save_for_backward(Z, res_x if res_x is not None else Z.new_empty(0),
@@ -961,8 +969,9 @@ class LayerDense(torch.autograd.Function):
         constant = constant if ctx.has_const else None
         W_res = W_res if ctx.has_wres else None
         rows = rows if ctx.has_rows else None
+        packs, ctx.packs = ctx.packs, None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
-                                   act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
+                                   act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], packs=packs)
         if out is None:  # bf16 shapes the bf16 kernels do not take: the fp32 kernels on widened copies
             out = layer_dense_backward(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows=rows,
                                        res_x=None if res_x is None else res_x.float(), W_res=W_res, act=ctx.act,

@@ -11,7 +11,10 @@
 // head_f128_kernel, its fp32-MFMA predecessor, with -DPG_HEAD_FP32). A persistent form of head_x3_kernel (W1 splits
 // and W2 kept in registers across a block's 32-row tiles, next tile's rows loaded behind the math; 128 VGPRs, four
 // blocks per CU) measured 0.062 ms against 0.050 for one tile per block; two 32-row tiles per block (W1 splits loaded
-// once per block; 128 VGPRs, occupancy 4) made the bench step 0.547 -> 0.580 ms (round 3).
+// once per block; 128 VGPRs, occupancy 4) made the bench step 0.547 -> 0.580 ms (round 3). Round 4: unconditional W2
+// loads (no per-lane branch join, whose vmcnt(0) waited on the h rows an HBM round trip early) 47.6 -> 45.8 us per
+// launch (bench HIP events, two runs); W1 loaded first with its split pinned ahead of the h rows' arrival measured
+// 47.5 us (112 VGPRs, occupancy 4; forcing 5 spills), so the split stays where the compiler puts it.
 #include "pg_common.h"
 #include "pg_split3.h"
 
@@ -384,11 +387,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     float4 w2f[4];
     {
+        // classes c >= C load row 0 instead of zeros: their logit columns (Ls[.., c]) are never read by the softmax,
+        // and unconditional loads keep the compiler from waiting on every load in flight (h included) at a
+        // per-lane branch join (a vmcnt(0) one HBM round trip early)
         const int c = 16 * (wave >> 1) + li;
-        const bool cok = c < p.C;
-        const float* w2row = p.W2 + (int64_t)(cok ? c : 0) * H + 4 * q;
+        const float* w2row = p.W2 + (int64_t)(c < p.C ? c : 0) * H + 4 * q;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) w2f[m] = cok ? ld4(w2row + 16 * m) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int m = 0; m < 4; ++m) w2f[m] = ld4(w2row + 16 * m);
     }
     const float b1v = p.b1[16 * wave + li];
     const int c2 = 16 * (wave >> 1) + li;

@@ -360,28 +360,31 @@ def main():
     head_name = "pg_directgcn_head_" + ("bf16" if args.bf16 else "f32")
     per_step = {"propagation": L, "dense": L, "head": 1}
 
-    def entry(cls, name, nbytes, extra=None):
-        ms = avg_ms[cls]
+    def kernel_entry(cls, name, nbytes, extra=None):
+        # every derived field is computed from the EMITTED avg_launch_ms (rounded to 1 ns), so a reader recomputing
+        # achieved / frac from the line gets the same numbers up to the 0.1 GB/s rounding of achieved
+        ms = round(avg_ms[cls], 6)
         ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         e = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes_per_launch": int(nbytes),
-             "avg_launch_ms": round(ms, 4), "launches_timed": len(kms[cls]), "launches_per_step": per_step[cls],
-             "ms_per_step": round(ms * per_step[cls], 4)}
+             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "algorithmic_bytes_per_launch": int(nbytes),
+             "avg_launch_ms": ms, "launches_timed": len(kms[cls]), "launches_per_step": per_step[cls],
+             "ms_per_step": round(ms * per_step[cls], 6)}
         if extra:
             e.update(extra)
         return e
 
     kernels = {
-        "propagation": entry("propagation", kname, comp,
+        "propagation": kernel_entry("propagation", kname, comp,
                              {"no_reuse_bytes_per_launch": noreuse,
-                              "no_reuse_gbs": round(noreuse / (spmm_avg_ms * 1e-3) / 1e9, 1) if spmm_avg_ms else None,
+                              "no_reuse_gbs": (round(noreuse / (round(spmm_avg_ms, 6) * 1e-3) / 1e9, 1)
+                                               if round(spmm_avg_ms, 6) else None),
                               "bytes_model": "compulsory: the kernel's own inputs once (n-gram tile kernel: its plan "
                                              "weights; CSR kernels: 8(N+1) rowptr + 16 B records per entry, SURVEY "
                                              "8d) + X once + 3 output rows (+ 20 B/row gates)"}),
-        "dense": entry("dense", dense_name, dense_comp,
+        "dense": kernel_entry("dense", dense_name, dense_comp,
                        {"bytes_model": "Z (3F) + residual row (F) + per-node constant (F_out, fp32) + 5 gates (fp32) "
                                        "+ output row, per row; + the layer's weights"}),
-        "head": entry("head", head_name, head_comp,
+        "head": kernel_entry("head", head_name, head_comp,
                       {"bytes_model": "h row + log-probs + L2-normalised embedding (fp32), per row; + the decoder"}),
     }
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
@@ -411,7 +414,7 @@ def main():
                 ent["traffic_source"] = pmc["traffic_source"]
                 ms = ent["avg_launch_ms"]
                 ent["traffic_gbs"] = round(ent["traffic"] / (ms * 1e-3) / 1e9, 1) if ms else None
-                ent["traffic_frac"] = round(ent["traffic_gbs"] / HBM_PEAK_GBS, 4) if ms else None
+                ent["traffic_frac"] = round(ent["traffic"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if ms else None
                 ent["traffic_over_compulsory"] = round(ent["traffic"] / ent["algorithmic_bytes_per_launch"], 3)
 
     extra = {}
@@ -422,7 +425,7 @@ def main():
         line = {
             "metric": "edges/sec propagated, DirectGCN fwd on 4-gram graph, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 6), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "bf16" if args.bf16 else "f32", "data": "synthetic",
             "config": {"workload": wl["workload"], "graph": wl["desc"],
                        "num_nodes": N, "transitions": int(wl["E"]), "nnz_per_adjacency": g.nnz, "feat_dim": Fd,

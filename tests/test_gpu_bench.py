@@ -24,14 +24,18 @@ def test_bench_json_line_is_self_consistent():
         assert out["metric"] == json.load(f)["metric"]
     assert out["n_gpus"] == 1 and out["steps"] == 5 and out["warmup"] == 2 and out["higher_is_better"] is True
     cfg = out["config"]
+    # the default entry is the reference trainer's COO wiring (bench.py --entry coo)
+    assert cfg["entry"].startswith("trainer COO"), cfg["entry"]
     assert cfg["num_nodes"] == 160_000 and cfg["nnz_per_adjacency"] == 6_559_580 and cfg["feat_dim"] == 128
     edges = 3 * cfg["nnz_per_adjacency"] * cfg["layers"]
     assert abs(out["value"] - edges / (out["ms_per_step"] * 1e-3)) <= 2e-3 * out["value"]
     rf = out["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    # bench.py derives achieved / frac from the avg_launch_ms it emits: recomputing them from the line differs only
+    # by the 0.1 GB/s rounding of achieved (no dependence on the measured time's digits)
     achieved = rf["algorithmic_bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
-    assert abs(rf["achieved"] - achieved) <= 1e-3 * achieved + 0.1
-    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) <= 1e-3
+    assert abs(rf["achieved"] - achieved) <= 0.051 + 1e-9 * achieved
+    assert abs(rf["frac"] - achieved / rf["peak"]) <= 1e-5
     assert 0.0 < rf["frac"] < 1.0  # compulsory bytes: physically below peak
     # the dominant kernel is one of the step's kernels: its launches take less than the whole step
     assert rf["avg_launch_ms"] < out["ms_per_step"]
@@ -41,10 +45,12 @@ def test_bench_json_line_is_self_consistent():
     assert set(ks) == {"propagation", "dense", "head"}
     for k, e in ks.items():
         a = e["algorithmic_bytes_per_launch"] / (e["avg_launch_ms"] * 1e-3) / 1e9
-        assert abs(e["achieved"] - a) <= 1e-3 * a + 0.1, k
+        assert abs(e["achieved"] - a) <= 0.051 + 1e-9 * a, k
         assert 0.0 < e["frac"] < 1.0 and e["launches_timed"] >= e["launches_per_step"], k
     assert rf["kernel"] == max(ks.values(), key=lambda e: e["ms_per_step"])["kernel"]
-    assert sum(e["ms_per_step"] for e in ks.values()) <= out["ms_per_step"] * 1.05
+    # per-kernel times come from eager steps after the timed (graph-replay) region: a loose bound, so that clock
+    # drift between the two phases cannot flip it
+    assert sum(e["ms_per_step"] for e in ks.values()) <= out["ms_per_step"] * 1.5
     assert ks["propagation"]["algorithmic_bytes_per_launch"] == 411_520_000  # SURVEY 8(d) / DESIGN §4 at B(20,4)
     assert abs(ks["dense"]["algorithmic_bytes_per_launch"] - 494.7e6) < 0.5e6
 

@@ -1147,10 +1147,16 @@ class MiddleRunner:
 # all-gather + N x F reduce-scatter. Reference: protgram_directgcn_trainer.py:76-108 (loop), config.py:63 (dims).
 class TorchComm:
     """The collectives the middle trainer uses, over torch.distributed (RCCL for CUDA tensors on 'nccl'; gloo stages
-    device tensors through host buffers)."""
+    device tensors through host buffers).
+
+    `capturable` (RCCL only): every call is a synchronous-form torch.distributed collective on the caller's current
+    stream, so inside a HIP-graph capture (MiddleTrainer(graphs=True)) ProcessGroupNCCL's fork onto its RCCL stream and
+    the join back (event record / stream wait) are captured with the RCCL kernels, and each replay re-runs the
+    exchange on the same buffers. gloo stages through host memory (`.cpu()` synchronises): not capturable."""
 
     def __init__(self, group=None):
         self.group = group
+        self.capturable = dist.is_initialized() and dist.get_backend(group) == "nccl"
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits):
         if inp.is_cuda and dist.get_backend(self.group) == "gloo":
@@ -1554,6 +1560,14 @@ class MiddleTrainer:
         self._graph.replay()
         return self._loss
 
+    def close(self):
+        """Release the captured step (its graph holds RCCL kernels of this process group's communicator): call before
+        destroy_process_group. Later steps run eagerly again until the next capture."""
+        torch.cuda.synchronize()
+        self._graph = None
+        self._keep = None
+        self._eager_steps = 0
+
     def _capture(self, x_full, y_own):
         self._x, self._y = x_full, y_own
         torch.cuda.synchronize()
@@ -1613,7 +1627,7 @@ class MiddleTrainer:
                 if id(p) not in self._touched:
                     p.grad = None
             l2_rep = l2_own = zero
-        if self.xchg and mp.world > 1 and self.flat.numel():
+        if self.xchg and (mp.world > 1 or FORCE_COLLECTIVES) and self.flat.numel():
             self.comm.all_reduce(self.flat)
         if lam and not fold:
             ps = [p for p in self.params if p.grad is not None]
@@ -1633,7 +1647,7 @@ class MiddleTrainer:
             l2_rep = sums[gd] if gd is not None and sums[gd] is not None else zero
             l2_own = sums[gn] if gn is not None and sums[gn] is not None else zero
         parts = torch.stack([nll.detach().reshape(()), (lam * l2_own).reshape(())])
-        if self.xchg and mp.world > 1:
+        if self.xchg and (mp.world > 1 or FORCE_COLLECTIVES):
             self.comm.all_reduce(parts)
         return parts.sum() + lam * l2_rep
 

@@ -32,7 +32,12 @@ def _free_port():
 
 def _worker(rank, world, port, out_q, bf16):
     import faulthandler
+    import time
+    t_start = time.time()
     faulthandler.dump_traceback_later(150, exit=True)  # a stuck rank prints where it is and exits (the parent fails)
+
+    def phase(what):  # per-rank progress on stderr (pytest -s shows it): where the time of a slow run goes
+        print(f"[p8 rank {rank} bf16={bf16}] {what} at {time.time() - t_start:.1f}s", file=sys.stderr, flush=True)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [REPO, HERE]
     import torch.distributed as dist
@@ -43,6 +48,7 @@ def _worker(rank, world, port, out_q, bf16):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    phase("process group up")
     bad = []
     try:
         n, dims, lam = 4, [128, 256, 256, 256], 1e-7
@@ -59,6 +65,7 @@ def _worker(rank, world, port, out_q, bf16):
         loss_r = float(loss_r.detach())
         del ref, lp
         torch.cuda.synchronize()
+        phase("single-GPU reference step done")
         # this rank of the middle partition
         mp_ = shard.middle_partition(g, rank, world)
         m = _model(pkg, dims, N, n).to(dev).eval()
@@ -70,8 +77,10 @@ def _worker(rank, world, port, out_q, bf16):
         hits = []
         real = ops.spmm3_middles
         ops.spmm3_middles = lambda *a, **k: hits.append(1) or real(*a, **k)
+        phase("trainer built")
         loss = float(tr.step(x, y[mp_.own]))
         torch.cuda.synchronize()
+        phase("trainer step done")
         if len(hits) != len(dims) - 1:
             bad.append(("middle-tile launches", len(hits)))
         if bf16:

@@ -42,6 +42,54 @@ def _model(pkg, N, dims, dev, n):
     return model.to(dev).eval()
 
 
+class _LoopbackComm:
+    """World-1 collectives in-process: all_to_all = copy, all_reduce = identity (capturable)."""
+    capturable = True
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        out.copy_(inp)
+
+    def all_reduce(self, t):
+        pass
+
+
+def _middle_trainer_rccl(pkg, shard, dev, steps=6):
+    import torch.distributed as dist
+    bad = []
+    n, dims = 3, [64, 64, 64, 32]
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(7)).to(dev)
+    y = ((torch.arange(N, device=dev) // 400) % 20)
+    mp_ = shard.middle_partition(g, 0, 1, chunks=2, loopback=True)
+    comm = shard.TorchComm()
+    if not comm.capturable or dist.get_backend() != "nccl":
+        return [("TorchComm not capturable on nccl",)]
+    shard.FORCE_COLLECTIVES = True
+    try:
+        for dt in (torch.float32, torch.bfloat16):
+            res = {}
+            for name, cm, graphs in (("loopback", _LoopbackComm(), False), ("rccl", comm, False),
+                                     ("rccl_graph", comm, True)):
+                m = _model(pkg, N, dims, dev, n)
+                m.compute_dtype = dt
+                tr = shard.MiddleTrainer(m, mp_, l2_lambda=1e-3, comm=cm, graphs=graphs)
+                losses = [float(tr.step(x, y[mp_.own])) for _ in range(steps)]
+                torch.cuda.synchronize()
+                if graphs and tr._graph is None:
+                    bad.append((str(dt), name, "not captured"))
+                res[name] = (losses, [p.detach().clone() for p in tr.params])
+                tr.close()
+            for name in ("rccl", "rccl_graph"):
+                if res[name][0] != res["loopback"][0]:
+                    bad.append((str(dt), name, "losses", res[name][0], res["loopback"][0]))
+                if not all(torch.equal(a, b) for a, b in zip(res[name][1], res["loopback"][1])):
+                    bad.append((str(dt), name, "parameters differ"))
+    finally:
+        shard.FORCE_COLLECTIVES = False
+    return bad
+
+
 def _worker(port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     sys.path[:0] = [REPO, HERE]
@@ -128,12 +176,22 @@ def _worker(port, out_q):
                 if not close(v, res[True][1][k]):
                     bad.append((str(dt), "trainer param", k, float((v - res[True][1][k]).abs().max())))
         shard.FORCE_COLLECTIVES = False
+        # ---- MiddleTrainer (config 5's trainer) on a loopback middle partition over RCCL: the product's TorchComm,
+        # eager and HIP-graph captured (the RCCL all_to_all / all_reduce inside the captured step), against the same
+        # steps with an in-process loopback comm (copy / identity): bit for bit, fp32 and bf16
+        bad += _middle_trainer_rccl(pkg, shard, dev)
         out_q.put((not bad, str(bad[:6])))
     except Exception as e:  # report, then re-raise for the exit code
         out_q.put((False, repr(e)))
         raise
     finally:
+        import faulthandler
+        import gc
+        gc.collect()  # the captured graphs (their RCCL kernels) go before the communicator
+        torch.cuda.synchronize()
+        faulthandler.dump_traceback_later(45, exit=True)  # a teardown that hangs prints where, and the rank exits
         dist.destroy_process_group()
+        faulthandler.cancel_dump_traceback_later()
 
 
 @pytest.mark.timeout(240)
@@ -143,6 +201,9 @@ def test_rccl_paths_world1(pkg, cuda):
     p = ctx.Process(target=_worker, args=(_free_port(), q))
     p.start()
     ok, msg = q.get(timeout=220)
-    p.join(timeout=60)
+    p.join(timeout=90)
+    if p.exitcode is None:  # never leave a stuck rank behind (pytest would wait for it at exit)
+        p.kill()
+        p.join(timeout=10)
     assert p.exitcode == 0, msg
     assert ok, msg

@@ -692,8 +692,15 @@ struct DgradB {
     int remap;
 };
 
+// Reproducibility (round 5). With packed-FP32 VALU math (v_pk_fma_f32 / v_pk_mul_f32, formed by the SLP vectoriser
+// from the lead tile's bias dots) this kernel's segment-0 gate partials came out wrong for 4-row groups (lanes 48-63
+// of a wave; up to 0.8 % of one partial) in about half of the runs with cold caches, while its accumulators, its A
+// images and its epilogue products were bit-identical (stage dumps of a diagnostics build, tools/r05_dgrad_dbg.py);
+// padding after the wave's own MFMAs did not help, the same source built without SLP vectorisation is reproducible.
+// pg_dense_bwd.hip is therefore compiled with -fno-slp-vectorize (Makefile). The occupancy bound is 2 waves per SIMD
+// (154 VGPRs): at 4 (128 VGPRs) the compiler spilled 76 B per lane to scratch and the kernel ran 5 % slower.
 template <int BM, int BN, int NW>
-__global__ __launch_bounds__(64 * NW, 4) void dgrad_bf16_kernel(DgradB p) {
+__global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
     using namespace pgbf;
     constexpr int NT = 64 * NW;
     constexpr int WN = 2, WM = NW / WN;

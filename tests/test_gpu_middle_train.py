@@ -2,10 +2,11 @@
 8 MI355X) through shard.MiddleTrainer at its size: P = 8 ranks as 8 processes sharing this one GPU, gloo carrying
 the ghost-row exchanges, their transposes and the gradient all-reduce (the same calls RCCL runs on the 8-GPU node;
 tests/test_gpu_rccl.py runs the RCCL branch itself). Every rank propagates its middles on the middle-tile kernel
-(launches counted) and backpropagates through the transposed CSR kernel over its column block.
+(launches counted) and backpropagates in scatter form (pg_spmm3t_ngram_scatter_*: its middles' dZ to the D / P / S
+row sets, the ghost rows' sums back to their owners).
 
-Each rank checks its own share against the single-GPU step on the same model and inputs (computed in the rank's
-process before the trainer runs): the global loss, every replicated parameter gradient after the all-reduce and the
+Each rank checks its own share against the single-GPU step on the same model and inputs (computed once in the test's
+process and loaded by the ranks): the global loss, every replicated parameter gradient after the all-reduce and the
 owned rows of every per-node parameter gradient (plus the L2 term 2 lam p, which the trainer's train.Adam folds
 into its update instead of the gradient). fp32: |d| <= 1e-4 max|ref| + 1e-4 |ref| (the kernels sum in
 other orders than the single-GPU step's); bf16 mode against the fp32 step (as test_gpu_configs' config-5 test):
@@ -30,11 +31,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_q, bf16):
+def _reference(pkg, path):
+    """The single-GPU fp32 step (loss and every parameter gradient) on the config-5 model and inputs, computed ONCE
+    in the test's own process and saved for the ranks (round 4 had every rank compute it: 8 full-graph steps at once
+    on one GPU, 14-73 s, whose slow runs crossed the ranks' 150 s watchdog -- the intermittent 'stall')."""
+    from protgram_directgcn_amd import train
+    from test_gpu_configs import _labels, _model
+    n, dims, lam = 4, [128, 256, 256, 256], 1e-7
+    dev = torch.device("cuda", 0)
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=dev)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(dev)
+    y = _labels(N, n).to(dev)
+    ref = _model(pkg, dims, N, n).to(dev).eval()
+    lp, _ = ref(pkg.Data(x=x, graph=g))
+    loss_r = train.nll_mean(lp, y) + lam * sum(p.norm(2).pow(2) for p in ref.parameters())
+    loss_r.backward()
+    torch.save({"loss": float(loss_r.detach()),
+                "grads": {k: p.grad.detach().float().cpu() for k, p in ref.named_parameters()}}, path)
+    del ref, lp, g
+    torch.cuda.empty_cache()
+
+
+def _worker(rank, world, port, out_q, bf16, ref_path):
     import faulthandler
     import time
     t_start = time.time()
-    faulthandler.dump_traceback_later(150, exit=True)  # a stuck rank prints where it is and exits (the parent fails)
+    faulthandler.dump_traceback_later(300, exit=True)  # a stuck rank prints where it is and exits (the parent fails)
 
     def phase(what):  # per-rank progress on stderr (pytest -s shows it): where the time of a slow run goes
         print(f"[p8 rank {rank} bf16={bf16}] {what} at {time.time() - t_start:.1f}s", file=sys.stderr, flush=True)
@@ -43,7 +66,7 @@ def _worker(rank, world, port, out_q, bf16):
     import torch.distributed as dist
     from __graft_entry__ import load_package
     pkg = load_package()
-    from protgram_directgcn_amd import ops, shard, train
+    from protgram_directgcn_amd import ops, shard
     from test_gpu_configs import _labels, _model
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -56,16 +79,9 @@ def _worker(rank, world, port, out_q, bf16):
         g = pkg.build_propagation_csr(N, s, d, c, device=dev)
         x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(dev)
         y = _labels(N, n).to(dev)
-        # single-GPU reference step (fp32): loss and gradients
-        ref = _model(pkg, dims, N, n).to(dev).eval()
-        lp, _ = ref(pkg.Data(x=x, graph=g))
-        loss_r = train.nll_mean(lp, y) + lam * sum(p.norm(2).pow(2) for p in ref.parameters())
-        loss_r.backward()
-        rgrad = {k: p.grad.detach().float().clone() for k, p in ref.named_parameters()}
-        loss_r = float(loss_r.detach())
-        del ref, lp
-        torch.cuda.synchronize()
-        phase("single-GPU reference step done")
+        saved = torch.load(ref_path, weights_only=True, mmap=True)  # the single-GPU step, from the parent
+        loss_r, rgrad = saved["loss"], saved["grads"]
+        phase("reference loaded")
         # this rank of the middle partition
         mp_ = shard.middle_partition(g, rank, world)
         m = _model(pkg, dims, N, n).to(dev).eval()
@@ -93,9 +109,10 @@ def _worker(rank, world, port, out_q, bf16):
             r = rgrad[name]
             if shard._is_node_param(name, p, N):
                 gg = tr.own[int(name.split(".")[1])][name.split(".")[-1]].grad
-                r = r[own]
+                r = r[own.cpu()]
             else:
                 gg = p.grad
+            r = r.to(dev)
             if gg is None:
                 bad.append((name, "no grad"))
                 continue
@@ -145,14 +162,20 @@ def _collect(q, procs, n, limit):
     return res
 
 
+_REF = {}
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("bf16", [False, True])
-def test_config5_middle_trainer_p8_one_gpu(cuda, bf16):
+def test_config5_middle_trainer_p8_one_gpu(pkg, cuda, bf16, tmp_path_factory):
+    if "path" not in _REF:  # one single-GPU reference step for both cases
+        _REF["path"] = str(tmp_path_factory.mktemp("p8ref") / "ref.pt")
+        _reference(pkg, _REF["path"])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, bf16)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, bf16, _REF["path"])) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = sorted(_collect(q, procs, WORLD, 840))

@@ -621,6 +621,55 @@ def test_dense_backward_deterministic(pkg, cuda):
             assert torch.equal(a[k], c[k]), k
 
 
+_FLUSH = []
+
+
+def _poison_allocator(dev, seed):
+    """Allocate and free blocks of many sizes filled with random bits: the caching allocator hands them out again,
+    and the caches go cold (the condition under which the round-4 bf16 dense backward's gate gradients varied)."""
+    import os
+    if os.environ.get("PG_POISON_MODE") == "flush":  # diagnostics: cold caches only, no reused blocks
+        if not _FLUSH:
+            _FLUSH.append(torch.empty(1 << 29, device=dev))
+        _FLUSH[0].fill_(float(seed))
+        torch.cuda.synchronize()
+        return
+    g = torch.Generator(device=dev).manual_seed(seed)
+    keep = []
+    for k in range(8, 25):
+        for _ in range(2):
+            t_ = torch.empty(1 << k, device=dev)
+            t_.view(torch.int32).random_(generator=g)
+            keep.append(t_)
+    torch.cuda.synchronize()
+    del keep
+
+
+def test_dense_backward_bf16_deterministic(pkg, cuda):
+    """bf16 twin of test_dense_backward_deterministic, with the allocator's blocks poisoned and the caches cold before
+    each call: every output bit-identical over 12 calls (round 4: the lead n-tile's segment-0 gate partials of two
+    rows in eight differed in the last bit in about half of such runs, while the kernel spilled registers to scratch;
+    tools/r05_dgrad_bf16_probe.py)."""
+    from protgram_directgcn_amd import ops
+    Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(20000, 128, 128, False, True, False, 3)
+    dv = {k: v.to(cuda) for k, v in prm.items()}
+    Zg, dYg, xg = Z.to(cuda).to(torch.bfloat16), dY.to(cuda).to(torch.bfloat16), xres.to(cuda).to(torch.bfloat16)
+    packs = []
+    Y = ops.layer_dense(Zg, dv, 0, res_x=xg, act=True, packs=packs)
+    assert Y.dtype == torch.bfloat16 and len(packs) == 2
+    ref = None
+    for rep in range(12):
+        _poison_allocator(cuda, rep)
+        out = ops.layer_dense_backward(dYg, Zg, Y, dv, 0, res_x=xg, act=True, packs=packs)
+        assert out is not None
+        out = {k: v.clone() for k, v in out.items() if v is not None}
+        if ref is None:
+            ref = out
+            continue
+        for k in ("dpre", "dZ", "dgate", "dB", "dbsum"):
+            assert torch.equal(out[k], ref[k]), (rep, k, int((out[k] != ref[k]).sum()))
+
+
 @pytest.mark.parametrize("M,P,N", [(160000, 20, 64), (160000, 64, 128), (1000, 128, 384), (33, 4, 8), (0, 8, 8),
                                    (70001, 256, 132)])
 def test_gemm_at_b_vs_float64(pkg, cuda, M, P, N):

@@ -22,27 +22,55 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 dev = torch.device("cuda", 0)
 M, F = 8000, 128
 K = 3 * F
-gen = torch.Generator().manual_seed(3)
 
 
-def rnd(*s, scale=1.0):
-    return (torch.randn(*s, generator=gen) * scale).to(dev)
+from protgram_directgcn_amd import shard  # noqa: E402
+
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from test_gpu_rccl import _model  # noqa: E402
+
+rec = []
+real_bwd = ops.layer_dense_backward
 
 
-conv = pkg.DirectGCNLayer(F, F, M, True).to(dev)
-with torch.no_grad():
-    for name, p in conv.named_parameters():
-        if name.startswith("C_"):
-            p.copy_(torch.rand(p.shape, generator=gen).to(dev) + 0.5)
-prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
-Z = rnd(M, K).to(torch.bfloat16)
-Y = rnd(M, F).to(torch.bfloat16)
-dY = rnd(M, F, scale=1e-3).to(torch.bfloat16)
-packed, p16 = ops.pack_weights_bf16(prm)
+def rec_bwd(dY, Z, Y, prm, gate_mode, **kw):
+    rec.append((dY.detach().clone(), Z.detach().clone(), Y.detach().clone(),
+                {k: v.detach().clone() for k, v in prm.items()}, [t.clone() for t in (kw.get("packs") or [])]))
+    return real_bwd(dY, Z, Y, prm, gate_mode, **kw)
+
+
+ops.layer_dense_backward = rec_bwd
+Ng, sg, dg, cg = pkg.synth.de_bruijn_edges(3)
+gph = pkg.build_propagation_csr(Ng, sg, dg, cg, device=dev)
+xg = torch.randn(Ng, 128, generator=torch.Generator().manual_seed(1234)).to(dev)
+yg = (torch.arange(Ng, device=dev) // 400) % 20
+mdl = _model(pkg, Ng, [128, 128, 128], dev, 3)
+mdl.compute_dtype = torch.bfloat16
+shard.ShardedTrainer(mdl, shard.partition(gph, 0, 1, transpose=True), lr=1e-3, l2_lambda=1e-3).step(xg, yg)
+torch.cuda.synchronize()
+ops.layer_dense_backward = real_bwd
+dY, Z, Y, prm, packs = rec[0]  # the last layer's backward (autograd runs it first)
+packed, p16 = packs
 lib = ops.load_library()
 
 
+POISON = {"mode": None}
+
+
+def poison():
+    keep = []
+    for k in range(8, 25):
+        for _ in range(2):
+            t = torch.empty(1 << k, device=dev)
+            t.view(torch.int32).random_() if POISON["mode"] == "random" else t.fill_(1e30)
+            keep.append(t)
+    del keep
+
+
 def run(flags):
+    if POISON["mode"] in ("random", "big"):
+        poison()
+    shift = torch.empty(int(torch.randint(1, 4096, (1,))), device=dev) if POISON["mode"] == "shift" else None
     a, keep = ops._layer_args(Z, prm, 0, None, None, None, None, True, ops.LEAKY_SLOPE, Y=Y)
     dpre = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
     dZ = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
@@ -63,12 +91,18 @@ def run(flags):
     off_dsp = K * F  # plan_of: up4(K * F_out) floats of (bf16) BT first
     ntn = K // 128
     dsp = work[off_dsp:off_dsp + ntn * 3 * M].view(ntn, 3, M).clone()
-    del keep
+    del keep, shift
     return {"dsp": dsp, "dgate": dgate, "dZ": dZ, "dpre": dpre, "dW": dW}
 
 
 out = {}
-for fname, fl in (("default", ops.default_flags()), ("no_remap", ops.default_flags() | _lib.PG_FLAG_NO_XCD_REMAP)):
+MODES = (("plain", ops.default_flags(), None), ("poison_random", ops.default_flags(), "random"),
+         ("poison_big", ops.default_flags(), "big"), ("shift", ops.default_flags(), "shift"),
+         ("no_remap_random", ops.default_flags() | _lib.PG_FLAG_NO_XCD_REMAP, "random"))
+if os.environ.get("PROBE_MODES"):
+    MODES = tuple(m for m in MODES if m[0] in os.environ["PROBE_MODES"].split(","))
+for fname, fl, mode in MODES:
+    POISON["mode"] = mode
     ref = run(fl)
     var = {}
     for r in range(reps):
@@ -98,4 +132,6 @@ for fname, fl in (("default", ops.default_flags()), ("no_remap", ops.default_fla
                          "ref_bd": float(bd[m, q]), "ref_sum": float(part[m, q] + bd[m, q]) if nt == 0 else None})
         det["dsp_samples"] = samp
     out[fname] = det
-    print(json.dumps({fname: det}, default=str), flush=True)
+    print(json.dumps({"lib": os.environ.get("PG_DIRECTGCN_LIB", "default"), fname: {
+        k: (v if k == "dsp_samples" else {"reps": v["reps"], "n_where": v["n_where"]}) for k, v in det.items()}},
+        default=str), flush=True)

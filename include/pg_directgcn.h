@@ -77,6 +77,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_TILED (1u << 15)    /* dense forward: the tiled fp32 kernel even where the split-bf16 W-stationary
                                             kernels apply (F_out = 128, K = 384 or 256, no row map: the default) */
 #define PG_FLAG_DENSE_X3 (1u << 16)       /* dense backward: the split-bf16 weight gradient (opt-in) */
+#define PG_FLAG_DGRAD_F32MFMA (1u << 17)  /* fp32 dense backward: the fp32-MFMA input-gradient kernel instead of the
+                                           * split-bf16 one (the default where F_out % 32 == 0) */
 #define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */
 #define PG_FLAG_NGRAM_BLOCK4 (1u << 21)   /* host-side: the 4x4-block n-gram forward (pg_spmm3_ngram_f32) instead of the
                                              middle-tile kernel (pg_spmm3_ngram_mid_f32) */
@@ -359,7 +361,9 @@ int pg_rows_gather_sum(const float* A, int64_t lda, const void* B, int64_t ldb, 
  * work: pg_directgcn_dense_bwd_workspace(args) floats. Deterministic (fixed-order reductions).
  * Returns PG_ERR_UNSUPPORTED unless F_in, F_out and every leading dimension are multiples of 4 and the
  * buffers 16-B aligned. Five launches on `stream`: transpose, dgrad (MFMA), gate grads, wgrad (MFMA,
- * split over rows), split reduction. */
+ * split over rows), split reduction. Where F_out % 32 == 0 dgrad runs on the bf16 matrix cores in the exact
+ * three-way split (six bf16 products per fp32 product, fp32 sums; the transpose also splits the packed weights),
+ * unless flags has PG_FLAG_DGRAD_F32MFMA (the fp32-MFMA kernel). */
 typedef struct pg_layer_grad_args {
     const float* dY; int64_t lddy;
     float* dpre; int64_t ldp;

@@ -305,6 +305,291 @@ __global__ __launch_bounds__(64 * NW) void dgrad_kernel(DgradP p) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// dgrad_x3_kernel (round 5; the fp32 default where F_out % 32 == 0): dgrad_kernel's tiling, outputs and epilogue
+// with the products on the bf16 matrix cores in the exact three-way split (pg_split3.h): every fp32 operand value
+// v = v0 + v1 + v2 (bf16 each), G = sum of the six products a_i b_j with i + j <= 2 on v_mfma_f32_32x32x16_bf16,
+// fp32 accumulation (the dropped terms are below 2^-24 |a b|; the forward's split-bf16 kernel makes the same
+// choice). The 32x32x16 bf16 form takes 6 x 32 cycles per 16-deep k-step where v_mfma_f32_32x32x2f32 takes 8 x 64:
+// 2.7x fewer matrix-core cycles, which at B(20,4) F = 128 turns dgrad_kernel's 0.23 ms of fp32 MFMA time into a
+// memory-bound kernel. A = dpre (split once per k-tile while staging, as bf16 images), B = the packed weights
+// transposed and split once per backward (transpose_split3_kernel: BT3 [3][N][F_out] bf16). LDS per buffer: three
+// A and three B images of BM / BN rows x 32 k (rows padded to 40 bf16 = 80 B: conflict-free ds_read_b128).
+// Built without SLP vectorisation (see dgrad_bf16_kernel).
+constexpr int XBK = 32;
+constexpr int XLDK = 40;
+
+__device__ __forceinline__ f32x16 mfma32_bf(uint4 a, uint4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(pgx3::bf16x8_t, a),
+                                                   __builtin_bit_cast(pgx3::bf16x8_t, b), c, 0, 0, 0);
+}
+
+// exact three-way split of 4 fp32 values into three bf16x4 (8-B) pieces
+__device__ __forceinline__ void split4(float4 v, uint2& s0, uint2& s1, uint2& s2) {
+    float a = v.x, b = v.y, c = v.z, d = v.w, fa, fb, fc, fd;
+    uint32_t w0 = pgx3::bf2(a, b, fa, fb), w1 = pgx3::bf2(c, d, fc, fd);
+    s0 = make_uint2(w0, w1);
+    a -= fa; b -= fb; c -= fc; d -= fd;
+    w0 = pgx3::bf2(a, b, fa, fb);
+    w1 = pgx3::bf2(c, d, fc, fd);
+    s1 = make_uint2(w0, w1);
+    a -= fa; b -= fb; c -= fc; d -= fd;
+    w0 = pgx3::bf2(a, b, fa, fb);
+    w1 = pgx3::bf2(c, d, fc, fd);
+    s2 = make_uint2(w0, w1);
+}
+
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(64 * NW, 3) void dgrad_x3_kernel(DgradP p, const uint16_t* BT3) {
+    constexpr int NT = 64 * NW;
+    constexpr int WN = 2;
+    constexpr int WM = NW / WN;
+    constexpr int TM = BM / WM / 32;
+    constexpr int TN = BN / WN / 32;
+    static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+    constexpr int A_F4 = BM * XBK / 4 / NT;  // fp32 float4 pieces of dY (and Y) per thread per k-tile
+    constexpr int B_C = BN * XBK / 8 / NT;   // bf16x8 pieces of each B split per thread per k-tile
+    static_assert(A_F4 >= 1 && B_C >= 1, "tile shape");
+    constexpr int TLD = BN + 4;
+    constexpr int IMG = XLDK;                              // u16 per image row
+    constexpr int MAIN_U16 = 3 * (BM + BN) * IMG;          // one buffer of three A and three B images
+    constexpr int SMEM_BYTES = MAIN_U16 * 2 > BM * TLD * 4 ? MAIN_U16 * 2 : BM * TLD * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ float Bd[BM * 3];
+    uint16_t* const img = reinterpret_cast<uint16_t*>(smem);
+    auto Aimg = [&](int buf, int sp) { return img + (buf * 3 + sp) * BM * IMG; };  // buf = 0: one LDS buffer
+    auto Bimg = [&](int buf, int sp) { return img + 3 * BM * IMG + (buf * 3 + sp) * BN * IMG; };
+
+    const int ntn = (p.N + BN - 1) / BN;
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int nt = (int)(lb % ntn);
+    const int64_t m0 = (lb / ntn) * BM;
+    const int n0 = nt * BN;
+    const bool lead = nt == 0;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+
+    if (tid < BM) {
+        const int64_t m = m0 + tid;
+        float4 sv = make_float4(0.f, 0.f, 0.f, 1.f);
+        if (m < p.M) {
+            float ci, co, cd, cu, ca;
+            gate_values(p.g, m, ci, co, cd, cu, ca);
+            const float cad = ca * cd;
+            sv.x = cad * ci;
+            sv.y = cad * co;
+            sv.z = ca * cu;
+            if (lead) st4(p.gates + m * 4, sv);
+        }
+        st4(&Sg[tid * 4], sv);
+    }
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    float4 ra[A_F4], ry[A_F4];
+    uint4 rb[B_C][3];
+    float bd[A_F4][3];
+#pragma unroll
+    for (int q = 0; q < A_F4; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
+    const int64_t mlast = p.M - 1;
+    const int64_t bsplit = (int64_t)p.N * p.F_out;  // elements per BT3 split
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int64_t m = min(m0 + (idx >> 3), mlast);
+            const int k = k0 + 4 * (idx & 7);
+            const int kc = k < p.F_out ? k : 0;
+            ra[q] = ld4(p.dY + m * p.lddy + kc);
+            if (p.act) ry[q] = ld4(p.Y + m * p.ldy + kc);
+        }
+#pragma unroll
+        for (int q = 0; q < B_C; ++q) {
+            const int idx = tid + NT * q;
+            const int n = min(n0 + (idx >> 2), p.N - 1);
+            const int k = k0 + 8 * (idx & 3);
+            const int64_t o = (int64_t)n * p.F_out + (k < p.F_out ? k : 0);
+#pragma unroll
+            for (int sp = 0; sp < 3; ++sp) rb[q][sp] = *reinterpret_cast<const uint4*>(BT3 + sp * bsplit + o);
+        }
+    };
+    auto stash = [&](int buf, int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 4 * (idx & 7);
+            const int64_t m = m0 + (idx >> 3);
+            float4 d = ra[q];
+            if (p.act) {
+                const float4 y = ry[q];
+                d.x = y.x > 0.f ? d.x : d.x * p.slope;
+                d.y = y.y > 0.f ? d.y : d.y * p.slope;
+                d.z = y.z > 0.f ? d.z : d.z * p.slope;
+                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+            }
+            if (k >= p.F_out) d = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lead && k < p.F_out && m < p.M) {
+                st4(p.dpre + m * p.ldp + k, d);
+#pragma unroll
+                for (int sg = 0; sg < 3; ++sg) bd[q][sg] += dot4(d, ld4(p.bsum + sg * p.F_out + k));
+            }
+            uint2 s0, s1, s2;
+            split4(d, s0, s1, s2);
+            const int o = (idx >> 3) * IMG + 4 * (idx & 7);
+            *reinterpret_cast<uint2*>(Aimg(buf, 0) + o) = s0;
+            *reinterpret_cast<uint2*>(Aimg(buf, 1) + o) = s1;
+            *reinterpret_cast<uint2*>(Aimg(buf, 2) + o) = s2;
+        }
+#pragma unroll
+        for (int q = 0; q < B_C; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 8 * (idx & 3);
+            const int o = (idx >> 2) * IMG + 8 * (idx & 3);
+#pragma unroll
+            for (int sp = 0; sp < 3; ++sp)
+                *reinterpret_cast<uint4*>(Bimg(buf, sp) + o) = k < p.F_out ? rb[q][sp] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+
+    // one LDS buffer (so that three workgroups fit a CU and one's epilogue overlaps another's k-loop): the next
+    // k-tile's operands wait in registers during this tile's MFMAs, then are split into the buffer between two
+    // barriers
+    const int ntiles = (p.F_out + XBK - 1) / XBK;
+    fetch(0);
+    stash(0, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = 0;
+        if (t + 1 < ntiles) fetch((t + 1) * XBK);
+#pragma unroll
+        for (int kk = 0; kk < XBK / 16; ++kk) {
+            uint4 a[TM][3], b[TN][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int sp = 0; sp < 3; ++sp)
+                    a[i][sp] = *reinterpret_cast<const uint4*>(Aimg(cur, sp) + (wm * TM * 32 + i * 32 + li) * IMG +
+                                                               kk * 16 + 8 * lh);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int sp = 0; sp < 3; ++sp)
+                    b[j][sp] = *reinterpret_cast<const uint4*>(Bimg(cur, sp) + (wn * TN * 32 + j * 32 + li) * IMG +
+                                                               kk * 16 + 8 * lh);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {  // small terms first (the order of every split-bf16 kernel here)
+                    acc[i][j] = mfma32_bf(a[i][2], b[j][0], acc[i][j]);
+                    acc[i][j] = mfma32_bf(a[i][1], b[j][1], acc[i][j]);
+                    acc[i][j] = mfma32_bf(a[i][0], b[j][2], acc[i][j]);
+                    acc[i][j] = mfma32_bf(a[i][1], b[j][0], acc[i][j]);
+                    acc[i][j] = mfma32_bf(a[i][0], b[j][1], acc[i][j]);
+                    acc[i][j] = mfma32_bf(a[i][0], b[j][0], acc[i][j]);
+                }
+        }
+        if (t + 1 < ntiles) {
+            __syncthreads();
+            stash(0, (t + 1) * XBK);
+        }
+        __syncthreads();
+    }
+
+    // bias dots <dpre[m], bsum_q>: 8 consecutive lanes hold one row's K slices
+    if (lead) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+#pragma unroll
+            for (int sg = 0; sg < 3; ++sg) {
+                float v = bd[q][sg];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                bd[q][sg] = v;
+            }
+            const int idx = tid + NT * q;
+            if ((idx & 7) == 0) {
+                Bd[(idx >> 3) * 3 + 0] = bd[q][0];
+                Bd[(idx >> 3) * 3 + 1] = bd[q][1];
+                Bd[(idx >> 3) * 3 + 2] = bd[q][2];
+            }
+        }
+    }
+
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                T[rl * TLD + wn * TN * 32 + j * 32 + li] = acc[i][j][r];
+            }
+    __syncthreads();
+
+    constexpr int C4 = BN / 4;
+    constexpr int ITER = BM * C4 / NT;
+    constexpr int BATCH = ITER < 4 ? ITER : 4;
+    const int c4 = tid % C4;
+    const int j = n0 + 4 * c4;
+    const int seg = j < p.N ? j / p.F_in : 4;  // F_in % 4 == 0: a float4 never straddles segments
+    for (int it0 = 0; it0 < ITER; it0 += BATCH) {
+        float4 zv[BATCH];
+        int rl[BATCH];
+        int64_t mm[BATCH];
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            rl[u] = (tid + NT * (it0 + u)) / C4;
+            mm[u] = m0 + rl[u];
+            zv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (mm[u] < p.M && seg < 3) zv[u] = ld4(p.Z + mm[u] * p.ldz + j);
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            float part = 0.f;
+            if (mm[u] < p.M && seg < 4) {
+                const float4 gv = ld4(&T[rl[u] * TLD + 4 * c4]);
+                if (seg < 3) {
+                    const float sc = Sg[rl[u] * 4 + seg];
+                    if (p.dZ) st4(p.dZ + mm[u] * p.lddz + j, make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
+                    part = dot4(gv, zv[u]);
+                } else {
+                    st4(p.dres + mm[u] * p.lddres + (j - 3 * p.F_in), gv);
+                }
+            }
+            T[rl[u] * TLD + 4 * c4] = part;  // own slot, already consumed
+        }
+    }
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+        const int64_t m = m0 + tid;
+        float ds[3] = {0.f, 0.f, 0.f};
+        if (lead) {
+            ds[0] = Bd[tid * 3 + 0];
+            ds[1] = Bd[tid * 3 + 1];
+            ds[2] = Bd[tid * 3 + 2];
+        }
+        for (int c = 0; c < C4; ++c) {
+            const int jj = n0 + 4 * c;
+            if (jj >= p.N) break;
+            const int q = jj / p.F_in;
+            if (q < 3) ds[q] += T[tid * TLD + 4 * c];
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
+    }
+}
+
 // ds_q[m] = sum over n-tiles (fixed order) -> dL/dc_* per row (chain rule of s_q(c), :116-133)
 __global__ __launch_bounds__(256) void gate_grad_kernel(int64_t M, int ntn, const float* dsp, Gates g, float* dgate) {
     for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
@@ -322,6 +607,23 @@ __global__ __launch_bounds__(256) void gate_grad_kernel(int64_t M, int ntn, cons
         dgate[2 * M + m] = ca * (d0 * ci + d1 * co);        // c_directed
         dgate[3 * M + m] = d2 * ca;                        // c_undirected
         dgate[4 * M + m] = cd * (d0 * ci + d1 * co) + d2 * cu;  // c_all
+    }
+}
+
+// BT3[sp][c][r] = split sp of in[r][c] (the exact three-way bf16 split of pg_split3.h); R x C, once per backward
+__global__ __launch_bounds__(256) void transpose_split3_kernel(int R, int C, const float* in, uint16_t* out) {
+    const int64_t total = (int64_t)R * C;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int c = (int)(i / R), r = (int)(i % R);
+        float v = in[(int64_t)r * C + c], fa, fb;
+        const uint32_t w0 = pgx3::bf2(v, 0.f, fa, fb);
+        v -= fa;
+        const uint32_t w1 = pgx3::bf2(v, 0.f, fa, fb);
+        v -= fa;
+        const uint32_t w2 = pgx3::bf2(v, 0.f, fa, fb);
+        out[i] = (uint16_t)(w0 & 0xffffu);
+        out[total + i] = (uint16_t)(w1 & 0xffffu);
+        out[2 * total + i] = (uint16_t)(w2 & 0xffffu);
     }
 }
 
@@ -1101,6 +1403,7 @@ __global__ __launch_bounds__(256) void transpose_u16_kernel(int R, int C, const 
 }
 
 constexpr int DG_BM = 128, DG_BN = 128, DG_NW = 8, WG_NW = 8;
+constexpr int X3_BM = 64, X3_NW = 4;  // dgrad_x3_kernel: 64-row blocks of 4 waves, three workgroups per CU
 
 struct BwdPlan {
     int K, ntn, splits;
@@ -1246,8 +1549,8 @@ BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
     b.splits = sp.splits;
     b.rows_per_split = sp.rows_per_split;
     b.part_stride = up4(F_out * b.K + 4 * F_out);
-    b.off_bt = 0;
-    b.off_dsp = up4((int64_t)b.K * F_out);
+    b.off_bt = 0;  // BT (fp32), or BT3 (three bf16 splits, dgrad_x3_kernel), or the bf16 BT
+    b.off_dsp = up4(2 * (int64_t)b.K * F_out);
     b.off_part = b.off_dsp + up4((int64_t)b.ntn * 3 * M);
     b.total = b.off_part + (int64_t)b.splits * b.part_stride;
     return b;
@@ -1301,10 +1604,14 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
             return pg::set_error(PG_ERR_HIP, "pg_directgcn_dense_bwd_f32: memset failed");
         return PG_OK;
     }
+    // the split-bf16 dgrad where the k-tiles are whole (F_out % 32 == 0); PG_FLAG_DGRAD_F32MFMA keeps the fp32 MFMAs
+    const bool x3 = vec && a->F_out % XBK == 0 && !(flags & PG_FLAG_DGRAD_F32MFMA);
+    uint16_t* BT3 = reinterpret_cast<uint16_t*>(BT);
     {
         const int64_t total = (int64_t)K * F_out;
         const int nb = (int)std::min<int64_t>((total + 255) / 256, 1024);
-        hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed, BT);
+        if (x3) hipLaunchKernelGGL(transpose_split3_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed, BT3);
+        else hipLaunchKernelGGL(transpose_kernel, dim3(nb), dim3(256), 0, s, F_out, K, packed, BT);
     }
     Gates gt{a->gate_mode, a->C_in, a->C_out, a->C_directed, a->C_undirected, a->C_all, a->rows};
     if (!vec) {  // any shape: per-element kernels (same outputs, sums in another order)
@@ -1386,7 +1693,10 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         p.dsp = dsp;
         p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
         const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
-        hipLaunchKernelGGL((dgrad_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
+        if (x3)
+            hipLaunchKernelGGL((dgrad_x3_kernel<X3_BM, DG_BN, X3_NW>), dim3((unsigned)(((a->M + X3_BM - 1) / X3_BM) * pl.ntn)),
+                               dim3(64 * X3_NW), 0, s, p, (const uint16_t*)BT3);
+        else hipLaunchKernelGGL((dgrad_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
     }
     {
         const int nb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);

@@ -38,6 +38,23 @@ class SoloComm:
         pass
 
 
+class RcclVolumeComm:
+    """Real RCCL collectives at world size 1 moving the P-rank exchange's byte volume: each all_to_all sends the
+    rank's rows to itself through RCCL (min(send, receive) rows of the chunk), the all-reduce runs on RCCL. The
+    per-rank step then carries the product's TorchComm call pattern and RCCL's per-call costs (not xGMI transfer)."""
+    capturable = True
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        import torch.distributed as dist
+        k = min(out.size(0), inp.size(0))
+        if k:
+            dist.all_to_all_single(out[:k], inp[:k])
+
+    def all_reduce(self, t):
+        import torch.distributed as dist
+        dist.all_reduce(t)
+
+
 def timed(fn, reps):
     for _ in range(3):
         fn()
@@ -60,10 +77,19 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--comm", choices=("solo", "rccl"), default="solo",
+                    help="solo: no-op collectives (compute alone); rccl: RcclVolumeComm on a world-1 RCCL group")
     ap.add_argument("--link-gbs", type=float, default=50.0,
                     help="assumed usable xGMI rate per peer link (GB/s) for the projection (not measured here)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if args.comm == "rccl":
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    make_comm = SoloComm if args.comm == "solo" else RcclVolumeComm
     n, dims, lam = 4, [128, 256, 256, 256], 1e-7
     N, s, d, c = pkg.synth.de_bruijn_edges(n)
     g = pkg.build_propagation_csr(N, s, d, c, device=dev)
@@ -85,16 +111,17 @@ def main():
         m = _model(pkg, dims, N, n).to(dev).eval()
         m.compute_dtype = dt
         t0 = time.time()
-        tr = shard.MiddleTrainer(m, mp_, l2_lambda=lam, comm=SoloComm())
+        tr = shard.MiddleTrainer(m, mp_, l2_lambda=lam, comm=make_comm())
         setup = time.time() - t0
         yo = y[mp_.own]
         ms = timed(lambda: tr.step(x, yo), args.reps)
         mg = _model(pkg, dims, N, n).to(dev).eval()
         mg.compute_dtype = dt
-        trg = shard.MiddleTrainer(mg, mp_, l2_lambda=lam, comm=SoloComm(), graphs=True)
+        trg = shard.MiddleTrainer(mg, mp_, l2_lambda=lam, comm=make_comm(), graphs=True)
         for _ in range(trg.WARM + 1):  # eager warm-up steps, then the capture
             trg.step(x, yo)
         ms_graph = timed(lambda: trg.step(x, yo), args.reps)
+        trg.close()
         del trg, mg
         ghost = int(mp_.recv_ids.numel())
         sent = int(mp_.send_pos.numel())
@@ -117,9 +144,19 @@ def main():
     out["projected_p8_step_ms"] = round(worst, 4)
     out["projected_speedup"] = round(out["single_gpu_step_ms"] / worst, 2)
     out["link_assumption_gbs"] = args.link_gbs
-    out["note"] = ("per-rank compute measured with no-op collectives; exchange priced at the assumed link rate, "
-                   "all ghost rows of a rank spread over its source peers' links, not overlapped with compute")
+    out["comm"] = args.comm
+    out["note"] = (("per-rank compute measured with no-op collectives" if args.comm == "solo" else
+                    "per-rank step with the product's collective calls on a world-1 RCCL group (RcclVolumeComm: "
+                    "the exchange's rows sent to the rank itself, RCCL per-call costs included, no xGMI transfer)")
+                   + "; exchange priced at the assumed link rate, all ghost rows of a rank spread over its source "
+                     "peers' links, not overlapped with compute")
     print(json.dumps(out))
+    if args.comm == "rccl":
+        import gc
+        import torch.distributed as dist
+        gc.collect()
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

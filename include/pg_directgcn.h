@@ -379,6 +379,19 @@ int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* args);
 int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* args, const float* packed, const pg_layer_grad_args_t* grads,
                                uint32_t flags, void* stream);
 
+/* pg_directgcn_dense_bwd_f32 that also writes the transposed propagation's diagonal term of the layer input's
+ * gradient (the autograd of protgram_directgcn.py:101-112 for the rows' own entries; with e_res, plus the identity
+ * residual's gradient dpre, :213-215):
+ *   E[m, f] = sum_q wdiag[m, q] * dZ_q[m, f]  (+ dpre[m, f])          m < M, f < F_in, row stride lde
+ * wdiag = the diagonal entries A_q[m, m] as fp32 [M, 3] (q = in, out, und; NgramPlan.diag3()). Each workgroup's
+ * n-tile spans the three segments of 64 features, so the term comes from the accumulators (dgrad_span_kernel); the
+ * caller then accumulates the off-diagonal part into E (pg_spmm3t_ngram_mid_offdiag_f32 with accumulate = 1), which
+ * makes E the input's whole gradient. Same outputs as pg_directgcn_dense_bwd_f32 otherwise (dZ required). Needs
+ * F_in % 64 == 0, F_out % 32 == 0, no projected residual (W_res == NULL), no row map (rows == NULL), F_in == F_out
+ * when e_res, the vector path's alignment, E 16-B aligned and lde % 4 == 0 (else PG_ERR_UNSUPPORTED). */
+int pg_directgcn_dense_bwd_span_f32(const pg_layer_args_t* args, const float* packed, const pg_layer_grad_args_t* grads,
+                                    const float* wdiag, float* E, int64_t lde, int e_res, uint32_t flags, void* stream);
+
 /* ---- bf16 mode (config 5: bf16 storage, fp32 accumulation) --------------------------------------
  * Features, aggregates, layer outputs and their gradients are bf16 (uint16_t bit patterns); every sum is
  * fp32, rounded once to bf16 (round-to-nearest-even, as torch) when stored. Parameters stay fp32. */

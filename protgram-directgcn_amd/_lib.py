@@ -120,6 +120,8 @@ SIGNATURES = {
     "pg_directgcn_dense_bwd_workspace": (c_i64, [ctypes.POINTER(LayerArgs)]),
     "pg_directgcn_dense_bwd_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
                                                   c_u32, c_vp]),
+    "pg_directgcn_dense_bwd_span_f32": (ctypes.c_int, [ctypes.POINTER(LayerArgs), c_vp, ctypes.POINTER(LayerGradArgs),
+                                                       c_vp, c_vp, c_i64, c_i32, c_u32, c_vp]),
     "pg_f32_to_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     "pg_spmm3_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_bf16": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_u32, c_vp]),

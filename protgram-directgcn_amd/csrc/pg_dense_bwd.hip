@@ -590,6 +590,252 @@ __global__ __launch_bounds__(64 * NW, 3) void dgrad_x3_kernel(DgradP p, const ui
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// dgrad_span_kernel (round 5): dgrad_x3_kernel's arithmetic with each workgroup's n-tile spanning ALL THREE segments
+// of a 64-feature block (columns (q, f) for q = in, out, und and f in [64 nt, 64 nt + 64)), so a lane holds
+// G_in, G_out, G_und of the same (row, feature) in its accumulators (TN = 3, one per segment). That makes the
+// transposed propagation's diagonal term free ("Transposed middle-tile kernel"):
+//   E[m, f] = sum_q Wdiag_q[m] dZ_q[m, f]  (+ dpre[m, f] for the model's identity residual)
+// is written next to dZ, and the off-diagonal transposed kernel (pg_spmm3t_ngram_mid_offdiag_f32) accumulates into E,
+// which then is the layer input's whole gradient. The epilogue runs from the accumulators (no tile in LDS): dZ / E
+// stores and Z loads are 128-B row pieces of 32 lanes; the gate partials <G_q, Z_q> go through LDS, summed per row in
+// feature order. Two workgroups of four waves per CU; wave (wm, wn): rows 32 wm.., features 64 nt + 32 wn + lane%32.
+struct SpanP {
+    const float* wdiag;  // [M or rows, 3]: Wdiag_in, _out, _und per row (NgramPlan.diag3())
+    float* E;
+    int64_t lde;
+    int e_res;           // add dpre (identity residual)
+};
+
+template <int BM, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const uint16_t* BT3, SpanP sp) {
+    constexpr int NT = 64 * NW;
+    constexpr int WN = 2, WM = NW / WN;
+    static_assert(BM == 32 * WM, "one 32-row MFMA tile per wave");
+    constexpr int FB = 64;                 // features per workgroup
+    constexpr int BNC = 3 * FB;            // B columns per workgroup (three segments)
+    constexpr int A_F4 = BM * XBK / 4 / NT;
+    constexpr int B_C = BNC * XBK / 8 / NT;
+    static_assert(A_F4 >= 1 && B_C >= 1 && BNC * XBK % (8 * NT) == 0, "tile shape");
+    constexpr int IMG = XLDK;
+    constexpr int MAIN_U16 = 3 * (BM + BNC) * IMG;
+    constexpr int PBYTES = BM * 3 * FB * 4;  // <G_q, Z_q> products per (row, q, feature)
+    constexpr int SMEM_BYTES = MAIN_U16 * 2 > PBYTES ? MAIN_U16 * 2 : PBYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ float Wd[BM * 3];
+    __shared__ float Bd[BM * 3];
+    uint16_t* const img = reinterpret_cast<uint16_t*>(smem);
+    auto Aimg = [&](int spl) { return img + spl * BM * IMG; };
+    auto Bimg = [&](int spl) { return img + 3 * BM * IMG + spl * BNC * IMG; };
+
+    const int ntn = p.F_in / FB;
+    const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
+    const int nt = (int)(lb % ntn);
+    const int64_t m0 = (lb / ntn) * BM;
+    const bool lead = nt == 0;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+    const int f = nt * FB + wn * 32 + li;  // this lane's feature (epilogue)
+
+    if (tid < BM) {
+        const int64_t m = m0 + tid;
+        float4 sv = make_float4(0.f, 0.f, 0.f, 1.f);
+        float w0 = 0.f, w1 = 0.f, w2 = 0.f;
+        if (m < p.M) {
+            float ci, co, cd, cu, ca;
+            gate_values(p.g, m, ci, co, cd, cu, ca);
+            const float cad = ca * cd;
+            sv.x = cad * ci;
+            sv.y = cad * co;
+            sv.z = ca * cu;
+            if (lead) st4(p.gates + m * 4, sv);
+            w0 = sp.wdiag[m * 3 + 0];
+            w1 = sp.wdiag[m * 3 + 1];
+            w2 = sp.wdiag[m * 3 + 2];
+        }
+        st4(&Sg[tid * 4], sv);
+        Wd[tid * 3 + 0] = w0;
+        Wd[tid * 3 + 1] = w1;
+        Wd[tid * 3 + 2] = w2;
+    }
+
+    f32x16 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    float4 ra[A_F4], ry[A_F4];
+    float bd[A_F4][3];
+#pragma unroll
+    for (int q = 0; q < A_F4; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
+    float dres[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dres[r] = 0.f;
+    const int64_t mlast = p.M - 1;
+    const int64_t bsplit = (int64_t)p.N * p.F_out;
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int64_t m = min(m0 + (idx >> 3), mlast);
+            const int k = k0 + 4 * (idx & 7);
+            ra[q] = ld4(p.dY + m * p.lddy + k);
+            if (p.act) ry[q] = ld4(p.Y + m * p.ldy + k);
+        }
+    };
+    auto stash = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+            const int idx = tid + NT * q;
+            const int k = k0 + 4 * (idx & 7);
+            const int64_t m = m0 + (idx >> 3);
+            float4 d = ra[q];
+            if (p.act) {
+                const float4 y = ry[q];
+                d.x = y.x > 0.f ? d.x : d.x * p.slope;
+                d.y = y.y > 0.f ? d.y : d.y * p.slope;
+                d.z = y.z > 0.f ? d.z : d.z * p.slope;
+                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+            }
+            if (lead && m < p.M) {
+                st4(p.dpre + m * p.ldp + k, d);
+#pragma unroll
+                for (int sg = 0; sg < 3; ++sg) bd[q][sg] += dot4(d, ld4(p.bsum + sg * p.F_out + k));
+            }
+            uint2 s0, s1, s2;
+            split4(d, s0, s1, s2);
+            const int o = (idx >> 3) * IMG + 4 * (idx & 7);
+            *reinterpret_cast<uint2*>(Aimg(0) + o) = s0;
+            *reinterpret_cast<uint2*>(Aimg(1) + o) = s1;
+            *reinterpret_cast<uint2*>(Aimg(2) + o) = s2;
+        }
+        // B (the split packed weights, 295 KB at F = 128: L2-resident) straight from global memory into the images:
+        // no registers held across the MFMAs
+#pragma unroll
+        for (int q = 0; q < B_C; ++q) {
+            const int idx = tid + NT * q;
+            const int c = idx >> 2;  // workgroup column: (wn_c, segment, lane)
+            const int n = (c % 96) / 32 * p.F_in + nt * FB + (c / 96) * 32 + (c % 32);
+            const int64_t gsrc = (int64_t)n * p.F_out + k0 + 8 * (idx & 3);
+            const int o = c * IMG + 8 * (idx & 3);
+            uint4 v[3];
+#pragma unroll
+            for (int spl = 0; spl < 3; ++spl) v[spl] = *reinterpret_cast<const uint4*>(BT3 + spl * bsplit + gsrc);
+#pragma unroll
+            for (int spl = 0; spl < 3; ++spl) *reinterpret_cast<uint4*>(Bimg(spl) + o) = v[spl];
+        }
+    };
+
+    const int ntiles = p.F_out / XBK;
+    const int t_res = (nt * FB + wn * 32) / XBK;  // the k-tile whose A image holds dpre of this lane's feature
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) fetch((t + 1) * XBK);
+#pragma unroll
+        for (int kk = 0; kk < XBK / 16; ++kk) {
+            uint4 a[3], b[3][3];
+#pragma unroll
+            for (int spl = 0; spl < 3; ++spl)
+                a[spl] = *reinterpret_cast<const uint4*>(Aimg(spl) + (wm * 32 + li) * IMG + kk * 16 + 8 * lh);
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int spl = 0; spl < 3; ++spl)
+                    b[j][spl] = *reinterpret_cast<const uint4*>(Bimg(spl) + (wn * 96 + j * 32 + li) * IMG + kk * 16 +
+                                                                8 * lh);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                acc[j] = mfma32_bf(a[2], b[j][0], acc[j]);
+                acc[j] = mfma32_bf(a[1], b[j][1], acc[j]);
+                acc[j] = mfma32_bf(a[0], b[j][2], acc[j]);
+                acc[j] = mfma32_bf(a[1], b[j][0], acc[j]);
+                acc[j] = mfma32_bf(a[0], b[j][1], acc[j]);
+                acc[j] = mfma32_bf(a[0], b[j][0], acc[j]);
+            }
+        }
+        if (sp.e_res && t == t_res) {  // dpre of this lane's 16 rows at its feature: the exact sum of the three splits
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const int o = rl * IMG + (f - t * XBK);
+                dres[r] = __uint_as_float((uint32_t)Aimg(0)[o] << 16) + __uint_as_float((uint32_t)Aimg(1)[o] << 16) +
+                          __uint_as_float((uint32_t)Aimg(2)[o] << 16);
+            }
+        }
+        if (t + 1 < ntiles) {
+            __syncthreads();
+            stash((t + 1) * XBK);
+        }
+        __syncthreads();
+    }
+
+    if (lead) {
+#pragma unroll
+        for (int q = 0; q < A_F4; ++q) {
+#pragma unroll
+            for (int sg = 0; sg < 3; ++sg) {
+                float v = bd[q][sg];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                bd[q][sg] = v;
+            }
+            const int idx = tid + NT * q;
+            if ((idx & 7) == 0) {
+                Bd[(idx >> 3) * 3 + 0] = bd[q][0];
+                Bd[(idx >> 3) * 3 + 1] = bd[q][1];
+                Bd[(idx >> 3) * 3 + 2] = bd[q][2];
+            }
+        }
+    }
+
+    // epilogue from the accumulators: dZ_q = s_q G_q, E = sum_q Wdiag_q dZ_q (+ dpre), products G_q Z_q into LDS
+    float* P = reinterpret_cast<float*>(smem);  // [BM][3][FB]; the k-loop ended with a barrier
+#pragma unroll
+    for (int r0 = 0; r0 < 16; r0 += 4) {
+        float zq[4][3];
+#pragma unroll
+        for (int r = r0; r < r0 + 4; ++r) {
+            const int64_t m = min(m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, mlast);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) zq[r - r0][j] = p.Z[m * p.ldz + j * p.F_in + f];
+        }
+#pragma unroll
+        for (int r = r0; r < r0 + 4; ++r) {
+            const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const int64_t m = m0 + rl;
+            float e = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float gv = acc[j][r];
+                const float dz = Sg[rl * 4 + j] * gv;
+                if (m < p.M && p.dZ) p.dZ[m * p.lddz + j * p.F_in + f] = dz;
+                e = __fmaf_rn(Wd[rl * 3 + j], dz, e);
+                P[(rl * 3 + j) * FB + wn * 32 + li] = gv * zq[r - r0][j];
+            }
+            if (m < p.M) sp.E[m * sp.lde + f] = sp.e_res ? e + dres[r] : e;
+        }
+    }
+    __syncthreads();
+    // gate partials: thread (row tid / 4, q = tid % 4 < 3) sums its row's 64 products of segment q in feature order
+    if (tid < 4 * BM) {
+        const int rl = tid >> 2, q = tid & 3;
+        const int64_t m = m0 + rl;
+        if (q < 3 && m < p.M) {
+            float ds = lead ? Bd[rl * 3 + q] : 0.f;
+            const float* row = P + (rl * 3 + q) * FB;
+            for (int c = 0; c < FB; ++c) ds += row[c];
+            p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds;
+        }
+    }
+}
+
 // ds_q[m] = sum over n-tiles (fixed order) -> dL/dc_* per row (chain rule of s_q(c), :116-133)
 __global__ __launch_bounds__(256) void gate_grad_kernel(int64_t M, int ntn, const float* dsp, Gates g, float* dgate) {
     for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
@@ -1565,8 +1811,13 @@ int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* a) {
     return plan_of(a->M, a->F_in, a->F_out, a->W_res != nullptr).total;
 }
 
-int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, const pg_layer_grad_args_t* g,
-                               uint32_t flags, void* stream) {
+}  // extern "C"
+
+namespace {
+// the fp32 backward; span != nullptr: pg_directgcn_dense_bwd_span_f32 (dgrad_span_kernel, E = diagonal term of the
+// transposed propagation (+ residual), PG_ERR_UNSUPPORTED unless its shape conditions hold)
+int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_layer_grad_args_t* g, uint32_t flags,
+                       void* stream, const SpanP* span) {
     PG_REQUIRE(a != nullptr && packed != nullptr && g != nullptr, "null args");
     PG_REQUIRE(a->M >= 0 && a->F_in > 0 && a->F_out > 0 && a->F_in < (1 << 20) && a->F_out < (1 << 20),
                "bad shape M=%lld F_in=%lld F_out=%lld", (long long)a->M, (long long)a->F_in, (long long)a->F_out);
@@ -1605,7 +1856,15 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         return PG_OK;
     }
     // the split-bf16 dgrad where the k-tiles are whole (F_out % 32 == 0); PG_FLAG_DGRAD_F32MFMA keeps the fp32 MFMAs
-    const bool x3 = vec && a->F_out % XBK == 0 && !(flags & PG_FLAG_DGRAD_F32MFMA);
+    const bool x3 = vec && a->F_out % XBK == 0 && (span || !(flags & PG_FLAG_DGRAD_F32MFMA));
+    if (span) {
+        const bool ok = x3 && !proj && a->F_in % 64 == 0 && a->rows == nullptr && g->dZ != nullptr &&
+                        (!span->e_res || a->F_in == a->F_out) && pg::aligned16(span->E) && span->lde % 4 == 0;
+        if (!ok)
+            return pg::set_error(PG_ERR_UNSUPPORTED, "pg_directgcn_dense_bwd_span_f32: needs F_in %% 64 == 0, "
+                                 "F_out %% 32 == 0, no projected residual, no row map, dZ, aligned buffers and "
+                                 "F_in == F_out with e_res");
+    }
     uint16_t* BT3 = reinterpret_cast<uint16_t*>(BT);
     {
         const int64_t total = (int64_t)K * F_out;
@@ -1693,14 +1952,19 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
         p.dsp = dsp;
         p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
         const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
-        if (x3)
+        if (span)
+            hipLaunchKernelGGL((dgrad_span_kernel<X3_BM, X3_NW>),
+                               dim3((unsigned)(((a->M + X3_BM - 1) / X3_BM) * (a->F_in / 64))), dim3(64 * X3_NW), 0, s,
+                               p, (const uint16_t*)BT3, *span);
+        else if (x3)
             hipLaunchKernelGGL((dgrad_x3_kernel<X3_BM, DG_BN, X3_NW>), dim3((unsigned)(((a->M + X3_BM - 1) / X3_BM) * pl.ntn)),
                                dim3(64 * X3_NW), 0, s, p, (const uint16_t*)BT3);
         else hipLaunchKernelGGL((dgrad_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
     }
     {
         const int nb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);
-        hipLaunchKernelGGL(gate_grad_kernel, dim3(nb), dim3(256), 0, s, a->M, pl.ntn, (const float*)dsp, gt, g->dgate);
+        hipLaunchKernelGGL(gate_grad_kernel, dim3(nb), dim3(256), 0, s, a->M, span ? (int)(a->F_in / 64) : pl.ntn,
+                           (const float*)dsp, gt, g->dgate);
     }
     {
         WgradP w{};
@@ -1729,7 +1993,24 @@ int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, co
     }
     // F_out % 4 == 0, so part_stride == F_out*K + 4*F_out == the dW buffer
     launch_reduce(pl.part_stride / 4, pl.splits, pl.part_stride, part, g->dW, s);
-    return pg::check_launch("pg_directgcn_dense_bwd_f32");
+    return pg::check_launch(span ? "pg_directgcn_dense_bwd_span_f32" : "pg_directgcn_dense_bwd_f32");
+}
+}  // namespace
+
+extern "C" {
+
+int pg_directgcn_dense_bwd_f32(const pg_layer_args_t* a, const float* packed, const pg_layer_grad_args_t* g,
+                               uint32_t flags, void* stream) {
+    return dense_bwd_f32_impl(a, packed, g, flags, stream, nullptr);
+}
+
+int pg_directgcn_dense_bwd_span_f32(const pg_layer_args_t* a, const float* packed, const pg_layer_grad_args_t* g,
+                                    const float* wdiag, float* E, int64_t lde, int e_res, uint32_t flags,
+                                    void* stream) {
+    PG_REQUIRE(wdiag != nullptr && E != nullptr && a != nullptr && g != nullptr, "null args");
+    PG_REQUIRE(lde >= a->F_in, "lde too small");
+    const SpanP sp{wdiag, E, lde, e_res ? 1 : 0};
+    return dense_bwd_f32_impl(a, packed, g, flags, stream, &sp);
 }
 
 int64_t pg_gemm_at_b_workspace(int64_t M, int64_t P, int64_t N) {

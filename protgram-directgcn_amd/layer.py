@@ -159,6 +159,12 @@ class DirectGCNLayer(nn.Module):
             if Z is not None:
                 return ops.layer_dense(Z, prm, gate_mode, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
                                        act=act, pregated=True)
+        if (ops.SPAN_BACKWARD and torch.is_grad_enabled() and x.requires_grad
+                and ops.PropagateDense.supports(graph, x, self.out_channels, res_x, W_res, rows, fused_norm)):
+            # training through a layer whose input needs its gradient: the input's whole gradient (diagonal term and
+            # identity residual from the dense backward, off-diagonal part accumulated into it) in two launches
+            return ops.PropagateDense.apply(x, graph, res_x is not None, constant, gate_mode, act, ops.LEAKY_SLOPE,
+                                            *params)
         Z = ops.Propagate3.apply(x, graph, fused_norm)
         return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, gate_mode, act, ops.LEAKY_SLOPE,
                                     *params)

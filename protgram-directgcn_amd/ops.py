@@ -21,6 +21,9 @@ from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
 
+# training on complete n-gram graphs: PropagateDense (the span dense backward + the off-diagonal transposed kernel)
+# for layers whose input needs its gradient; False: Propagate3 + LayerDense (the 4x4-block transposed kernel)
+SPAN_BACKWARD = True
 BF16_BACKWARD = True  # bf16 mode trains through pg_directgcn_dense_bwd_bf16 / pg_spmm3t_bf16
 # Inference (no autograd) forwards gate the aggregates in the propagation's store (pg_spmm3_gated_f32) and run the
 # dense kernel on the pre-gated operand; False = the training-path kernels in inference too.
@@ -768,14 +771,15 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
 
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
                          act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                         need_dZ: bool = True, packs: Optional[list] = None):
+                         need_dZ: bool = True, packs: Optional[list] = None, span: Optional[tuple] = None):
     """pg_directgcn_dense_bwd_f32 (any shape; bf16 operands: pg_directgcn_dense_bwd_bf16, None when F_in / F_out
     are not multiples of 8 -- the caller then runs the fp32 kernels on widened copies). Returns a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
       dgate [5, M] (per-row grads of c_in, c_out, c_directed, c_undirected, c_all),
       dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out].
     packs: the bf16 forward's packed weights of the same parameters (LayerDense: saved by its forward), else packed
-    here."""
+    here. span = (wdiag [M, 3], e_res): pg_directgcn_dense_bwd_span_f32 (fp32 only), which also returns
+    E [M, F_in] = sum_q wdiag[:, q] dZ_q (+ dpre when e_res); None when it does not take the shape."""
     lib = load_library()
     _require_gpu(dY, Z, Y)
     M, F_in = Z.size(0), Z.size(1) // 3
@@ -813,15 +817,27 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     g.dgate, g.gates, g.dW = _p(dgate), _p(gates), _p(dW)
     g.work, g.work_floats = _p(work), work.numel()
     fl = default_flags() if flags is None else flags
-    if bf:
+    E = None
+    if span is not None:
+        if bf or dZ is None:
+            return None
+        wdiag, e_res = span
+        wdiag = _f32c(wdiag)
+        E = torch.empty(M, F_in, device=dev, dtype=torch.float32)
+        rc = lib.pg_directgcn_dense_bwd_span_f32(ctypes.byref(a), _p(packed), ctypes.byref(g), _p(wdiag), _p(E),
+                                                 E.stride(0), int(bool(e_res)), fl, _stream(Z))
+        name = "pg_directgcn_dense_bwd_span_f32"
+    elif bf:
         rc = lib.pg_directgcn_dense_bwd_bf16(ctypes.byref(a), _p(packed), _p(p16), ctypes.byref(g), fl, _stream(Z))
+        name = "pg_directgcn_dense_bwd_bf16"
     else:
         rc = lib.pg_directgcn_dense_bwd_f32(ctypes.byref(a), _p(packed), ctypes.byref(g), fl, _stream(Z))
+        name = "pg_directgcn_dense_bwd_f32"
     if rc == _lib.PG_ERR_UNSUPPORTED:
         return None
-    check(rc, "pg_directgcn_dense_bwd_bf16" if bf else "pg_directgcn_dense_bwd_f32")
+    check(rc, name)
     del keep
-    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate,
+    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "E": E,
             "dB": dW[:F_out * K].view(F_out, K), "dbsum": dW[F_out * K:].view(4, F_out)}
 
 
@@ -979,57 +995,116 @@ class LayerDense(torch.autograd.Function):
             for k in ("dpre", "dZ", "dres"):
                 if out[k] is not None:
                     out[k] = out[k].to(torch.bfloat16)
-        dpre, dZ, dB, dbsum, dgate = out["dpre"], out["dZ"], out["dB"], out["dbsum"], out["dgate"]
-        M, F_in = Z.size(0), Z.size(1) // 3
-        F_out = dB.size(0)
-        # Every weight and bias gradient is handed to autograd as its own contiguous tensor, so AccumulateGrad keeps it
-        # instead of copying it: column slices of dB break the parameters' layout contract (one strided copy each), and
-        # a bias sum shared by two parameters is copied for one of them. One copy lays dB out by segment
-        # ([segments, F_out, F_in]); W_shared = (W_in' + W_out') + W_und' as before; one copy doubles the bias sums.
-        Wg = dB.view(F_out, dB.size(1) // F_in, F_in).transpose(0, 1).contiguous()
-        g = {"W_main_in": Wg[0], "W_main_out": Wg[1], "W_undirected": Wg[2]}
-        ws = Wg[0] + Wg[1]
-        ws += Wg[2]
-        g["W_shared"] = ws
-        bb = dbsum[:3].unsqueeze(0).expand(2, 3, F_out).contiguous()
-        g["b_main_in"], g["b_dir_shared_in"] = bb[0, 0], bb[1, 0]
-        g["b_main_out"], g["b_dir_shared_out"] = bb[0, 1], bb[1, 1]
-        g["b_undirected"], g["b_undirected_shared"] = bb[0, 2], bb[1, 2]
-        for q, name in enumerate(("C_in", "C_out", "C_directed", "C_undirected", "C_all")):
-            v = prm[name]
-            if not ctx.needs_input_grad[9 + _DENSE_KEYS.index(name)]:
-                continue
-            if ctx.gate_mode == 1:
-                g[name] = dgate[q].sum().reshape(v.shape)
-            elif rows is not None:
-                g[name] = torch.zeros_like(v).index_add_(0, rows, dgate[q].reshape(-1, *v.shape[1:]))
-            elif v.size(0) == M:
-                g[name] = dgate[q].reshape(v.shape)
+        grads, d_const, d_res, d_wres, d_bres = _dense_grads(out, prm, ctx.gate_mode, rows, Z, constant, res_x, W_res,
+                                                             lambda i: ctx.needs_input_grad[9 + i],
+                                                             ctx.needs_input_grad[2])
+        return (out["dZ"], d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)
+
+
+def _dense_grads(out, prm, gate_mode, rows, Z, constant, res_x, W_res, need, need_const):
+    """The parameter gradients of LayerDense / PropagateDense from the dense backward's outputs: (grads in _DENSE_KEYS
+    order, d_constant, d_res, d_W_res, d_b_res); need(i) says whether parameter i of _DENSE_KEYS needs its gradient."""
+    dpre, dB, dbsum, dgate = out["dpre"], out["dB"], out["dbsum"], out["dgate"]
+    M, F_in = Z.size(0), Z.size(1) // 3
+    F_out = dB.size(0)
+    # Every weight and bias gradient is handed to autograd as its own contiguous tensor, so AccumulateGrad keeps it
+    # instead of copying it: column slices of dB break the parameters' layout contract (one strided copy each), and
+    # a bias sum shared by two parameters is copied for one of them. One copy lays dB out by segment
+    # ([segments, F_out, F_in]); W_shared = (W_in' + W_out') + W_und' as before; one copy doubles the bias sums.
+    Wg = dB.view(F_out, dB.size(1) // F_in, F_in).transpose(0, 1).contiguous()
+    g = {"W_main_in": Wg[0], "W_main_out": Wg[1], "W_undirected": Wg[2]}
+    ws = Wg[0] + Wg[1]
+    ws += Wg[2]
+    g["W_shared"] = ws
+    bb = dbsum[:3].unsqueeze(0).expand(2, 3, F_out).contiguous()
+    g["b_main_in"], g["b_dir_shared_in"] = bb[0, 0], bb[1, 0]
+    g["b_main_out"], g["b_dir_shared_out"] = bb[0, 1], bb[1, 1]
+    g["b_undirected"], g["b_undirected_shared"] = bb[0, 2], bb[1, 2]
+    for q, name in enumerate(("C_in", "C_out", "C_directed", "C_undirected", "C_all")):
+        v = prm[name]
+        if not need(_DENSE_KEYS.index(name)):
+            continue
+        if gate_mode == 1:
+            g[name] = dgate[q].sum().reshape(v.shape)
+        elif rows is not None:
+            g[name] = torch.zeros_like(v).index_add_(0, rows, dgate[q].reshape(-1, *v.shape[1:]))
+        elif v.size(0) == M:
+            g[name] = dgate[q].reshape(v.shape)
+        else:
+            full = torch.zeros_like(v)
+            full[:M] = dgate[q].reshape(M, *v.shape[1:])
+            g[name] = full
+    d_const = None
+    if constant is not None and need_const:
+        dp = dpre.to(constant.dtype)
+        if rows is None and constant.size(0) == M:
+            d_const = dp  # every row of the constant receives exactly its dpre row (no zero-fill + add pass)
+        else:
+            d_const = torch.zeros_like(constant)
+            if rows is not None:
+                d_const.index_add_(0, rows, dp)
             else:
-                full = torch.zeros_like(v)
-                full[:M] = dgate[q].reshape(M, *v.shape[1:])
-                g[name] = full
-        d_const = None
-        if constant is not None and ctx.needs_input_grad[2]:
-            dp = dpre.to(constant.dtype)
-            if rows is None and constant.size(0) == M:
-                d_const = dp  # every row of the constant receives exactly its dpre row (no zero-fill + add pass)
-            else:
-                d_const = torch.zeros_like(constant)
-                if rows is not None:
-                    d_const.index_add_(0, rows, dp)
-                else:
-                    d_const[:M] += dp
-        d_res = d_wres = d_bres = None
-        if res_x is not None:
-            if W_res is None:
-                d_res = dpre
-            else:
-                d_res = out["dres"]
-                d_wres = Wg[3]
-                d_bres = dbsum[3]
-        grads = [g[k] if ctx.needs_input_grad[9 + i] else None for i, k in enumerate(_DENSE_KEYS)]
-        return (dZ, d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)
+                d_const[:M] += dp
+    d_res = d_wres = d_bres = None
+    if res_x is not None:
+        if W_res is None:
+            d_res = dpre
+        else:
+            d_res = out["dres"]
+            d_wres = Wg[3]
+            d_bres = dbsum[3]
+    grads = [g[k] if need(i) else None for i, k in enumerate(_DENSE_KEYS)]
+    return grads, d_const, d_res, d_wres, d_bres
+
+
+class PropagateDense(torch.autograd.Function):
+    """Propagate3 + LayerDense in one Function for a layer whose input needs its gradient, on a complete n-gram graph
+    (round 5; the autograd of protgram_directgcn.py:101-133 and the residual of :213-215). Forward: the same two
+    kernels. Backward: pg_directgcn_dense_bwd_span_f32 writes, next to dZ, E = the transposed propagation's diagonal
+    term (+ the identity residual's dpre) from its accumulators, and the off-diagonal transposed middle-tile kernel
+    (pg_spmm3t_ngram_mid_offdiag_f32, 657 MB at B(20,4) F = 128) accumulates into E: the input's whole gradient in
+    two launches, where Propagate3 + LayerDense run the 4x4-block transposed kernel (1,050 MB) and autograd adds the
+    residual's gradient in a third pass. Inputs: (x, g, res, constant, gate_mode, act, slope, *params) with
+    res = the layer's residual is x itself (identity)."""
+
+    @staticmethod
+    def forward(ctx, x, g: CSRGraph, res: bool, constant, gate_mode, act, slope, *params):
+        prm = dict(zip(_DENSE_KEYS, params))
+        Z = spmm3(g, x)
+        Y = layer_dense(Z, prm, gate_mode, constant=constant, res_x=x if res else None, act=act, slope=slope)
+        ctx.g, ctx.res, ctx.gate_mode, ctx.act, ctx.slope = g, res, gate_mode, act, slope
+        ctx.has_const = constant is not None
+        ctx.save_for_backward(Z, Y, constant if constant is not None else Z.new_empty(0), *params)
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        Z, Y, constant, *params = ctx.saved_tensors
+        prm = dict(zip(_DENSE_KEYS, params))
+        constant = constant if ctx.has_const else None
+        g = ctx.g
+        out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, act=ctx.act, slope=ctx.slope,
+                                   span=(g.ngram.diag3(), ctx.res))
+        if out is None:
+            raise RuntimeError("PropagateDense: pg_directgcn_dense_bwd_span_f32 refused a shape supports_span accepted")
+        dX = spmm3t_offdiag(g, out["dZ"], out=out["E"])
+        if dX is None:
+            raise RuntimeError("PropagateDense: the off-diagonal transposed kernel refused a shape supports_span accepted")
+        grads, d_const, _, _, _ = _dense_grads(out, prm, ctx.gate_mode, None, Z, constant, None, None,
+                                               lambda i: ctx.needs_input_grad[7 + i], ctx.needs_input_grad[3])
+        return (dX if ctx.needs_input_grad[0] else None, None, None, d_const, None, None, None, *grads)
+
+    @staticmethod
+    def supports(g: CSRGraph, x: torch.Tensor, F_out: int, res_x, W_res, rows, fused_norm: bool,
+                 flags: Optional[int] = None) -> bool:
+        """Whether a layer call takes this path: fp32, a symmetric shared-pattern graph with a middle plan (the
+        off-diagonal kernel's domain), F_in % 64 == 0, F_out % 32 == 0, an identity residual (res_x is x) or none,
+        no row map, no fused normalisation."""
+        fl = default_flags() if flags is None else flags
+        return (x.dtype == torch.float32 and x.is_cuda and not fused_norm and rows is None and W_res is None
+                and (res_x is None or res_x is x) and g.shared and g.symmetric and g.ngram is not None
+                and g.ngram.mplan is not None and g.n_rows == x.size(0) and x.size(1) % 64 == 0 and F_out % 32 == 0
+                and (res_x is None or x.size(1) == F_out) and not (fl & _lib.PG_FLAG_NO_NGRAM))
 
 
 class RowLinear(torch.autograd.Function):

@@ -305,3 +305,57 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
             l2 = l2_sqsum(params)
     total = loss.detach()
     return total + l2_lambda * l2 if l2 is not None else total
+
+
+class GraphedTrainStep:
+    """train_step(model, data, y, optimizer, l2_lambda, scaler) replayed from a HIP graph: `WARM` eager steps (the
+    caches the step builds on first use: the COO -> CSR conversion and tile plans, Adam's state and descriptor lists,
+    the allocator's pools), then the whole step -- forward, loss, backward, the L2 term and the optimizer launch -- is
+    captured once (torch.cuda.CUDAGraph) and every later call is one graph launch. At config 3 the eager step leaves
+    the GPU idle between the backward's launches (host-side autograd work); the replay does not. Dropout draws fresh
+    masks per replay (the capture registers the default generator's Philox offset). The inputs are static: `data.x`
+    and `y` are read where they were at capture (copy new values into them). Returns the loss as the graph's static
+    device scalar, overwritten by the next call. A step that cannot be captured (a host sync inside it) falls back to
+    eager steps, with a message on stderr."""
+    WARM = 3
+
+    def __init__(self, model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None,
+                 weight: float = 1.0):
+        self.args = (model, data, y, optimizer)
+        self.kw = dict(l2_lambda=l2_lambda, scaler=scaler, weight=weight)
+        self._graph, self._loss, self._keep, self._eager = None, None, None, 0
+        self.failed = None
+
+    def __call__(self) -> torch.Tensor:
+        if self._graph is not None:
+            self._graph.replay()
+            return self._loss
+        if self.failed is not None or self._eager < self.WARM:
+            self._eager += 1
+            return train_step(*self.args, **self.kw)
+        return self._capture()
+
+    def _capture(self) -> torch.Tensor:
+        import sys
+        opt = self.args[3]
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                loss = train_step(*self.args, **self.kw)
+        except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
+            self.failed = repr(e)[:300]
+            print(f"[GraphedTrainStep] HIP graph capture failed ({self.failed}); running eager steps", file=sys.stderr)
+            torch.cuda.synchronize()
+            return train_step(*self.args, **self.kw)
+        # the descriptor lists the captured launches read by address (and their pinned staging copies, which the
+        # captured uploads re-read) live as long as the graph
+        self._keep = list(getattr(opt, "_tl_cache", {}).values()) + list(_LISTS.values())
+        self._graph, self._loss = g, loss
+        g.replay()  # the step the capture recorded
+        return loss
+
+    def close(self):
+        """Drop the graph (later calls capture again after WARM eager steps)."""
+        torch.cuda.synchronize()
+        self._graph, self._loss, self._keep, self._eager = None, None, None, 0

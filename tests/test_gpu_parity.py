@@ -1006,6 +1006,36 @@ def test_train_step_matches_reference_loop(pkg, cuda, amp):
 
 
 @pytest.mark.parametrize("amp", [False, True])
+def test_graphed_train_step_matches_eager(pkg, cuda, amp):
+    """train.GraphedTrainStep (the whole train_step captured as a HIP graph after its warm-up steps, then replayed):
+    eight steps from the same start give the same losses and parameters, bit for bit, as eight eager train_step calls
+    (train.Adam with the folded L2 term; dropout off, so both runs draw nothing), with and without GradScaler."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        opt = train.Adam(m.parameters(), lr=1e-3)
+        scaler = torch.amp.GradScaler("cuda", enabled=amp)
+        if graphed:
+            st = train.GraphedTrainStep(m, data, y, opt, l2_lambda=1e-3, scaler=scaler)
+            losses = [float(st()) for _ in range(8)]
+            assert st._graph is not None and st.failed is None, st.failed
+            st.close()
+        else:
+            losses = [float(train.train_step(m, data, y, opt, l2_lambda=1e-3, scaler=scaler)) for _ in range(8)]
+        runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    assert runs[0][0] == runs[1][0], runs[0][0]
+    for k, v in runs[0][1].items():
+        assert torch.equal(runs[1][1][k], v), k
+
+
+@pytest.mark.parametrize("amp", [False, True])
 def test_train_step_adam_folded_l2_matches_reference_loop(pkg, cuda, amp):
     """train.train_step with train.Adam, where the L2 gradient 2*lambda*p rides in the Adam launch as extra weight
     decay (no separate gradient pass), against the reference loop with torch.optim.Adam (L2 term in the loss,
@@ -1287,3 +1317,65 @@ def test_dense_ngram_rows_map(pkg, cuda, n, m0, nm):
     assert torch.equal(compact, ref)  # residual mapped, output compact (the last layer)
     with pytest.raises(Exception):  # a partial middle is refused on the host
         ops.layer_dense_ngram_rows(Z[:399], prm, 0, Kn1, m0, res_x=X, map_res=True, act=True)
+
+
+# ---------------------------------------------------------------------------------------------
+# PropagateDense (round 5): the span dense backward + the off-diagonal transposed kernel
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,F,res", [(3, 64, True), (3, 128, True), (3, 128, False), (4, 128, True), (3, 256, True)])
+def test_propagate_dense_span_backward(pkg, cuda, n, F, res):
+    """A layer whose input needs its gradient trains through ops.PropagateDense: the input's gradient (off-diagonal
+    transposed middle-tile kernel accumulated into E = diagonal term + identity residual) and every parameter gradient
+    against the Propagate3 + LayerDense path (4x4-block transposed kernel, autograd's residual add), and at n = 3 the
+    input gradient against float64 on the host; E itself against its definition."""
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    torch.manual_seed(3)
+    conv = pkg.DirectGCNLayer(F, F, N, True).to(cuda)
+    with torch.no_grad():
+        gen = torch.Generator().manual_seed(9)
+        for name, p in conv.named_parameters():
+            if name.startswith("C_"):
+                p.copy_((torch.rand(p.shape, generator=gen) + 0.5).to(cuda))
+            elif "bias" in name:
+                p.copy_((torch.rand(p.shape, generator=gen) * 0.2 - 0.1).to(cuda))
+    x0 = torch.randn(N, F, generator=torch.Generator().manual_seed(4)).to(cuda)
+    w = torch.randn(N, F, generator=torch.Generator().manual_seed(5)).to(cuda)
+    assert ops.PropagateDense.supports(g, x0, F, x0 if res else None, None, None, False)
+    got = {}
+    for span in (True, False):
+        ops.SPAN_BACKWARD = span
+        try:
+            x = x0.clone().requires_grad_(True)
+            for p in conv.parameters():
+                p.grad = None
+            y = conv.fused_forward(x, g, res_x=x if res else None, act=True)
+            (y * w).sum().backward()
+            got[span] = {"x": x.grad.clone(), **{k: p.grad.clone() for k, p in conv.named_parameters()}}
+            if span:
+                y_span = y.detach()
+        finally:
+            ops.SPAN_BACKWARD = True
+    for k, v in got[False].items():
+        assert_grad_close(got[True][k], v, f"span vs 4x4 path: {k}")
+    if n == 3:  # the input's gradient in float64: A^T (s * (dpre W'))-style chain through the oracle's autograd
+        p64 = {k: v.detach().double().cpu().requires_grad_(False) for k, v in conv.state_dict().items()}
+        m = og.build_matrices(N, s, d, c)
+        xr = x0.double().cpu().requires_grad_(True)
+        ei = [m[k][0] for k in ("in", "out", "und")]
+        ew = [m[k][1].double() for k in ("in", "out", "und")]
+        yr = oc.layer_forward(p64, xr, ei[0], ew[0], ei[1], ew[1], ei[2], ew[2])
+        # leaky_relu with the GPU forward's slopes: a pre-activation within rounding of 0 would otherwise take the
+        # other slope in float64 and move a whole neighbourhood of input-gradient rows (one such entry at F = 128)
+        slope = torch.where(y_span.cpu() > 0, 1.0, ops.LEAKY_SLOPE).double()
+        yr = ((yr + xr) if res else yr) * slope
+        (yr * w.double().cpu()).sum().backward()
+        assert_grad_close(got[True]["x"], xr.grad, "span input gradient vs float64")
+    # E against its definition on the same dZ / dpre
+    Z = ops.spmm3(g, x0)
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    Y = ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x0 if res else None, act=True)
+    out = ops.layer_dense_backward(w, Z, Y, prm, 0, act=True, span=(g.ngram.diag3(), res))
+    ref = (out["dZ"].view(N, 3, F) * g.ngram.diag3().unsqueeze(2)).sum(1) + (out["dpre"] if res else 0.0)
+    assert_grad_close(out["E"], ref, "E = sum_q Wdiag_q dZ_q (+ dpre)")

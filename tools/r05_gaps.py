@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-step kernel timeline of a bench run from a rocprofv3 kernel trace (csv): steps are the intervals between
-consecutive ends of the head kernel; prints, for the median step, each kernel's duration and the idle gap before it.
-  tools/r05_gaps.py <kernel_trace.csv> [steps=20]"""
+consecutive ends of a marker kernel (default the head kernel; `adam` for a training step); prints, for the median
+step, each kernel's duration and the idle gap before it.
+  tools/r05_gaps.py <kernel_trace.csv> [steps=20] [marker=head]"""
 import csv
 import statistics
 import sys
@@ -9,7 +10,8 @@ import sys
 rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
               for r in csv.DictReader(open(sys.argv[1])))
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-ends = [i for i, (s, e, k) in enumerate(rows) if "head" in k]
+MARK = sys.argv[3] if len(sys.argv) > 3 else "head"
+ends = [i for i, (s, e, k) in enumerate(rows) if MARK in k]
 steps = []
 for a, b in zip(ends[-K - 1:-1], ends[-K:]):
     seg = rows[a:b + 1]

@@ -19,6 +19,7 @@ bf16 = "--bf16" in sys.argv
 fused = "--fused" in sys.argv          # train.train_step instead of the reference loop body
 adam_fused = "--adam-fused" in sys.argv
 our_adam = "--our-adam" in sys.argv     # train.Adam (one HIP launch per step)
+graphed = "--graph" in sys.argv         # train.GraphedTrainStep (implies --fused)
 dims = [128, 128, 128]
 for a in sys.argv:
     if a.startswith("--dims="):
@@ -42,9 +43,12 @@ model.train()
 
 
 scaler = torch.amp.GradScaler("cuda", enabled=amp)
+gstep = pkg.train.GraphedTrainStep(model, data, y, opt, l2_lambda=1e-7, scaler=scaler) if graphed else None
 
 
 def step():
+    if gstep is not None:
+        return gstep()
     if fused:
         return pkg.train.train_step(model, data, y, opt, l2_lambda=1e-7, scaler=scaler)
     opt.zero_grad()
@@ -57,11 +61,11 @@ def step():
     return loss
 
 
-for _ in range(3):
+for _ in range(5 if graphed else 3):
     step()
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}, our_adam={our_adam}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}, our_adam={our_adam}, graph={graphed}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

@@ -76,7 +76,12 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
 #define PG_FLAG_DENSE_TILED (1u << 15)    /* dense forward: the tiled fp32 kernel even where the split-bf16 W-stationary
                                             kernels apply (F_out = 128, K = 384 or 256, no row map: the default) */
-#define PG_FLAG_DENSE_X3 (1u << 16)       /* dense backward: the split-bf16 weight gradient (opt-in) */
+#define PG_FLAG_DENSE_X3 (1u << 16)       /* dense forward: the split-bf16 W-stationary kernel (see pg_dense.hip); the
+                                             backward ignores it since round 5 (its split-bf16 weight gradient is the
+                                             default, PG_FLAG_WGRAD_F32MFMA opts out) */
+#define PG_FLAG_WGRAD_F32MFMA (1u << 18)  /* fp32 dense backward: the fp32-MFMA weight-gradient kernel instead of the
+                                             split-bf16 one (default where F_in % 128 == 0, F_out % 128 == 0 and no
+                                             projected residual) */
 #define PG_FLAG_DGRAD_F32MFMA (1u << 17)  /* fp32 dense backward: the fp32-MFMA input-gradient kernel instead of the
                                            * split-bf16 one (the default where F_out % 32 == 0) */
 #define PG_FLAG_NO_NGRAM (1u << 20)       /* host-side: use the CSR propagation kernels even if the graph has an n-gram plan */

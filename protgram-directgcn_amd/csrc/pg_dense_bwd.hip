@@ -1039,132 +1039,186 @@ __global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
     }
 }
 
-// Split-bf16 weight gradient for the model's shape (P = F_out = 128, N = 3 F_in = 384, no projected residual):
-// the partial C[P x N] = A^T diag(s) B of one row split on v_mfma_f32_16x16x32_bf16 with exact three-way bf16
-// splits of both operands (pg_split3.h: six products, fp32-level accuracy; 2.7x fewer matrix-core cycles than
-// wgrad_kernel's fp32 MFMA). Two 512-thread blocks per split compute the 128 x 384 partial, one column half
-// each, so A is read twice (wgrad_kernel reads it once per 128-column tile). Per 32-row step a staging thread
-// owns one 8-row x 4-column fp32 block (threads 0-127: A = dpre, columns 0..127; threads 128-319: B = s_q Z_q,
-// the half's 192 columns), loaded into registers one step ahead; it splits each column's 8 rows (one MFMA
-// k-group) into three bf16 units and stores them transposed, [column][row group], swizzled so that every
-// ds_read_b128 lane group and 8-lane write group hits distinct bank slots. Wave w then owns output rows
-// 16w..16w+15: three A-split operands, and for each of the 12 column blocks three B-split operands and six
-// MFMAs. The A threads also sum the bias gradients (s_q dpre per column, in row order) and the first half's
-// block reduces them over its 4 row groups in fixed order.
-constexpr int WX_P = 128, WX_N = 384, WX_H = WX_N / 2, WX_NC = WX_P + WX_H;
-__device__ __forceinline__ int wx_unit(int col, int g) { return 4 * col + (g ^ ((-(col >> 2)) & 3)); }
+// Split-bf16 weight gradient (round 5; the fp32 default where F_out % 128 == 0 and F_in % 128 == 0, no projected
+// residual): the partial C[P x N] = A^T diag(s) B of one row split on v_mfma_f32_32x32x16_bf16 with exact three-way
+// bf16 splits of both operands (pg_split3.h: six products, fp32-level accuracy). wgrad_kernel's v_mfma_f32_32x32x2f32
+// takes 64 cycles per 2-deep k-step, the six bf16 products 6 x 32 per 16-deep one: 2.7x fewer matrix-core cycles,
+// which moves the B(20,4) F = 128 weight gradient (15.7 GFLOP, 0.33 GB of operands) from the fp32 matrix cores'
+// bound (~0.10 ms at peak, 0.175 ms measured) to about the HBM one.
+// One 512-thread workgroup per (row split, 128 x 384 output tile), one per CU (LDS 100 KB): each 16-row step is
+// staged ONCE for the whole tile -- A = dpre (128 columns) and B = s_q Z_q (384 columns), 8 rows x 2 columns per
+// thread, loaded two steps ahead through buffer descriptors -- split into three bf16 images and stored transposed, image [split][k-group][column]
+// of 16-B units (the 8 rows of a k-group of one column: one MFMA operand of one lane), double-buffered (one barrier
+// per step). Reads are conflict-free (16 lanes of a ds_read_b128 group read 16 consecutive columns, 256 B); the
+// writes of a thread's two columns are 2-way conflicted (16 LDS-array cycles for a 13-cycle store). Wave w owns
+// output rows 64 (w & 1).. (two 32-row tiles) and columns 96 (w >> 1).. (three 32-column tiles): 6 A and 3 x 3 B
+// operand reads for 36 MFMAs per step. The A threads also sum the bias gradients (s_q dpre per column, in row order);
+// the n-tile-0 workgroups reduce them over their two k-groups.
+constexpr int WX_BP = 128, WX_BN = 384, WX_COLS = WX_BP + WX_BN, WX_K = 16;
 
-// grid (splits, 2): blockIdx.y picks the half of the 384 output columns (A is read twice, not three times)
-__global__ __launch_bounds__(512) void wgrad_x3_kernel(WgradP p) {
-    __shared__ __attribute__((aligned(16))) uint4 Us[3][WX_NC * 4];
-    __shared__ __attribute__((aligned(16))) float Db[4][4][WX_P];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 15, kk = lane >> 4;
-    const int half = blockIdx.y;
+__global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgradP p) {
+    __shared__ __attribute__((aligned(16))) uint4 U[2][3][2][WX_COLS];
+    __shared__ float Db[2][4][WX_BP];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+    const int n_tiles = p.N / WX_BN;
+    const int pt = (int)blockIdx.y / n_tiles, nt = (int)blockIdx.y % n_tiles;
     const int64_t r0 = (int64_t)blockIdx.x * p.rows_per_split;
     const int64_t rend = min(r0 + p.rows_per_split, p.M);
-    // staging roles (wave-uniform): waves 0-1 stage A (128 columns), waves 2-4 B (this half's 192 columns),
-    // waves 5-7 only run MFMAs
-    const bool isA = tid < 128, isB = tid >= 128 && tid < 320;
-    const int u = isA ? tid : tid - 128;
-    const int g = isA ? (u >> 5) : (u / 48);
-    const int j = isA ? (u & 31) : (u % 48);
-    const int col0 = (isA ? 0 : WX_P) + 4 * j;                  // staged column
-    const int gcol = isA ? 4 * j : WX_H * half + 4 * j;          // column in A or in Z
-    const int seg = isA ? 3 : gcol / p.F_in;
-    const float* src = isA ? p.A + gcol : p.Z + gcol;
+    // staging role, from the wave index in a scalar register (so the buffer descriptors below are wave-uniform):
+    // waves 0-1 stage A (k-group = wave), waves 2-4 / 5-7 B (k-group 0 / 1), 64 column pairs per wave
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool isA = wv < 2;
+    const int kg = isA ? wv : (wv - 2) / 3;
+    const int pair = (isA ? 0 : 64 * ((wv - 2) % 3)) + lane;
+    const int col0 = (isA ? 0 : WX_BP) + 2 * pair;              // staged column (image index)
+    const int gcol = isA ? WX_BP * pt + 2 * pair : WX_BN * nt + 2 * pair;
+    const int seg = isA ? 3 : gcol / p.F_in;  // 3: unscaled (A)
+    const float* src = isA ? p.A + WX_BP * pt : p.Z + WX_BN * nt;  // wave-uniform; the lane's columns: + 2 pair
     const int64_t ld = isA ? p.lda : p.ldz;
-    const bool stage = isA || isB;
-    float4 x[8];
-    float gv[8][3];  // A: (s_in, s_out, s_und) per row; B: [e][0] = the row's scale of this segment
-    auto load = [&](int64_t base) {
-        if (!stage) return;
+    // Two register slots of one step's rows each (x: the operand values, gq: the row's scale of this thread's segment),
+    // loaded two steps ahead through buffer descriptors over the split's rows: rows past the split read as 0 (the
+    // hardware's range check), so the loads and splits carry no clamps or selects. The bias sums need the three
+    // gates of every row in the A threads: the B thread at the first column of a segment writes its scales to Gs with
+    // the images, and the A threads add the step's sums after the barrier, from the split-time values they keep (va,
+    // vb). A segment's bias belongs to the n-tile holding its first column, the unscaled one (q = 3) to n-tile 0.
+    __shared__ float Gs[2][3][WX_K];
+    const int gsel = seg < 3 ? seg : 0;
+    const bool gwriter = !isA && gcol % p.F_in == 0;
+    const int64_t nr64 = rend - r0;
+    const int nrows = __builtin_amdgcn_readfirstlane(nr64 > 0 ? (int)nr64 : 0);  // scalar (descriptor word 2)
+    const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src + r0 * ld), 0, nrows * (int)ld * 4,
+                                                        0x00020000);
+    const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.gates + r0 * 4), 0, nrows * 16, 0x00020000);
+    const int ld4b = (int)ld * 4;
+    const int xoff = 8 * kg * ld4b + 8 * pair, goff = (8 * kg * 4 + gsel) * 4;
+    auto load = [&](float2 (&x)[8], float (&gq)[8], int step) {  // step < 2^31 / (16 ld) (host-checked)
+        const int sx = step * WX_K * ld4b, sg = step * WX_K * 16;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            const int64_t m = base + 8 * g + e;
-            const bool ok = m < rend;
-            const int64_t mm = ok ? m : r0;
-            x[e] = ok ? ld4(src + mm * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (isA) {
-                const float4 s = p.gates ? ld4(p.gates + mm * 4) : make_float4(1.f, 1.f, 1.f, 1.f);
-                gv[e][0] = s.x;
-                gv[e][1] = s.y;
-                gv[e][2] = s.z;
-            } else {
-                gv[e][0] = p.gates ? p.gates[mm * 4 + seg] : 1.f;
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_x, xoff + sx + e * ld4b, 0, 0);
+            x[e] = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            gq[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_g, goff + sg + e * 16, 0, 0));
+        }
+    };
+    float db[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) db[t][0] = db[t][1] = 0.f;
+    float va[8], vb[8];
+    auto split_store = [&](const float2 (&x)[8], const float (&gq)[8], int buf) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float sc = isA ? 1.f : gq[e];
+            va[e] = __fmul_rn(x[e].x, sc);
+            vb[e] = __fmul_rn(x[e].y, sc);
+        }
+        uint4 a0, a1, a2, b0, b1, b2;
+        pgx3::split8(va, a0, a1, a2);
+        pgx3::split8(vb, b0, b1, b2);
+        U[buf][0][kg][col0] = a0;
+        U[buf][1][kg][col0] = a1;
+        U[buf][2][kg][col0] = a2;
+        U[buf][0][kg][col0 + 1] = b0;
+        U[buf][1][kg][col0 + 1] = b1;
+        U[buf][2][kg][col0 + 1] = b2;
+        if (gwriter) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Gs[buf][seg][8 * kg + e] = gq[e];
+        }
+    };
+    auto bias_step = [&](int cur) {  // A threads, after the barrier: the step's rows' bias sums, in row order
+        if (!isA) return;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int row = 8 * kg + e;
+            const float sv[4] = {Gs[cur][0][row], Gs[cur][1][row], Gs[cur][2][row], 1.f};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                db[t][0] += sv[t] * va[e];
+                db[t][1] += sv[t] * vb[e];
             }
         }
     };
-    float db[4][4];
+    if (tid < 2 * 3 * WX_K) (&Gs[0][0][0])[tid] = 0.f;  // segments that start in another n-tile stay 0
+    f32x16 acc[2][3];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) db[t][0] = db[t][1] = db[t][2] = db[t][3] = 0.f;
-    auto split_store = [&]() {
-        if (!stage) return;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float v[8];
+        for (int j = 0; j < 3; ++j)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float xv = c == 0 ? x[e].x : c == 1 ? x[e].y : c == 2 ? x[e].z : x[e].w;
-                v[e] = isA ? xv : __fmul_rn(xv, gv[e][0]);
-            }
-            uint4 s0, s1, s2;
-            pgx3::split8(v, s0, s1, s2);
-            const int pos = wx_unit(col0 + c, g);
-            Us[0][pos] = s0;
-            Us[1][pos] = s1;
-            Us[2][pos] = s2;
-        }
-        if (isA) {
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int ih = wave & 1, jq = wave >> 1;
+    auto mfma_step = [&](int cur) {
+        uint4 a[2][3];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float sv[4] = {gv[e][0], gv[e][1], gv[e][2], 1.f};
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    db[t][0] += sv[t] * x[e].x;
-                    db[t][1] += sv[t] * x[e].y;
-                    db[t][2] += sv[t] * x[e].z;
-                    db[t][3] += sv[t] * x[e].w;
-                }
+            for (int sp = 0; sp < 3; ++sp) a[i][sp] = U[cur][sp][kh][64 * ih + 32 * i + li];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            uint4 b[3];
+#pragma unroll
+            for (int sp = 0; sp < 3; ++sp) b[sp] = U[cur][sp][kh][WX_BP + 96 * jq + 32 * j + li];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                acc[i][j] = mfma32_bf(a[i][2], b[0], acc[i][j]);
+                acc[i][j] = mfma32_bf(a[i][1], b[1], acc[i][j]);
+                acc[i][j] = mfma32_bf(a[i][0], b[2], acc[i][j]);
+                acc[i][j] = mfma32_bf(a[i][1], b[0], acc[i][j]);
+                acc[i][j] = mfma32_bf(a[i][0], b[1], acc[i][j]);
+                acc[i][j] = mfma32_bf(a[i][0], b[0], acc[i][j]);
             }
         }
     };
-    pgx3::f32x4_t acc[WX_H / 16];
-#pragma unroll
-    for (int jb = 0; jb < WX_H / 16; ++jb) acc[jb] = pgx3::f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int ua = wx_unit(16 * wave + li, kk);
-    const int64_t nsteps = (rend - r0 + WROWS - 1) / WROWS;
-    if (nsteps > 0) load(r0);
-    for (int64_t t = 0; t < nsteps; ++t) {
-        split_store();
-        __syncthreads();  // the split images of step t are complete
-        if (t + 1 < nsteps) load(r0 + (t + 1) * WROWS);  // in flight during the MFMAs
-        const uint4 a0 = Us[0][ua], a1 = Us[1][ua], a2 = Us[2][ua];
-#pragma unroll
-        for (int jb = 0; jb < WX_H / 16; ++jb) {
-            const int ub = wx_unit(WX_P + 16 * jb + li, kk);
-            acc[jb] = pgx3::mfma_x3(a0, a1, a2, Us[0][ub], Us[1][ub], Us[2][ub], acc[jb]);
-            __builtin_amdgcn_sched_barrier(0);  // one column block's operands live at a time
-        }
-        __syncthreads();  // every wave is done with the images before the next split overwrites them
+    // step t: slot t & 1 takes step t + 2's rows, the MFMAs read image t & 1, slot (t + 1) & 1 (step t + 1's rows,
+    // loaded a step ago) is split into image (t + 1) & 1; one barrier
+    float2 x0[8], x1[8];
+    float g0[8], g1[8];
+    const int64_t nsteps = (rend - r0 + WX_K - 1) / WX_K;
+    __syncthreads();  // Gs zeroed
+    // Loads and splits are unconditional (past the last step: clamped rows, zero images, zero bias terms): VMEM
+    // loads under a branch would make the compiler's wait counts assume the worst at the join -- waiting for the
+    // newest step's loads before splitting the older one -- and undo the two-step prefetch
+    load(x0, g0, 0);
+    load(x1, g1, 1);
+    split_store(x0, g0, 0);
+    __syncthreads();
+    for (int t = 0; t < (int)nsteps; t += 2) {
+        bias_step(0);
+        load(x0, g0, t + 2);
+        mfma_step(0);
+        split_store(x1, g1, 1);
+        __syncthreads();
+        bias_step(1);
+        load(x1, g1, t + 3);
+        if (t + 1 < nsteps) mfma_step(1);
+        split_store(x0, g0, 0);
+        __syncthreads();
     }
     float* out = p.part + (int64_t)blockIdx.x * p.part_stride;
 #pragma unroll
-    for (int jb = 0; jb < WX_H / 16; ++jb)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            out[(int64_t)(16 * wave + 4 * kk + e) * WX_N + WX_H * half + 16 * jb + li] = acc[jb][e];
-    if (half != 0) return;  // the bias gradients come from the first half's blocks
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int oi = WX_BP * pt + 64 * ih + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int oj = WX_BN * nt + 96 * jq + 32 * j + li;
+                out[(int64_t)oi * p.N + oj] = acc[i][j][r];
+            }
     if (isA) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) Db[g][t][4 * j + c] = db[t][c];
+        for (int t = 0; t < 4; ++t) {
+            Db[kg][t][2 * pair] = db[t][0];
+            Db[kg][t][2 * pair + 1] = db[t][1];
+        }
     }
     __syncthreads();
     {
-        const int t = tid >> 7, c = tid & 127;  // 4 x 128 = 512 sums, row groups in fixed order
-        const float v = ((Db[0][t][c] + Db[1][t][c]) + Db[2][t][c]) + Db[3][t][c];
-        out[(int64_t)WX_P * WX_N + t * WX_P + c] = v;
+        const int t = tid >> 7, c = tid & 127;  // 4 x 128 sums, k-groups in fixed order
+        const int first = t * p.F_in;            // the segment's first column (q = 3: n-tile 0)
+        const bool mine = t == 3 ? nt == 0 : (first >= WX_BN * nt && first < WX_BN * (nt + 1));
+        if (mine) out[(int64_t)p.P * p.N + t * p.P + WX_BP * pt + c] = Db[0][t][c] + Db[1][t][c];
     }
 }
 
@@ -1784,21 +1838,34 @@ __global__ __launch_bounds__(256) void reduce_generic_kernel(int64_t n, int spli
 
 int64_t up4(int64_t v) { return (v + 3) / 4 * 4; }
 
-// the split-bf16 weight gradient (wgrad_x3_kernel, opt-in: PG_FLAG_DENSE_X3) takes the model's shape
-bool wgrad_x3_shape(int64_t F_in, int64_t F_out, bool proj) { return F_in == 128 && F_out == 128 && !proj; }
+// the split-bf16 weight gradient (wgrad_x3_kernel: 128 x 384 output tiles) takes these shapes
+bool wgrad_x3_shape(int64_t F_in, int64_t F_out, bool proj) {
+    return F_in % (WX_BN / 3) == 0 && F_out % WX_BP == 0 && !proj;
+}
 
-BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj) {
+// x3w: the row splits of wgrad_x3_kernel (one 512-thread workgroup per CU over all output tiles, 16-row steps)
+// instead of wgrad_kernel's (512 workgroups of 128 x 128 tiles, 32-row steps); the workspace covers both
+BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj, bool x3w = false) {
     BwdPlan b{};
     b.K = (int)((proj ? 4 : 3) * F_in);
     b.ntn = (b.K + DG_BN - 1) / DG_BN;
-    const SplitPlan sp = split_rows(M, ((F_out + 127) / 128) * ((b.K + 127) / 128));
-    b.splits = sp.splits;
-    b.rows_per_split = sp.rows_per_split;
+    if (x3w) {
+        const int64_t tiles = (F_out / WX_BP) * (b.K / WX_BN);
+        const int64_t steps = std::max<int64_t>((M + WX_K - 1) / WX_K, 1);
+        const int64_t splits = std::min<int64_t>(std::max<int64_t>((256 + tiles - 1) / tiles, 1), steps);
+        b.rows_per_split = ((steps + splits - 1) / splits) * WX_K;
+        b.splits = (int)std::max<int64_t>((M + b.rows_per_split - 1) / b.rows_per_split, 1);
+    } else {
+        const SplitPlan sp = split_rows(M, ((F_out + 127) / 128) * ((b.K + 127) / 128));
+        b.splits = sp.splits;
+        b.rows_per_split = sp.rows_per_split;
+    }
     b.part_stride = up4(F_out * b.K + 4 * F_out);
     b.off_bt = 0;  // BT (fp32), or BT3 (three bf16 splits, dgrad_x3_kernel), or the bf16 BT
     b.off_dsp = up4(2 * (int64_t)b.K * F_out);
     b.off_part = b.off_dsp + up4((int64_t)b.ntn * 3 * M);
     b.total = b.off_part + (int64_t)b.splits * b.part_stride;
+    if (!x3w && wgrad_x3_shape(F_in, F_out, proj)) b.total = std::max(b.total, plan_of(M, F_in, F_out, proj, true).total);
     return b;
 }
 
@@ -1828,7 +1895,8 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
     PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
     PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
     const bool proj = a->W_res != nullptr;
-    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj);
+    const bool x3w = wgrad_x3_shape(a->F_in, a->F_out, proj) && !(flags & PG_FLAG_WGRAD_F32MFMA);
+    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj, x3w);
     PG_REQUIRE(g->work_floats >= pl.total, "workspace too small: %lld < %lld floats", (long long)g->work_floats,
                (long long)pl.total);
     // vector paths only: every row / column block is float4
@@ -1982,10 +2050,9 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
         w.rows_per_split = pl.rows_per_split;
         w.part_stride = pl.part_stride;
         w.part = part;
-        // the split-bf16 wgrad measured slower than the fp32 one (0.270 vs 0.190 ms at B(20,4)): one split step of
-        // register prefetch at one block per CU leaves it latency bound, so it is opt-in
-        if (wgrad_x3_shape(F_in, F_out, proj) && (flags & PG_FLAG_DENSE_X3)) {
-            hipLaunchKernelGGL(wgrad_x3_kernel, dim3((unsigned)pl.splits, 2), dim3(512), 0, s, w);
+        if (x3w) {
+            hipLaunchKernelGGL(wgrad_x3_kernel, dim3((unsigned)pl.splits, (unsigned)((F_out / WX_BP) * (K / WX_BN))),
+                               dim3(512), 0, s, w);
         } else {
             dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
             hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);

@@ -1570,13 +1570,15 @@ class MiddleTrainer:
 
     def _capture(self, x_full, y_own):
         self._x, self._y = x_full, y_own
+        self._train.prepare_capture(x_full.device)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self._loss = self._step(self._x, self._y)
         # everything the captured launches read by address stays alive with the graph: Adam's and the L2 sum's
         # device descriptor lists (and their pinned staging copies, which captured uploads re-read)
-        self._keep = list(getattr(self.opt, "_tl_cache", {}).values()) + list(self._train._LISTS.values())
+        self._keep = (list(getattr(self.opt, "_tl_cache", {}).values()) + list(self._train._LISTS.values()) +
+                      self._train.flush_deferred())
         self._graph = g
         g.replay()  # the step the capture recorded
 

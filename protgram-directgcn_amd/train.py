@@ -27,9 +27,38 @@ import torch.nn.functional as F
 from ._lib import check, load_library
 
 
+_DEFERRED: list = []  # (device tensor, host array) uploads of a capture in progress, written after it ends
+_ARENA: dict = {}     # device -> [int64 tensor, next free index]: where a capture's uploads live (prepare_capture)
+
+
+def prepare_capture(dev, n: int = 1 << 16) -> torch.Tensor:
+    """A fresh device arena (n int64) for the descriptor tables built inside the next HIP-graph capture on `dev`.
+    Allocated here, outside the capture, so the graph's own memory pool never hands those bytes to a captured
+    kernel (a table in pool memory would be clobbered at every replay by the kernels that reused its bytes during
+    the capture). The graph's owner keeps the returned tensor as long as the graph."""
+    t = torch.zeros(n, dtype=torch.int64, device=dev)
+    _ARENA[torch.device(dev)] = [t, 0]
+    return t
+
+
 def _upload(a: np.ndarray, dev, keep: Optional[list] = None) -> torch.Tensor:
-    """Host array -> device without a host sync (pinned staging, stream-ordered copy). `keep` receives the pinned
-    staging tensor: a copy captured into a HIP graph re-reads it at every replay, so its owner must keep it alive."""
+    """Host array (int64) -> device without a host sync (pinned staging, stream-ordered copy). `keep` receives the
+    pinned staging tensor: a copy captured into a HIP graph re-reads it at every replay, so its owner must keep it
+    alive. Inside a HIP-graph capture (no pinned allocation is allowed there) the table takes a slice of the arena
+    of prepare_capture(), and its contents -- static for every replay: addresses and chunk offsets -- are written by
+    flush_deferred() after the capture ends."""
+    if torch.cuda.is_current_stream_capturing():
+        if a.dtype != np.int64:
+            raise TypeError("capture-time uploads are int64 tables")
+        slot = _ARENA.get(torch.device(dev))
+        n = int(a.size)
+        if slot is None or slot[1] + n > slot[0].numel():
+            raise RuntimeError("no room for a descriptor table in this capture: call train.prepare_capture(dev) "
+                               "before capturing")
+        t = slot[0][slot[1]:slot[1] + n].view(a.shape)
+        slot[1] += (n + 1) // 2 * 2  # 16-B aligned slices
+        _DEFERRED.append((t, np.array(a, copy=True)))
+        return t
     h = torch.from_numpy(a).pin_memory()
     if keep is not None:
         keep.append(h)
@@ -63,6 +92,54 @@ class TensorList:
         self.chunk_ptr = _upload(chunks, dev, self.host)
         self.nchunks = int(chunks[-1])
         self.partial = torch.empty(max(self.nchunks, 1), dtype=torch.float32, device=dev)
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURED_LISTS.append(self)  # fields kept: a replay reads them by address
+
+
+_CAPTURED_LISTS: list = []  # TensorLists built inside a capture: kept (with the tensors they point to) by its owner
+
+
+def flush_deferred() -> list:
+    """Write the uploads deferred during a capture (see _upload); call after the capture, before the first replay.
+    Returns what the captured launches read by address -- the written tensors and the TensorLists built during the
+    capture, with the tensors their descriptors point to: the owner of the graph keeps them as long as the graph."""
+    keep = []
+    for t, a in _DEFERRED:
+        t.copy_(torch.from_numpy(a))
+        keep.append((t, a))
+    _DEFERRED.clear()
+    keep += _CAPTURED_LISTS
+    _CAPTURED_LISTS.clear()
+    keep += [slot[0] for slot in _ARENA.values()]
+    _ARENA.clear()
+    return keep
+
+
+def check_deferred(keep: list):
+    """Debug check of flush_deferred's result before a first replay: every written table reads back as built, and
+    every address in a descriptor table (all but its last column) lies inside a live allocation of the caching
+    allocator. Raises instead of letting a replay dereference a stale address."""
+    live = []
+    for seg in torch.cuda.memory_snapshot():
+        addr = seg["address"]
+        for b in seg["blocks"]:
+            if b["state"] == "active_allocated":
+                live.append((addr, addr + b["size"]))
+            addr += b["size"]
+    live.sort()
+    import bisect
+    starts = [a for a, _ in live]
+    for item in keep:
+        if not isinstance(item, tuple):
+            continue
+        t, a = item
+        if not torch.equal(t.cpu(), torch.from_numpy(a)):
+            raise RuntimeError("a deferred descriptor table does not read back as written")
+        if a.ndim == 2:
+            for ptr in a[:, :-1].reshape(-1).tolist():
+                i = bisect.bisect_right(starts, ptr) - 1
+                if i < 0 or not (live[i][0] <= ptr < live[i][1]):
+                    raise RuntimeError(f"descriptor address {ptr:#x} is not inside a live allocation")
 
 
 _LISTS: dict = {}
@@ -318,6 +395,7 @@ class GraphedTrainStep:
     device scalar, overwritten by the next call. A step that cannot be captured (a host sync inside it) falls back to
     eager steps, with a message on stderr."""
     WARM = 3
+    CHECK = False  # check_deferred before the first replay (debug)
 
     def __init__(self, model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None,
                  weight: float = 1.0):
@@ -338,19 +416,25 @@ class GraphedTrainStep:
     def _capture(self) -> torch.Tensor:
         import sys
         opt = self.args[3]
+        prepare_capture(self.args[2].device)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 loss = train_step(*self.args, **self.kw)
         except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
+            _DEFERRED.clear()
+            _CAPTURED_LISTS.clear()
+            _ARENA.clear()
             self.failed = repr(e)[:300]
             print(f"[GraphedTrainStep] HIP graph capture failed ({self.failed}); running eager steps", file=sys.stderr)
             torch.cuda.synchronize()
             return train_step(*self.args, **self.kw)
         # the descriptor lists the captured launches read by address (and their pinned staging copies, which the
         # captured uploads re-read) live as long as the graph
-        self._keep = list(getattr(opt, "_tl_cache", {}).values()) + list(_LISTS.values())
+        self._keep = list(getattr(opt, "_tl_cache", {}).values()) + list(_LISTS.values()) + flush_deferred()
+        if self.CHECK:
+            check_deferred(self._keep)
         self._graph, self._loss = g, loss
         g.replay()  # the step the capture recorded
         return loss

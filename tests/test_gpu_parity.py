@@ -544,7 +544,8 @@ def _dense_case(M, Fin, Fout, proj, vec, rows, seed):
                                                       (129, 16, 40, True, True, True), (64, 128, 96, False, True, True),
                                                       (5000, 32, 32, False, True, False), (300, 18, 10, True, True, False),
                                                       (257, 7, 5, True, True, False), (100, 13, 30, False, True, True),
-                                                      (64, 6, 9, True, False, False)])
+                                                      (64, 6, 9, True, False, False), (2000, 256, 256, False, True, False),
+                                                      (1500, 128, 256, False, True, True), (20, 128, 128, False, True, False)])
 def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
     """Autograd of the fused dense layer (pg_directgcn_dense_bwd_f32: the MFMA kernels, or its any-shape kernels
     when F_in / F_out are not multiples of 4) against float64 autograd of protgram_directgcn.py:100-133 + residual
@@ -597,11 +598,11 @@ def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
 
 
 @pytest.mark.parametrize("M,rows", [(1000, False), (3001, True)])
-def test_dense_backward_x3_wgrad_vs_float64(pkg, cuda, monkeypatch, M, rows):
-    """The opt-in split-bf16 weight gradient (PG_FLAG_DENSE_X3 in the backward flags) through the same float64
-    autograd check as the default fp32 one."""
-    from protgram_directgcn_amd._lib import PG_FLAG_DENSE_X3
-    monkeypatch.setenv("PG_SPMM_FLAGS", hex(PG_FLAG_DENSE_X3))
+def test_dense_backward_f32mfma_wgrad_vs_float64(pkg, cuda, monkeypatch, M, rows):
+    """The fp32-MFMA weight gradient (PG_FLAG_WGRAD_F32MFMA: wgrad_kernel instead of the default split-bf16
+    wgrad_x3_kernel at these shapes) through the same float64 autograd check."""
+    from protgram_directgcn_amd._lib import PG_FLAG_WGRAD_F32MFMA
+    monkeypatch.setenv("PG_SPMM_FLAGS", hex(PG_FLAG_WGRAD_F32MFMA))
     test_dense_backward_vs_float64(pkg, cuda, M, 128, 128, False, True, rows)
 
 
@@ -1005,11 +1006,13 @@ def test_train_step_matches_reference_loop(pkg, cuda, amp):
         assert_grad_close(runs[1][1][k], v.cpu(), f"param {k}")
 
 
-@pytest.mark.parametrize("amp", [False, True])
-def test_graphed_train_step_matches_eager(pkg, cuda, amp):
+@pytest.mark.parametrize("amp,adam", [(False, True), (True, True), (False, False)])
+def test_graphed_train_step_matches_eager(pkg, cuda, amp, adam):
     """train.GraphedTrainStep (the whole train_step captured as a HIP graph after its warm-up steps, then replayed):
     eight steps from the same start give the same losses and parameters, bit for bit, as eight eager train_step calls
-    (train.Adam with the folded L2 term; dropout off, so both runs draw nothing), with and without GradScaler."""
+    (dropout off, so both runs draw nothing): train.Adam with the folded L2 term, with and without GradScaler, and
+    torch SGD with the L2 gradient added by pg_multi_axpy_f32 (its descriptor table built inside the capture, in the
+    arena of train.prepare_capture; checked by train.check_deferred before the first replay)."""
     from protgram_directgcn_amd import train
     N, s, d, c = pkg.synth.de_bruijn_edges(3)
     g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
@@ -1020,10 +1023,11 @@ def test_graphed_train_step_matches_eager(pkg, cuda, amp):
     for graphed in (False, True):
         torch.manual_seed(0)
         m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
-        opt = train.Adam(m.parameters(), lr=1e-3)
+        opt = train.Adam(m.parameters(), lr=1e-3) if adam else torch.optim.SGD(m.parameters(), lr=1e-2)
         scaler = torch.amp.GradScaler("cuda", enabled=amp)
         if graphed:
             st = train.GraphedTrainStep(m, data, y, opt, l2_lambda=1e-3, scaler=scaler)
+            st.CHECK = True
             losses = [float(st()) for _ in range(8)]
             assert st._graph is not None and st.failed is None, st.failed
             st.close()

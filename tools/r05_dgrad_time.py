@@ -42,8 +42,8 @@ for F in (128, 256):
     res[f"bwd_bf16_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(dY, Z, Y, prm, 0, act=True, packs=packs))
     res[f"bwd_f32_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(dYf, Zf, Yf, prm, 0, act=True))
     from protgram_directgcn_amd import _lib
-    res[f"bwd_f32_wgradx3_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(
-        dYf, Zf, Yf, prm, 0, act=True, flags=ops.default_flags() | _lib.PG_FLAG_DENSE_X3))
+    res[f"bwd_f32_wgradf32mfma_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(
+        dYf, Zf, Yf, prm, 0, act=True, flags=ops.default_flags() | _lib.PG_FLAG_WGRAD_F32MFMA))
     res[f"bwd_f32_dgradf32mfma_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(
         dYf, Zf, Yf, prm, 0, act=True, flags=ops.default_flags() | _lib.PG_FLAG_DGRAD_F32MFMA))
 print(json.dumps(res), flush=True)

@@ -486,6 +486,19 @@ int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr
                 const float* found_inf, float* sq_partial, void* stream);
 int pg_multi_sum_f32(int64_t n, const float* x, float* out, void* stream);
 
+/* Training step of the prediction head (decoder_fc -> log_softmax -> nll_loss, protgram_directgcn.py:218-222 and
+ * protgram_directgcn_trainer.py:91-100), forward and backward in one pass over the M rows of h [M, F]:
+ *   a = dropout(relu(h W1^T + b1)), logits = a W2^T + b2, loss = loss_weight * sum_m -log_softmax(logits[m])[y[m]];
+ * with s = *grad_scale (or 1): dh [M, F] and grads = [dW1 (H x F) | db1 (H) | dW2 (C x H) | db2 (C)] of s * loss;
+ * loss[0] = the unscaled loss. drop_p > 0: keep element (m, j) of a by a counter-based draw from seed[0] (device
+ * int64), scaled by 1 / (1 - drop_p). W1 [H, F], W2 [C, H] row-major (nn.Linear weights); y int64 [M].
+ * F = 128, H = 64, C <= 32 only (PG_ERR_UNSUPPORTED otherwise). work: pg_head_train_workspace floats. */
+int64_t pg_head_train_workspace(int64_t M, int64_t F, int64_t H, int64_t C);
+int pg_head_train_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h, int64_t ldh, const float* W1,
+                      const float* b1, const float* W2, const float* b2, const int64_t* y, float loss_weight,
+                      float drop_p, const int64_t* seed, const float* grad_scale, float* dh, int64_t lddh,
+                      float* grads, float* loss, float* work, int64_t work_floats, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

@@ -142,6 +142,9 @@ SIGNATURES = {
     "pg_gemm_at_b_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                              c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "pg_head_train_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "pg_head_train_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                         c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
 }
 
 _lib = None

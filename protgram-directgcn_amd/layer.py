@@ -246,6 +246,10 @@ class ProtGramDirectGCN(nn.Module):
                             data.edge_index_undirected_norm, getattr(data, "edge_weight_undirected_norm", None))
 
     def forward(self, data) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self.head(self.body(data))
+
+    def body(self, data) -> torch.Tensor:
+        """The layers (protgram_directgcn.py:195-216): h before the prediction head."""
         x = getattr(data, "x", None)
         ei_in = getattr(data, "edge_index_in", None)
         ei_out = getattr(data, "edge_index_out", None)
@@ -269,7 +273,16 @@ class ProtGramDirectGCN(nn.Module):
             else:
                 h = conv.fused_forward(h, g, original_indices, res_x=h, act=True, fused_norm=self.fused_norm)
             h = F.dropout(h, p=self.dropout, training=self.training)
-        return self.head(h)
+        return h
+
+    def head_train_args(self):
+        """(W1, b1, W2, b2, dropout p) of the decoder when ops.head_train takes it (Linear, ReLU, Dropout, Linear),
+        else None."""
+        dec = self.decoder_fc
+        if not (len(dec) == 4 and isinstance(dec[0], nn.Linear) and isinstance(dec[1], nn.ReLU) and
+                isinstance(dec[2], nn.Dropout) and isinstance(dec[3], nn.Linear)):
+            return None
+        return dec[0].weight, dec[0].bias, dec[3].weight, dec[3].bias, dec[2].p if self.training else 0.0
 
     def head(self, h, need_emb: bool = True):
         """decoder_fc -> log_softmax, and l2_normalize (protgram_directgcn.py:218-222). Inference (eval, no

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import ops
 from ._lib import check, load_library
 
 
@@ -336,6 +337,11 @@ class Adam(torch.optim.Optimizer):
         return loss
 
 
+# train_step runs the prediction head through ops.head_train (one kernel for its forward and backward) when the model
+# offers it (ProtGramDirectGCN.head_train_args) and the kernel takes the shape; False: the framework ops
+HEAD_FUSED = True
+
+
 def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None, weight: float = 1.0,
                autocast: bool = True) -> torch.Tensor:
     """One step of the reference loop (trainer :91-100, or :129-140 with weight = batch nodes / total nodes).
@@ -343,9 +349,39 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
     params = [p for p in model.parameters() if p.requires_grad]
     optimizer.zero_grad(set_to_none=True)  # autograd then assigns gradients instead of adding into zeros
     use_amp = autocast and scaler is not None and scaler.is_enabled()
-    with torch.amp.autocast("cuda", enabled=use_amp):
-        lp, _ = model(data=data)
+    scaled = scaler is not None and scaler.is_enabled()
+    head = model.head_train_args() if HEAD_FUSED and hasattr(model, "head_train_args") else None
+    if head is not None:
+        # the prediction head's forward and backward in one kernel (ops.head_train): the layers' output h gets its
+        # gradient (already scaled by the GradScaler's scale) from the kernel, the decoder parameters theirs
+        with torch.amp.autocast("cuda", enabled=use_amp):
+            h = model.body(data)
+        hf = h.float()
+        W1, b1, W2, b2, p_drop = head
+        seed = torch.randint(0, 2 ** 62, (1,), device=hf.device, dtype=torch.int64) if p_drop > 0 else None
+        scale = None
+        if scaled:
+            scaler.scale(torch.zeros((), device=hf.device))  # the scale tensor exists from here on
+            scale = scaler._scale
+        r = ops.head_train(hf, W1, b1, W2, b2, y, weight, p_drop, seed, scale) if hf.is_cuda else None
+        if r is not None:
+            loss, dh, grads = r
+            for prm, gr in zip((W1, b1, W2, b2), grads):
+                if prm.requires_grad:
+                    prm.grad = gr
+            torch.autograd.backward(hf, grad_tensors=dh)
+            return _finish_step(model, params, optimizer, loss, l2_lambda, scaler, scaled, backward=False)
+        lp, _ = model.head(hf, need_emb=False)
         loss = nll_mean(lp.float(), y) * weight
+    else:
+        with torch.amp.autocast("cuda", enabled=use_amp):
+            lp, _ = model(data=data)
+            loss = nll_mean(lp.float(), y) * weight
+    return _finish_step(model, params, optimizer, loss, l2_lambda, scaler, scaled, backward=True)
+
+
+def _finish_step(model, params, optimizer, loss, l2_lambda, scaler, scaled, backward: bool):
+    """train_step after the forward: backward (unless done), the L2 term, the optimizer step; returns the loss."""
     # train.Adam takes the L2 gradient 2 * l2_lambda * p as extra weight decay inside its one launch (added to
     # the unscaled gradient before the moments, exactly where the gradient sum would put it), and -- when it steps
     # exactly these parameters -- the L2 value too, from the pre-update parameters it reads anyway; other
@@ -354,8 +390,8 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
     fused_sq = fold and ({id(p) for g in optimizer.param_groups for p in g["params"]} == {id(p) for p in params}
                          and len({p.device for p in params}) == 1)
     l2 = l2_sqsum(params) if l2_lambda and not fused_sq else None
-    scaled = scaler is not None and scaler.is_enabled()
-    (scaler.scale(loss) if scaled else loss).backward()
+    if backward:
+        (scaler.scale(loss) if scaled else loss).backward()
     if l2_lambda and not fold:
         add_l2_grad(params, l2_lambda, scale=scaler._scale if scaled else None)  # device-side scale: no sync
     else:  # the reference's (0 *) l2 term gives every parameter a gradient, so it is stepped

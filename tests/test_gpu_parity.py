@@ -1383,3 +1383,85 @@ def test_propagate_dense_span_backward(pkg, cuda, n, F, res):
     out = ops.layer_dense_backward(w, Z, Y, prm, 0, act=True, span=(g.ngram.diag3(), res))
     ref = (out["dZ"].view(N, 3, F) * g.ngram.diag3().unsqueeze(2)).sum(1) + (out["dpre"] if res else 0.0)
     assert_grad_close(out["E"], ref, "E = sum_q Wdiag_q dZ_q (+ dpre)")
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# ops.head_train (round 5): the prediction head's training step in one kernel
+def _drop_keep(seed: int, M: int, H: int, p: float):
+    """The kernel's dropout draw restated on the host (pg_head_train.hip, drop_hash): keep (m, j) when the mixed
+    index's top 24 of 32 bits are >= ceil(p 2^24)."""
+    m = np.arange(M, dtype=np.uint64)[:, None]
+    j = np.arange(H, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed) ^ (np.uint64(0x9E3779B97F4A7C15) * (m * np.uint64(64) + j + np.uint64(1)))
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xff51afd7ed558ccd)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xc4ceb9fe1a85ec53)
+        x ^= x >> np.uint64(33)
+    u = (x & np.uint64(0xffffffff)) >> np.uint64(8)
+    thr = min(16777215, int(np.ceil(p * 16777216.0)))
+    return torch.from_numpy(u >= np.uint64(thr))
+
+
+@pytest.mark.parametrize("M,drop,scaled", [(3001, 0.0, False), (64, 0.0, False), (1000, 0.5, False),
+                                           (777, 0.5, True), (20000, 0.25, False)])
+def test_head_train_vs_float64(pkg, cuda, M, drop, scaled):
+    """ops.head_train against torch autograd in float64 on the same inputs: loss (nll mean x weight of
+    decoder Linear -> ReLU -> Dropout -> Linear -> log_softmax), dh and the four decoder gradients; with dropout the
+    kernel's counter-based mask is restated on the host (_drop_keep); with a loss scale (GradScaler) every gradient
+    carries it and the loss does not."""
+    from protgram_directgcn_amd import ops
+    F, H, C, weight = 128, 64, 20, 0.75
+    gen = torch.Generator().manual_seed(M)
+    h = torch.randn(M, F, generator=gen)
+    W1, b1 = torch.randn(H, F, generator=gen) * 0.1, torch.randn(H, generator=gen) * 0.1
+    W2, b2 = torch.randn(C, H, generator=gen) * 0.2, torch.randn(C, generator=gen) * 0.1
+    y = torch.randint(0, C, (M,), generator=gen)
+    seed = 0x1234_5678_9abc_def0 + M
+    seed_t = torch.tensor([seed], dtype=torch.int64, device=cuda)
+    s = 1024.0 if scaled else 1.0
+    scale_t = torch.tensor(s, device=cuda) if scaled else None
+    r = ops.head_train(h.to(cuda), W1.to(cuda), b1.to(cuda), W2.to(cuda), b2.to(cuda), y.to(cuda), weight, drop,
+                       seed_t if drop > 0 else None, scale_t)
+    assert r is not None
+    loss, dh, grads = r
+    torch.cuda.synchronize()
+    # float64 reference
+    ps = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2)]
+    a = torch.relu(ps[0] @ ps[1].t() + ps[2])
+    if drop > 0:
+        a = a * _drop_keep(seed, M, H, drop).double() / (1.0 - drop)
+    lp = torch.log_softmax(a @ ps[3].t() + ps[4], dim=1)
+    loss_r = torch.nn.functional.nll_loss(lp, y) * weight
+    (loss_r * s).backward()
+    assert abs(float(loss) - float(loss_r)) <= 1e-5 * abs(float(loss_r)), (float(loss), float(loss_r))
+    for got, ref, what in [(dh, ps[0].grad, "dh")] + [(g, q.grad, n) for g, q, n in
+                                                       zip(grads, ps[1:], ("dW1", "db1", "dW2", "db2"))]:
+        assert_grad_close(got.cpu(), ref.float(), f"head_train {what}")
+
+
+def test_train_step_fused_head_matches_framework_head(pkg, cuda):
+    """train.train_step with the head in one kernel (HEAD_FUSED, the default) against the framework ops
+    (HEAD_FUSED = False): 3 SGD steps with the L2 gradient (parameter updates linear in the gradients), eval mode (no
+    dropout draw), losses and parameters within fp32 rounding of each other."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    runs = []
+    for fused in (False, True):
+        train.HEAD_FUSED = fused
+        try:
+            torch.manual_seed(0)
+            m = pkg.ProtGramDirectGCN([64, 128, 128], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+            opt = torch.optim.SGD(m.parameters(), lr=0.05)
+            losses = [float(train.train_step(m, data, y, opt, l2_lambda=1e-3)) for _ in range(3)]
+            runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+        finally:
+            train.HEAD_FUSED = True
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-6)
+    for k, v in runs[0][1].items():
+        assert_grad_close(runs[1][1][k].cpu(), v.cpu(), f"param {k}")

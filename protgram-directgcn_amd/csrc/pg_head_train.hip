@@ -131,14 +131,23 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
         if (t + gridDim.x < ntiles) load(t + gridDim.x);
 
         // A: a = dropout(relu(h W1^T + b1))
+        {
+            f32x4 accA[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            // tiles wave and wave + 8: row tiles wave / 4 and wave / 4 + 2, the same column tile; the two chains
+            // interleaved in one k loop (as in every phase below)
+            const float* ap0 = &Hs[(16 * (wave / (TH / 16)) + l16) * LDH + kq];
+            const float* ap1 = &Hs[(16 * ((wave + 8) / (TH / 16)) + l16) * LDH + kq];
+            const float* bp = &W1s[(16 * (wave % (TH / 16)) + l16) * LDW1 + kq];  // same column tile for both
+#pragma unroll 8
+            for (int k = 0; k < TF; k += 4) {
+                const float b = bp[k];
+                accA[0] = mfma16(ap0[k], b, accA[0]);
+                accA[1] = mfma16(ap1[k], b, accA[1]);
+            }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int tt = wave + 8 * q, rt = tt / (TH / 16), ct = tt % (TH / 16);
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            const float* ap = &Hs[(16 * rt + l16) * LDH + kq];
-            const float* bp = &W1s[(16 * ct + l16) * LDW1 + kq];
-#pragma unroll 8
-            for (int k = 0; k < TF; k += 4) acc = mfma16(ap[k], bp[k], acc);
+            const f32x4 acc = accA[q];
             const int j = 16 * ct + l16;
             const float bj = p.b1[j];
 #pragma unroll
@@ -148,6 +157,7 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
                 if (p.drop_thr) v = (drop_hash(seed, m0 + row, j) >> 8) >= p.drop_thr ? v * p.inv_keep : 0.f;
                 As[row * LDA + j] = v;
             }
+        }
         }
         __syncthreads();
 
@@ -210,13 +220,22 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
             for (int k = 0; k < TR; k += 4)
                 accW2 = mfma16(Ls[(k + kq) * LDL + 16 * ct + l16], As[(k + kq) * LDA + 16 * ht + l16], accW2);
         }
+        f32x4 accD[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        {
+            const float* ap0 = &Ls[(16 * (wave / (TH / 16)) + l16) * LDL + kq];
+            const float* ap1 = &Ls[(16 * ((wave + 8) / (TH / 16)) + l16) * LDL + kq];
+            const float* bp = &W2s[kq * LDW2 + 16 * (wave % (TH / 16)) + l16];
+#pragma unroll
+            for (int k = 0; k < TC; k += 4) {
+                const float b = bp[k * LDW2];
+                accD[0] = mfma16(ap0[k], b, accD[0]);
+                accD[1] = mfma16(ap1[k], b, accD[1]);
+            }
+        }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int tt = wave + 8 * q, rt = tt / (TH / 16), ht = tt % (TH / 16);
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            const float* ap = &Ls[(16 * rt + l16) * LDL + kq];
-#pragma unroll
-            for (int k = 0; k < TC; k += 4) acc = mfma16(ap[k], W2s[(k + kq) * LDW2 + 16 * ht + l16], acc);
+            const f32x4 acc = accD[q];
             const int j = 16 * ht + l16;
             const float ik = p.drop_thr ? p.inv_keep : 1.f;
 #pragma unroll
@@ -233,26 +252,33 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
         __syncthreads();
 
         // E: dh = da W1 (stored); dW1 += da^T h; db1 += column sums of da
+        {
+            // dh: tiles wave + 8 q = (row tile q, feature tile wave); four chains interleaved
+            f32x4 accE[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int tt = wave + 8 * q, rt = tt / (TF / 16), ft = tt % (TF / 16);
-            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            const float* ap = &Ds[(16 * rt + l16) * LDA + kq];
-#pragma unroll 8
-            for (int k = 0; k < TH; k += 4) acc = mfma16(ap[k], W1s[(k + kq) * LDW1 + 16 * ft + l16], acc);
-            const int f = 16 * ft + l16;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t m = m0 + 16 * rt + 4 * kq + r;
-                if (m < p.M) p.dh[m * p.lddh + f] = acc[r];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int tt = wave + 8 * q, ht = tt / (TF / 16), ft = tt % (TF / 16);
+            for (int q = 0; q < 4; ++q) accE[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const float* bp = &W1s[kq * LDW1 + 16 * wave + l16];
 #pragma unroll 4
-            for (int k = 0; k < TR; k += 4)
-                accW1[q] = mfma16(Ds[(k + kq) * LDA + 16 * ht + l16], Hs[(k + kq) * LDH + 16 * ft + l16], accW1[q]);
+            for (int k = 0; k < TH; k += 4) {
+                const float b = bp[k * LDW1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) accE[q] = mfma16(Ds[(16 * q + l16) * LDA + k + kq], b, accE[q]);
+            }
+            const int f = 16 * wave + l16;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t m = m0 + 16 * q + 4 * kq + r;
+                    if (m < p.M) p.dh[m * p.lddh + f] = accE[q][r];
+                }
+            // dW1 += da^T h: tiles wave + 8 q = (hidden tile q, feature tile wave)
+#pragma unroll 4
+            for (int k = 0; k < TR; k += 4) {
+                const float b = Hs[(k + kq) * LDH + 16 * wave + l16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) accW1[q] = mfma16(Ds[(k + kq) * LDA + 16 * q + l16], b, accW1[q]);
+            }
         }
         if (tid < TH) {  // db1: rows in order
             float s = 0.f;
@@ -290,15 +316,23 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
     }
 }
 
-// grads[i] = sum over workgroups of part[b][i] (workgroup order), i < P_LOSS + 1: dW1, db1, dW2 (C rows), db2, loss
+// grads[i] = sum over workgroups of part[b][i], i <= P_LOSS: dW1, db1, dW2 (C rows), db2, loss. A block owns 32
+// consecutive entries; its 8 thread groups take every 8th partial and are combined in group order (deterministic).
 __global__ __launch_bounds__(256) void head_train_reduce_kernel(int nparts, int C, const float* part, float* grads,
                                                                 float* loss) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i > P_LOSS) return;
+    __shared__ float acc_s[8][32];
+    const int c = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    const int i = blockIdx.x * 32 + c;
     float s = 0.f;
-    for (int b = 0; b < nparts; ++b) s += part[(int64_t)b * P_STRIDE + i];
-    if (i < P_DW2) grads[i] = s;                                                      // dW1, db1
-    else if (i < P_DB2) { if ((i - P_DW2) / TH < C) grads[i] = s; }                   // dW2 rows < C
+    if (i <= P_LOSS)
+        for (int b = grp; b < nparts; b += 8) s += part[(int64_t)b * P_STRIDE + i];
+    acc_s[grp][c] = s;
+    __syncthreads();
+    if (grp != 0 || i > P_LOSS) return;
+    s = acc_s[0][c];
+    for (int g = 1; g < 8; ++g) s += acc_s[g][c];
+    if (i < P_DW2) grads[i] = s;                                                          // dW1, db1
+    else if (i < P_DB2) { if ((i - P_DW2) / TH < C) grads[i] = s; }                       // dW2 rows < C
     else if (i < P_LOSS) { if (i - P_DB2 < C) grads[P_DW2 + C * TH + (i - P_DB2)] = s; }  // db2
     else loss[0] = s;
 }
@@ -349,7 +383,7 @@ int pg_head_train_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h
     p.part = work;
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(head_train_kernel, dim3((unsigned)grid), dim3(NT), 0, s, p);
-    hipLaunchKernelGGL(head_train_reduce_kernel, dim3((P_LOSS + 1 + 255) / 256), dim3(256), 0, s, grid, (int)C,
+    hipLaunchKernelGGL(head_train_reduce_kernel, dim3((P_LOSS + 1 + 31) / 32), dim3(256), 0, s, grid, (int)C,
                        (const float*)work, grads, loss);
     return pg::check_launch("pg_head_train_f32");
 }

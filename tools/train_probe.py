@@ -20,6 +20,12 @@ fused = "--fused" in sys.argv          # train.train_step instead of the referen
 adam_fused = "--adam-fused" in sys.argv
 our_adam = "--our-adam" in sys.argv     # train.Adam (one HIP launch per step)
 graphed = "--graph" in sys.argv         # train.GraphedTrainStep (implies --fused)
+NO_OPTS = [a for a in sys.argv[2:] if a.startswith("--no")]
+if "--no-span" in sys.argv:             # the 4x4-block transposed kernel instead of ops.PropagateDense
+    from protgram_directgcn_amd import ops as _ops
+    _ops.SPAN_BACKWARD = False
+if "--no-head" in sys.argv:             # the framework ops for the prediction head instead of ops.head_train
+    pkg.train.HEAD_FUSED = False
 dims = [128, 128, 128]
 for a in sys.argv:
     if a.startswith("--dims="):
@@ -68,4 +74,4 @@ t0 = time.perf_counter()
 for _ in range(steps):
     loss = step()
 torch.cuda.synchronize()
-print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}, our_adam={our_adam}, graph={graphed}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")
+print(f"train step dims={dims} (amp={amp}, bf16={bf16}, fused={fused}, adam_fused={adam_fused}, our_adam={our_adam}, graph={graphed}, opts={NO_OPTS}) {1e3 * (time.perf_counter() - t0) / steps:.3f} ms  loss {loss.item():.4f}")

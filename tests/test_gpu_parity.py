@@ -10,6 +10,8 @@ vectors. Tolerances:
     below the summed magnitude; they are checked against the tensor's scale:
     |d| <= 2e-5*max|ref| + 1e-4*|ref|  (observed errors ~1e-7 of the summed magnitude)
 """
+import functools
+
 import numpy as np
 import pytest
 import torch
@@ -1393,7 +1395,7 @@ def _drop_keep(seed: int, M: int, H: int, p: float):
     m = np.arange(M, dtype=np.uint64)[:, None]
     j = np.arange(H, dtype=np.uint64)[None, :]
     with np.errstate(over="ignore"):
-        x = np.uint64(seed) ^ (np.uint64(0x9E3779B97F4A7C15) * (m * np.uint64(64) + j + np.uint64(1)))
+        x = np.uint64(seed) ^ (np.uint64(0x9E3779B97F4A7C15) * (m * np.uint64(H) + j + np.uint64(1)))
         x ^= x >> np.uint64(33)
         x *= np.uint64(0xff51afd7ed558ccd)
         x ^= x >> np.uint64(33)
@@ -1404,15 +1406,15 @@ def _drop_keep(seed: int, M: int, H: int, p: float):
     return torch.from_numpy(u >= np.uint64(thr))
 
 
-@pytest.mark.parametrize("M,drop,scaled", [(3001, 0.0, False), (64, 0.0, False), (1000, 0.5, False),
-                                           (777, 0.5, True), (20000, 0.25, False)])
-def test_head_train_vs_float64(pkg, cuda, M, drop, scaled):
-    """ops.head_train against torch autograd in float64 on the same inputs: loss (nll mean x weight of
+@pytest.mark.parametrize("M,drop,scaled,F", [(3001, 0.0, False, 128), (64, 0.0, False, 128), (1000, 0.5, False, 128),
+                                             (777, 0.5, True, 128), (20000, 0.25, False, 128)])
+def test_head_train_vs_float64(pkg, cuda, M, drop, scaled, F):
+    """ops.head_train (F = 128, hidden 64) against torch autograd in float64 on the same inputs: loss (nll mean x weight of
     decoder Linear -> ReLU -> Dropout -> Linear -> log_softmax), dh and the four decoder gradients; with dropout the
     kernel's counter-based mask is restated on the host (_drop_keep); with a loss scale (GradScaler) every gradient
     carries it and the loss does not."""
     from protgram_directgcn_amd import ops
-    F, H, C, weight = 128, 64, 20, 0.75
+    H, C, weight = F // 2, 20, 0.75
     gen = torch.Generator().manual_seed(M)
     h = torch.randn(M, F, generator=gen)
     W1, b1 = torch.randn(H, F, generator=gen) * 0.1, torch.randn(H, generator=gen) * 0.1
@@ -1425,6 +1427,9 @@ def test_head_train_vs_float64(pkg, cuda, M, drop, scaled):
     r = ops.head_train(h.to(cuda), W1.to(cuda), b1.to(cuda), W2.to(cuda), b2.to(cuda), y.to(cuda), weight, drop,
                        seed_t if drop > 0 else None, scale_t)
     assert r is not None
+    # F = 256 (config 5) is declined: the caller runs the framework ops
+    z = functools.partial(torch.zeros, device=cuda)
+    assert ops.head_train(z(4, 256), z(128, 256), z(128), z(C, 128), z(C), y[:4].to(cuda)) is None
     loss, dh, grads = r
     torch.cuda.synchronize()
     # float64 reference

@@ -196,8 +196,32 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     g_gpu = {k: prm.grad.detach().cpu() for k, prm in m.named_parameters()}
     m.zero_grad(set_to_none=True)
     opt = train.Adam(m.parameters(), lr=LR)
+    p_pre = {k: prm.detach().cpu().clone() for k, prm in m.named_parameters()}
+    # rows whose decoder pre-activation sits within fp32 rounding of ReLU's kink: there the head kernel and the oracle
+    # may take different branches (as the layers' leaky_relu above, whose GPU choices the oracle was handed)
+    with torch.no_grad():
+        hb = m.body(data_coo).double().cpu()
+    dec = m.decoder_fc[0]
+    W1d, b1d = dec.weight.detach().double().cpu(), dec.bias.detach().double().cpu()
+    zpre = hb @ W1d.t() + b1d
+    zabs = hb.abs() @ W1d.abs().t() + b1d.abs()  # the size of the fp32 sum's terms: its rounding is ~1e-7 of this
+    kink_rows = (zpre.abs() <= 2e-6 * zabs).any(1)
+    assert int(kink_rows.sum()) <= 1e-3 * N, int(kink_rows.sum())
     calls.clear()
     loss_s = train.train_step(m, data_coo, yd, opt, l2_lambda=LAM, scaler=None)  # through the trainer's COO wiring
+    # the gradients the step's Adam launch used: train_step's own (its head runs in one kernel, ops.head_train, whose
+    # sums are ordered differently from the autograd path's g_gpu) plus the L2 gradient Adam folds in
+    g_step = {k: prm.grad.detach().cpu() + 2 * LAM * p_pre[k] for k, prm in m.named_parameters()}
+    fails = []
+    for k in g_step:  # those gradients against the oracle, as the autograd path's above (per-node rows at a kink aside)
+        got = g_step[k]
+        if got.dim() >= 1 and got.size(0) == N:
+            got = torch.where(kink_rows.view(-1, *([1] * (got.dim() - 1))), p[k].grad, got)
+        try:
+            _grad_close_or_as_exact(got, p[k].grad, p64[k].grad, f"train_step grad {k}")
+        except AssertionError as ex:
+            fails.append(str(ex).split("\n")[0])
+    assert not fails, "\n".join(fails)
     # the transposed propagation of every layer whose input needs a gradient: the span dense backward (diagonal term
     # and residual into E) + the off-diagonal transposed middle-tile kernel (ops.PropagateDense), not the 4x4 kernel
     assert _fwd_tile(calls) == len(m.convs), calls
@@ -206,8 +230,9 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     assert abs(float(loss_s) - loss_r) <= 1e-5 * abs(loss_r)
     for k, prm in m.named_parameters():
         gref = p[k].grad
-        # the gradient tolerance, or the actual GPU-vs-oracle gradient difference where that is larger
-        delta = torch.maximum(2e-5 * float(gref.abs().max()) + 1e-4 * gref.abs(), 1.5 * (g_gpu[k] - gref).abs())
+        # the gradient tolerance, or the actual GPU-vs-oracle gradient difference (of either GPU path) where larger
+        delta = torch.maximum(2e-5 * float(gref.abs().max()) + 1e-4 * gref.abs(),
+                              1.5 * torch.maximum((g_gpu[k] - gref).abs(), (g_step[k] - gref).abs()))
         # Adam's first update is lr * g / (|g| + eps): a gradient within delta of the oracle's moves it by at most
         # lr * eps * delta / (|g| - delta + eps)^2, or by up to 2 lr where the sign itself is within tolerance
         sens = torch.where(gref.abs() > delta, LR * 1e-8 * delta / (gref.abs() - delta + 1e-8) ** 2,

@@ -79,6 +79,8 @@ typedef struct pg_edge1 {
 #define PG_FLAG_DENSE_X3 (1u << 16)       /* dense forward: the split-bf16 W-stationary kernel (see pg_dense.hip); the
                                              backward ignores it since round 5 (its split-bf16 weight gradient is the
                                              default, PG_FLAG_WGRAD_F32MFMA opts out) */
+#define PG_FLAG_WGRAD_BF16_TILED (1u << 11) /* bf16 dense backward: the 128 x 128-tile weight-gradient kernel instead of
+                                               the staged 128 x 384 one (default where F_in, F_out % 128 == 0) */
 #define PG_FLAG_WGRAD_F32MFMA (1u << 18)  /* fp32 dense backward: the fp32-MFMA weight-gradient kernel instead of the
                                              split-bf16 one (default where F_in % 128 == 0, F_out % 128 == 0 and no
                                              projected residual) */

@@ -1045,7 +1045,8 @@ __global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
 // takes 64 cycles per 2-deep k-step, the six bf16 products 6 x 32 per 16-deep one: 2.7x fewer matrix-core cycles,
 // which moves the B(20,4) F = 128 weight gradient (15.7 GFLOP, 0.33 GB of operands) from the fp32 matrix cores'
 // bound (~0.10 ms at peak, 0.175 ms measured) to about the HBM one.
-// One 512-thread workgroup per (row split, 128 x 384 output tile), one per CU (LDS 100 KB): each 16-row step is
+// One 512-thread workgroup per (row split, 128 x 384 output tile), one per CU (LDS 100 KB; the tiles of a split on
+// one XCD at neighbouring times, wgrad_tile_of, so they share the split's rows through its L2): each 16-row step is
 // staged ONCE for the whole tile -- A = dpre (128 columns) and B = s_q Z_q (384 columns), 8 rows x 2 columns per
 // thread, loaded two steps ahead through buffer descriptors -- split into three bf16 images and stored transposed, image [split][k-group][column]
 // of 16-B units (the 8 rows of a k-group of one column: one MFMA operand of one lane), double-buffered (one barrier
@@ -1056,13 +1057,25 @@ __global__ __launch_bounds__(64 * NW) void wgrad_kernel(WgradP p) {
 // the n-tile-0 workgroups reduce them over their two k-groups.
 constexpr int WX_BP = 128, WX_BN = 384, WX_COLS = WX_BP + WX_BN, WX_K = 16;
 
-__global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgradP p) {
+// blockIdx.x -> (split, tile) with the `tiles` workgroups of a split on one XCD (hardware dispatch: block b on XCD
+// b % 8), dispatched together: b = xcd + 8 (tiles j + tile) for split 8 j + xcd. Splits past `splits` get tile -1.
+__device__ __forceinline__ void wgrad_tile_of(int b, int tiles, int splits, int& split, int& tile) {
+    const int xcd = b & 7, q = b >> 3;
+    split = 8 * (q / tiles) + xcd;
+    tile = q % tiles;
+    if (split >= splits) tile = -1;
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgradP p, int splits) {
     __shared__ __attribute__((aligned(16))) uint4 U[2][3][2][WX_COLS];
     __shared__ float Db[2][4][WX_BP];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, kh = lane >> 5;
     const int n_tiles = p.N / WX_BN;
-    const int pt = (int)blockIdx.y / n_tiles, nt = (int)blockIdx.y % n_tiles;
-    const int64_t r0 = (int64_t)blockIdx.x * p.rows_per_split;
+    int split, tile;
+    wgrad_tile_of((int)blockIdx.x, (p.P / WX_BP) * n_tiles, splits, split, tile);
+    if (tile < 0) return;  // whole workgroup: no barrier reached
+    const int pt = tile / n_tiles, nt = tile % n_tiles;
+    const int64_t r0 = (int64_t)split * p.rows_per_split;
     const int64_t rend = min(r0 + p.rows_per_split, p.M);
     // staging role, from the wave index in a scalar register (so the buffer descriptors below are wave-uniform):
     // waves 0-1 stage A (k-group = wave), waves 2-4 / 5-7 B (k-group 0 / 1), 64 column pairs per wave
@@ -1195,7 +1208,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgradP p) {
         split_store(x0, g0, 0);
         __syncthreads();
     }
-    float* out = p.part + (int64_t)blockIdx.x * p.part_stride;
+    float* out = p.part + (int64_t)split * p.part_stride;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1730,6 +1743,186 @@ SplitPlan split_rows(int64_t M, int64_t tiles) {
     return sp;
 }
 
+// Staged bf16 weight gradient (round 5; the bf16 mode's default where F_in, F_out % 128 == 0, no projected residual):
+// wgrad_x3_kernel's structure on bf16 operands, one product per pair instead of six. One 512-thread workgroup per
+// (row split, 128 x 384 output tile), one per CU; every 32-row step is staged once for the whole tile (A = dpre,
+// B = bf16(s_q Z_q) rounded as wgrad_bf16_kernel rounds it, 8 rows x 4 columns per thread) through buffer descriptors
+// two steps ahead, repacked into [k-group][column] units of 8 rows, double-buffered; wave w owns output rows
+// 64 (w & 1).. and columns 96 (w >> 1)... The workgroups of one row split (its 128 x 384 tiles) are numbered onto
+// one XCD at neighbouring times (blockIdx -> (split, tile), see wgrad_tile_of), so the tiles that read the same rows
+// share them through that XCD's L2. wgrad_bf16_kernel (128 x 128 tiles, one step of prefetch) re-read dpre once per
+// 128-column tile: 984 MB at F = 256 against the 656 MB here.
+constexpr int WB_K = 32;  // rows per step (4 k-groups of 8)
+
+__global__ __launch_bounds__(512, 1) void wgrad_bfs_kernel(WgradB p, int splits) {
+    __shared__ __attribute__((aligned(16))) uint4 U[2][4][WX_COLS];
+    __shared__ float Db[4][4][WX_BP];
+    __shared__ float Gs[2][3][WB_K];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, kh = lane >> 5;
+    const int n_tiles = p.N / WX_BN;
+    int split, tile;
+    wgrad_tile_of((int)blockIdx.x, (p.P / WX_BP) * n_tiles, splits, split, tile);
+    if (tile < 0) return;  // whole workgroup: no barrier reached
+    const int pt = tile / n_tiles, nt = tile % n_tiles;
+    const int64_t r0 = (int64_t)split * p.rows_per_split;
+    const int64_t rend = min(r0 + p.rows_per_split, p.M);
+    // staging role: waves 0-1 stage A (128 columns: 32 quads x 4 k-groups), waves 2-7 B (384 columns: 96 x 4); the
+    // wave index in a scalar register keeps the buffer descriptors wave-uniform
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const bool isA = wv < 2;
+    const int u = isA ? tid : tid - 128;
+    const int kg = isA ? (u >> 5) : (u / 96);
+    const int quad = isA ? (u & 31) : (u % 96);
+    const int col0 = (isA ? 0 : WX_BP) + 4 * quad;
+    const int gcol = isA ? WX_BP * pt + 4 * quad : WX_BN * nt + 4 * quad;
+    const int seg = isA ? 3 : gcol / p.F_in;
+    const uint16_t* src = isA ? p.A + WX_BP * pt : p.Z + WX_BN * nt;
+    const int64_t ld = isA ? p.lda : p.ldz;
+    const int gsel = seg < 3 ? seg : 0;
+    const bool gwriter = !isA && gcol % p.F_in == 0;
+    const int64_t nr64 = rend - r0;
+    const int nrows = __builtin_amdgcn_readfirstlane(nr64 > 0 ? (int)nr64 : 0);
+    const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(src + r0 * ld), 0, nrows * (int)ld * 2,
+                                                        0x00020000);
+    const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.gates + r0 * 4), 0, nrows * 16, 0x00020000);
+    const int ld2b = (int)ld * 2;
+    const int xoff = 8 * kg * ld2b + 8 * quad, goff = (8 * kg * 4 + gsel) * 4;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    auto load = [&](uint2 (&x)[8], float (&gq)[8], int step) {  // step < 2^31 / (32 ld) (host-checked)
+        const int sx = step * WB_K * ld2b, sg = step * WB_K * 16;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_x, xoff + sx + e * ld2b, 0, 0);
+            x[e] = make_uint2(v.x, v.y);
+            gq[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_g, goff + sg + e * 16, 0, 0));
+        }
+    };
+    float db[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) db[t][0] = db[t][1] = db[t][2] = db[t][3] = 0.f;
+    uint2 xa[8];  // A threads: the staged rows, kept for the bias sums after the barrier
+    auto pack_store = [&](const uint2 (&x)[8], const float (&gq)[8], int buf) {
+        uint32_t w[4][4];  // [column][row pair]
+        if (isA) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint2 r0v = x[2 * i], r1v = x[2 * i + 1];
+                w[0][i] = (r0v.x & 0xffffu) | (r1v.x << 16);
+                w[1][i] = (r0v.x >> 16) | (r1v.x & 0xffff0000u);
+                w[2][i] = (r0v.y & 0xffffu) | (r1v.y << 16);
+                w[3][i] = (r0v.y >> 16) | (r1v.y & 0xffff0000u);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xa[e] = x[e];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float f[2][4];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint2 v = x[2 * i + h];
+                    const float s = gq[2 * i + h];
+                    f[h][0] = __fmul_rn(pgbf::lo(v.x), s);
+                    f[h][1] = __fmul_rn(pgbf::hi(v.x), s);
+                    f[h][2] = __fmul_rn(pgbf::lo(v.y), s);
+                    f[h][3] = __fmul_rn(pgbf::hi(v.y), s);
+                }
+                float d0, d1;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) w[c][i] = pgx3::bf2(f[0][c], f[1][c], d0, d1);  // RNE, as f2bf
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) U[buf][kg][col0 + c] = make_uint4(w[c][0], w[c][1], w[c][2], w[c][3]);
+        if (gwriter) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Gs[buf][seg][8 * kg + e] = gq[e];
+        }
+    };
+    auto bias_step = [&](int cur) {  // A threads, after the barrier: the step's rows in order
+        if (!isA) return;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int row = 8 * kg + e;
+            const float sv[4] = {Gs[cur][0][row], Gs[cur][1][row], Gs[cur][2][row], 1.f};
+            const float f[4] = {pgbf::lo(xa[e].x), pgbf::hi(xa[e].x), pgbf::lo(xa[e].y), pgbf::hi(xa[e].y)};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) db[t][c] += sv[t] * f[c];
+        }
+    };
+    if (tid < 2 * 3 * WB_K) (&Gs[0][0][0])[tid] = 0.f;
+    f32x16 acc[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const int ih = wave & 1, jq = wave >> 1;
+    auto mfma_step = [&](int cur) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {  // k-groups 2 ks + kh
+            const int g = 2 * ks + kh;
+            uint4 a[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = U[cur][g][64 * ih + 32 * i + li];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint4 b = U[cur][g][WX_BP + 96 * jq + 32 * j + li];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][j] = mfma32_bf(a[i], b, acc[i][j]);
+            }
+        }
+    };
+    uint2 x0[8], x1[8];
+    float g0[8], g1[8];
+    const int64_t nsteps = (rend - r0 + WB_K - 1) / WB_K;
+    __syncthreads();  // Gs zeroed
+    // loads and packs unconditional (past the last step: zero rows), as in wgrad_x3_kernel
+    load(x0, g0, 0);
+    load(x1, g1, 1);
+    pack_store(x0, g0, 0);
+    __syncthreads();
+    for (int t = 0; t < (int)nsteps; t += 2) {
+        bias_step(0);
+        load(x0, g0, t + 2);
+        mfma_step(0);
+        pack_store(x1, g1, 1);
+        __syncthreads();
+        bias_step(1);
+        load(x1, g1, t + 3);
+        if (t + 1 < nsteps) mfma_step(1);
+        pack_store(x0, g0, 0);
+        __syncthreads();
+    }
+    float* out = p.part + (int64_t)split * p.part_stride;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int oi = WX_BP * pt + 64 * ih + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
+                const int oj = WX_BN * nt + 96 * jq + 32 * j + li;
+                out[(int64_t)oi * p.N + oj] = acc[i][j][r];
+            }
+    if (isA) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) Db[kg][t][4 * quad + c] = db[t][c];
+    }
+    __syncthreads();
+    {
+        const int t = tid >> 7, c = tid & 127;  // 4 x 128 sums, k-groups in fixed order
+        const int first = t * p.F_in;
+        const bool mine = t == 3 ? nt == 0 : (first >= WX_BN * nt && first < WX_BN * (nt + 1));
+        if (mine) out[(int64_t)p.P * p.N + t * p.P + WX_BP * pt + c] = ((Db[0][t][c] + Db[1][t][c]) + Db[2][t][c]) + Db[3][t][c];
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Any-shape path (F_in / F_out not multiples of 4, unaligned or odd leading dimensions): the same outputs as
 // dgrad_kernel + wgrad_kernel from plain per-element loops. Sums run in another order (within fp32 rounding of
@@ -2051,8 +2244,9 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
         w.part_stride = pl.part_stride;
         w.part = part;
         if (x3w) {
-            hipLaunchKernelGGL(wgrad_x3_kernel, dim3((unsigned)pl.splits, (unsigned)((F_out / WX_BP) * (K / WX_BN))),
-                               dim3(512), 0, s, w);
+            const int tiles = (F_out / WX_BP) * (K / WX_BN);
+            hipLaunchKernelGGL(wgrad_x3_kernel, dim3((unsigned)(8 * ((pl.splits + 7) / 8) * tiles)), dim3(512), 0, s, w,
+                               (int)pl.splits);
         } else {
             dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
             hipLaunchKernelGGL((wgrad_kernel<WG_NW>), grid, dim3(64 * WG_NW), 0, s, w);
@@ -2138,7 +2332,12 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
     PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
     PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
     const bool proj = a->W_res != nullptr;
-    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj);
+    // the staged weight gradient (wgrad_bfs_kernel) where its tiles fit; PG_FLAG_WGRAD_BF16_TILED keeps the 128 x 128
+    // tiles of wgrad_bf16_kernel
+    const bool bfs = wgrad_x3_shape(a->F_in, a->F_out, proj) && !(flags & PG_FLAG_WGRAD_BF16_TILED) &&
+                     a->ldz % 4 == 0 && g->ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(a->Z) & 7) == 0 &&
+                     (reinterpret_cast<uintptr_t>(g->dpre) & 7) == 0;
+    const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj, bfs);
     PG_REQUIRE(g->work_floats >= pl.total, "workspace too small");
     const uint16_t* Zb = reinterpret_cast<const uint16_t*>(a->Z);
     const uint16_t* Yb = reinterpret_cast<const uint16_t*>(a->Y);
@@ -2226,8 +2425,14 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         w.rows_per_split = pl.rows_per_split;
         w.part_stride = pl.part_stride;
         w.part = part;
-        dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
-        hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(512), 0, s, w);
+        if (bfs) {
+            const int tiles = (F_out / WX_BP) * (K / WX_BN);
+            const unsigned nb = (unsigned)(8 * ((pl.splits + 7) / 8) * tiles);
+            hipLaunchKernelGGL(wgrad_bfs_kernel, dim3(nb), dim3(512), 0, s, w, (int)pl.splits);
+        } else {
+            dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
+            hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(512), 0, s, w);
+        }
     }
     launch_reduce(pl.part_stride / 4, pl.splits, pl.part_stride, part, g->dW, s);
     return pg::check_launch("pg_directgcn_dense_bwd_bf16");

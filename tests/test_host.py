@@ -1,5 +1,6 @@
 """CPU-side tests (no GPU): C-ABI library loads and exports the header's symbols; host graph logic;
 drop-in surface (init, state_dict keys, errors); no CPU fallback in the product path."""
+import ctypes
 import os
 import re
 
@@ -35,6 +36,28 @@ def test_abi_argument_errors_without_gpu(pkg):
     assert rc == -1
     rc = lib.pg_spmm3_f32(0, None, None, None, None, 4, 4, None, 8, 0, None)
     assert rc == -1 and b"ldz" in lib.pg_last_error()
+
+
+def test_training_abi_shape_gates_without_gpu(pkg):
+    """The round-5 training entry points decide what they take before any HIP call: the head kernel's workspace
+    (F = 128, H = 64, C <= 32 only; -1 declines, and the trainer runs the framework ops), its argument errors, and the
+    dense backward workspace, which covers both weight-gradient plans (staged 128 x 384 tiles and 128 x 128 tiles)."""
+    from protgram_directgcn_amd import _lib
+    lib = pkg.load_library()
+    assert lib.pg_head_train_workspace(160000, 128, 64, 20) > 0
+    assert lib.pg_head_train_workspace(0, 128, 64, 20) > 0  # one (empty) partial
+    for shape in ((160000, 256, 128, 20), (1000, 128, 32, 20), (1000, 128, 64, 40), (-1, 128, 64, 20)):
+        assert lib.pg_head_train_workspace(*shape) == -1, shape
+    def call(F, H):  # h, ldh, W1, b1, W2, b2, y, weight, p, seed, scale, dh, lddh, grads, loss, work, n, stream
+        return lib.pg_head_train_f32(10, F, H, 20, None, F, None, None, None, None, None, 1.0, 0.0, None, None, None, F,
+                                     None, None, None, 0, None)
+    assert call(256, 128) == _lib.PG_ERR_UNSUPPORTED and b"F = 128" in lib.pg_last_error()
+    assert call(128, 64) == -1 and b"null" in lib.pg_last_error()
+    a = _lib.LayerArgs()
+    a.M, a.F_in, a.F_out = 160000, 256, 256
+    staged = lib.pg_directgcn_dense_bwd_workspace(ctypes.byref(a))
+    a.F_in = 96  # no staged tiles: the 128 x 128-tile plan alone
+    assert staged > 0 and lib.pg_directgcn_dense_bwd_workspace(ctypes.byref(a)) > 0
 
 
 def _closed_form(raw: np.ndarray, nn: np.ndarray, rowptr: np.ndarray, eps=np.float32(1e-9)):

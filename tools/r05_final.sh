@@ -7,7 +7,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-O=gpurun_out/r05f1
+O=gpurun_out/${R05_TAG:-r05f1}
 PART=${1:-all}
 if [ "$PART" != "2" ]; then
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > ${O}_smoke.log 2>&1 || { tail -30 ${O}_smoke.log; exit 1; }

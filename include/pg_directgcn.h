@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 1
+#define PG_ABI_VERSION 2  /* 2: pg_layer_args_t gained drop_p / drop_seed (fused layer dropout) */
 
 #define PG_OK 0
 #define PG_ERR_ARG (-1)
@@ -180,6 +180,11 @@ typedef struct pg_layer_args {
     const float* W_res; const float* b_res;
     int32_t act; float slope;
     float* Y; int64_t ldy;
+    /* Fused layer dropout (the F.dropout after each layer, protgram_directgcn.py:216), applied after the activation
+     * by the dense forward: output element m * F_out + j is kept when a counter-based hash of (*drop_seed, index)
+     * passes p, and scaled by 1 / (1 - p). drop_p = 0: none. Needs act. The dense backward takes the same drop_p and
+     * recovers the mask from the stored output Y (drop_seed is not read there). */
+    float drop_p; const int64_t* drop_seed;
 } pg_layer_args_t;
 
 /* Number of floats of the packed operand: B = [W_mi+W_s | W_mo+W_s | W_u+W_s (| W_res)] as [F_out, K]

@@ -56,7 +56,8 @@ class LayerArgs(ctypes.Structure):
                 ("res_x", c_vp), ("ld_res", c_i64),
                 ("W_res", c_vp), ("b_res", c_vp),
                 ("act", c_i32), ("slope", c_f32),
-                ("Y", c_vp), ("ldy", c_i64)]
+                ("Y", c_vp), ("ldy", c_i64),
+                ("drop_p", c_f32), ("drop_seed", c_vp)]
 
 
 class LayerGradArgs(ctypes.Structure):
@@ -172,7 +173,7 @@ def load_library():
         if fn is None:
             raise NativeLibraryError(f"{_LIB_PATH} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.pg_abi_version() != 1:
+    if lib.pg_abi_version() != 2:
         raise NativeLibraryError("ABI version mismatch")
     _lib = lib
     return lib

@@ -199,6 +199,9 @@ struct DenseB {
     uint16_t* Y;
     int64_t ldy;
     int remap;
+    uint32_t drop_thr;  // fused layer dropout (pg_dense.hip DenseP::drop_*)
+    float drop_s;
+    const int64_t* drop_seed;
 };
 
 __device__ __forceinline__ float4 ld4f(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -206,6 +209,7 @@ __device__ __forceinline__ float4 ld4f(const float* p) { return *reinterpret_cas
 template <int BM, int BN, int NW>
 __global__ __launch_bounds__(64 * NW) void dense_bf16_kernel(DenseB p) {
     constexpr int NT = 64 * NW;
+    const uint64_t dseed = p.drop_s != 0.f ? (uint64_t)*p.drop_seed : 0ull;
     constexpr int WN = 2, WM = NW / WN;
     constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
     static_assert(TM >= 1 && TN >= 1, "wave tile");
@@ -387,6 +391,8 @@ __global__ __launch_bounds__(64 * NW) void dense_bf16_kernel(DenseB p) {
         for (int e = 0; e < 4; ++e) {
             float y = o[e] + (sg[0] * b0[e] + sg[1] * b1[e] + sg[2] * b2[e]) + br[e] + cc[e] + rr[e];
             if (p.act) y = y > 0.f ? y : y * p.slope;
+            if (p.drop_s != 0.f)
+                y = (pg::drop_hash(dseed, (uint32_t)(m * p.F_out + nb + e)) >> 8) >= p.drop_thr ? y * p.drop_s : 0.f;
             o[e] = y;
         }
         *reinterpret_cast<uint2*>(p.Y + m * p.ldy + nb) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
@@ -476,6 +482,9 @@ int pg_directgcn_dense_bf16(const pg_layer_args_t* a, const float* packed, const
     p.Y = Yb;
     p.ldy = a->ldy;
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+    if (const int rc = pg::drop_params(a, p.drop_thr, p.drop_s)) return rc;
+    p.drop_seed = a->drop_seed;
+    PG_REQUIRE(p.drop_s == 0.f || a->M * a->F_out <= (int64_t(1) << 32), "fused dropout: M * F_out > 2^32");
     constexpr int BM = 128, BN = 128, NW = 8;
     const int64_t nb = ((p.M + BM - 1) / BM) * ((p.F_out + BN - 1) / BN);
     hipLaunchKernelGGL((dense_bf16_kernel<BM, BN, NW>), dim3((unsigned)nb), dim3(64 * NW), 0, (hipStream_t)stream, p);

@@ -44,6 +44,44 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     return tiny ? y * 0x1p-32f : y;
 }
 
+// Layer-output dropout fused into the dense epilogue (the F.dropout after every layer, protgram_directgcn.py:216):
+// element e = m * F_out + j of the layer output is kept when (drop_hash(seed, e) >> 8) >= thr, thr = p * 2^24
+// rounded, and a kept element is scaled by 1 / (1 - p). Counter-based (murmur3's 32-bit finalizer of the index
+// mixed with the device seed): nothing is stored, and the backward needs no draw at all (act_grad).
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint32_t e) {
+    uint32_t x = (e * 0x9E3779B1u + (uint32_t)seed) ^ (uint32_t)(seed >> 32);
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
+
+// Gradient through the layer's leaky_relu (slope) and, when ds != 0, the fused dropout after it (scale ds = 1/(1-p)),
+// from the stored layer output y: a kept element of a leaky_relu output is nonzero (its sign is the pre-activation's),
+// a dropped one is 0. ds == 0: leaky_relu' alone, y > 0 ? d : d * slope. (An exactly-zero pre-activation that was kept
+// reads as dropped: its gradient is 0 instead of d * ds * slope.)
+__device__ __forceinline__ float act_grad(float d, float y, float slope, float ds) {
+    if (ds == 0.f) return y > 0.f ? d : d * slope;
+    const float e = d * ds;
+    return y > 0.f ? e : (y < 0.f ? e * slope : 0.f);
+}
+
+// Host side of the fused dropout: threshold and scale from args->drop_p (0 <= p < 1; p == 0: off). Fused dropout
+// needs the activation (act_grad recovers the mask from the sign of the output) and, in the forward, a device seed.
+inline int drop_params(const pg_layer_args_t* a, uint32_t& thr, float& scale, bool need_seed = true) {
+    thr = 0;
+    scale = 0.f;
+    if (a->drop_p == 0.f) return PG_OK;
+    if (!(a->drop_p > 0.f && a->drop_p < 1.f) || !a->act || (need_seed && !a->drop_seed))
+        return set_error(PG_ERR_ARG, "fused dropout needs 0 <= drop_p < 1, act and drop_seed (drop_p = %g)",
+                         (double)a->drop_p);
+    thr = (uint32_t)((double)a->drop_p * 16777216.0 + 0.5);
+    scale = (float)(1.0 / (1.0 - (double)a->drop_p));
+    return PG_OK;
+}
+
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(PG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));

@@ -70,7 +70,21 @@ struct DenseP {
     int nt_a;  // pipelined kernels: A rows and the per-node constant (read once) by non-temporal LDS-DMA
                // (PG_FLAG_DENSE_A_CACHED clears)
     int exp;  // diagnostics build only (PG_DENSE_EXP, tools/dense_exp.py): phases skipped in dense_x3p_kernel
+    // fused layer dropout after the activation (drop_s = 1 / (1 - p); 0: none): pg::drop_hash of (*drop_seed, the
+    // element's index m * F_out + j over the launch's rows) against drop_thr
+    uint32_t drop_thr;
+    float drop_s;
+    const int64_t* drop_seed;
 };
+
+// the fused dropout of output element (m, j) on an activated value y (DenseP::drop_*)
+__device__ __forceinline__ float drop_apply(const DenseP& p, uint64_t seed, int64_t m, int j, float y) {
+    const uint32_t e = (uint32_t)(m * p.F_out + j);
+    return (pg::drop_hash(seed, e) >> 8) >= p.drop_thr ? y * p.drop_s : 0.f;
+}
+__device__ __forceinline__ uint64_t drop_seed_of(const DenseP& p) {
+    return p.drop_s != 0.f ? (uint64_t)*p.drop_seed : 0ull;
+}
 
 // Diagnostics build only: dense_x3p_kernel timing experiments, flag bits 24..28 (bit 0: no MFMAs, 1: no split,
 // 2: no Y stores, 3: no A DMA, 4: no constant / residual DMA). Results are garbage in those runs.
@@ -123,6 +137,7 @@ __device__ __forceinline__ float a_elem(const DenseP& p, const float* sg, int64_
 template <int BM, int BN, int NW, bool VEC>
 __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
     constexpr int NT = 64 * NW;  // threads
+    const uint64_t dseed = drop_seed_of(p);
     constexpr int WN = (BM == 64 && NW == 8) ? 4 : (BN == 128 || BM == 64 || NW == 8) ? 2 : 1;
     constexpr int WM = NW / WN;
     static_assert(BM / WM >= 32 && BN / WN >= 32, "wave tile too small");
@@ -362,6 +377,7 @@ __global__ __launch_bounds__(64 * NW) void dense_kernel(DenseP p) {
             for (int e = 0; e < 4; ++e) {
                 float y = o[e] + (sg[0] * bb0[e] + sg[1] * bb1[e] + sg[2] * bb2[e]) + bbr[e] + cc[e] + rr[e];
                 if (p.act) y = y > 0.f ? y : y * p.slope;
+                if (p.drop_s != 0.f) y = drop_apply(p, dseed, mm[u], nb + e, y);
                 o[e] = y;
             }
             if (vec_out) {
@@ -504,6 +520,7 @@ __device__ __forceinline__ int a_unit(int s, int r, int g) { return 128 * s + 4 
 template <int F_IN, int KSEG, bool PRE>
 __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
     constexpr int K = F_IN * KSEG;
+    const uint64_t dseed = drop_seed_of(p);
     constexpr int CH = K / 4;     // fp32 16-B chunks per row
     constexpr int NU = K / 8;     // bf16 16-B units per row (one MFMA operand of one lane for one k step)
     constexpr int NS = K / 32;    // MFMA k steps
@@ -749,6 +766,7 @@ __global__ __launch_bounds__(512) void dense_x3_kernel(DenseP p) {
             for (int e = 0; e < 4; ++e) {
                 const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                 y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
+                if (p.drop_s != 0.f) y[e] = drop_apply(p, dseed, m0 + rl, 4 * ej + e, y[e]);
             }
             *reinterpret_cast<float4*>(p.Y + (m0 + rl) * p.ldy + 4 * ej) = make_float4(y[0], y[1], y[2], y[3]);
         }
@@ -799,7 +817,8 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     const int wave = tid >> 6, lane = tid & 63;
     const int lc = lane & 15, kg = lane >> 4;
     const int col = 16 * wave + lc;
-    const bool mfma_first = wave < 4;  // waves w and w + 4 share a SIMD
+    const bool mfma_first = wave < 4;
+    const uint64_t dseed = drop_seed_of(p);  // waves w and w + 4 share a SIMD
     const int64_t T = (p.M + BM - 1) / BM;
     DSTAMP_INIT;
     {
@@ -1058,6 +1077,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                 for (int e = 0; e < 4; ++e) {
                     const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                     y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
+                    if (p.drop_s != 0.f) y[e] = drop_apply(p, dseed, m0 + er, 4 * ej + e, y[e]);
                 }
                 if (!DEXP(2)) {
                     const int64_t yr = p.map_y ? ngram_row(p, m0 + er) : m0 + er;
@@ -1184,6 +1204,9 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
     p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
     p.pregated = (flags & PG_FLAG_DENSE_PREGATED) ? 1 : 0;
     p.nt_a = (flags & PG_FLAG_DENSE_A_CACHED) ? 0 : 1;
+    if (const int rc = pg::drop_params(a, p.drop_thr, p.drop_s)) return rc;
+    p.drop_seed = a->drop_seed;
+    PG_REQUIRE(p.drop_s == 0.f || a->M * a->F_out <= (int64_t(1) << 32), "fused dropout: M * F_out > 2^32");
 #ifdef PG_DENSE_EXP
     p.exp = (int)((flags >> 24) & 31u);
 #endif

@@ -64,6 +64,7 @@ struct DgradP {
     int64_t ldy;
     int act;
     float slope;
+    float drop_s;       // fused layer dropout's scale (pg::act_grad), 0: none
     const float* BT;    // [N, F_out]
     const float* bsum;  // [4, F_out]
     const float* Z;
@@ -168,10 +169,10 @@ __global__ __launch_bounds__(64 * NW) void dgrad_kernel(DgradP p) {
             float4 d = ra[q];
             if (p.act) {
                 const float4 y = ry[q];
-                d.x = y.x > 0.f ? d.x : d.x * p.slope;
-                d.y = y.y > 0.f ? d.y : d.y * p.slope;
-                d.z = y.z > 0.f ? d.z : d.z * p.slope;
-                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+                d.x = pg::act_grad(d.x, y.x, p.slope, p.drop_s);
+                d.y = pg::act_grad(d.y, y.y, p.slope, p.drop_s);
+                d.z = pg::act_grad(d.z, y.z, p.slope, p.drop_s);
+                d.w = pg::act_grad(d.w, y.w, p.slope, p.drop_s);
             }
             if (k >= p.F_out) d = make_float4(0.f, 0.f, 0.f, 0.f);
             if (lead && k < p.F_out && m < p.M) {
@@ -431,10 +432,10 @@ __global__ __launch_bounds__(64 * NW, 3) void dgrad_x3_kernel(DgradP p, const ui
             float4 d = ra[q];
             if (p.act) {
                 const float4 y = ry[q];
-                d.x = y.x > 0.f ? d.x : d.x * p.slope;
-                d.y = y.y > 0.f ? d.y : d.y * p.slope;
-                d.z = y.z > 0.f ? d.z : d.z * p.slope;
-                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+                d.x = pg::act_grad(d.x, y.x, p.slope, p.drop_s);
+                d.y = pg::act_grad(d.y, y.y, p.slope, p.drop_s);
+                d.z = pg::act_grad(d.z, y.z, p.slope, p.drop_s);
+                d.w = pg::act_grad(d.w, y.w, p.slope, p.drop_s);
             }
             if (k >= p.F_out) d = make_float4(0.f, 0.f, 0.f, 0.f);
             if (lead && k < p.F_out && m < p.M) {
@@ -696,10 +697,10 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
             float4 d = ra[q];
             if (p.act) {
                 const float4 y = ry[q];
-                d.x = y.x > 0.f ? d.x : d.x * p.slope;
-                d.y = y.y > 0.f ? d.y : d.y * p.slope;
-                d.z = y.z > 0.f ? d.z : d.z * p.slope;
-                d.w = y.w > 0.f ? d.w : d.w * p.slope;
+                d.x = pg::act_grad(d.x, y.x, p.slope, p.drop_s);
+                d.y = pg::act_grad(d.y, y.y, p.slope, p.drop_s);
+                d.z = pg::act_grad(d.z, y.z, p.slope, p.drop_s);
+                d.w = pg::act_grad(d.w, y.w, p.slope, p.drop_s);
             }
             if (lead && m < p.M) {
                 st4(p.dpre + m * p.ldp + k, d);
@@ -1291,6 +1292,7 @@ struct DgradB {
     int64_t ldy;
     int act;
     float slope;
+    float drop_s;        // fused layer dropout's scale (pg::act_grad), 0: none
     const uint16_t* BT;  // [N, F_out] bf16
     const float* bsum;   // [4, F_out]
     const uint16_t* Z;
@@ -1406,7 +1408,7 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
                     float y[8];
                     unpack8(ry[q], y);
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) d[e] = y[e] > 0.f ? d[e] : d[e] * p.slope;
+                    for (int e = 0; e < 8; ++e) d[e] = pg::act_grad(d[e], y[e], p.slope, p.drop_s);
                 }
                 v = pack8(d);
                 if (lead && m < p.M) {
@@ -1949,7 +1951,7 @@ __global__ __launch_bounds__(256) void dgrad_generic_kernel(DgradP p) {
         float ds[3] = {0.f, 0.f, 0.f};
         for (int o = tid; o < p.F_out; o += 256) {
             float d = p.dY[m * p.lddy + o];
-            if (p.act) d = p.Y[m * p.ldy + o] > 0.f ? d : d * p.slope;
+            if (p.act) d = pg::act_grad(d, p.Y[m * p.ldy + o], p.slope, p.drop_s);
             dp[o] = d;
             p.dpre[m * p.ldp + o] = d;
 #pragma unroll
@@ -2087,6 +2089,9 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
     PG_REQUIRE(g->dY && g->dpre && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
     PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
     PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
+    uint32_t drop_thr = 0;
+    float drop_s = 0.f;
+    if (const int rc = pg::drop_params(a, drop_thr, drop_s, false)) return rc;
     const bool proj = a->W_res != nullptr;
     const bool x3w = wgrad_x3_shape(a->F_in, a->F_out, proj) && !(flags & PG_FLAG_WGRAD_F32MFMA);
     const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj, x3w);
@@ -2146,6 +2151,7 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
         p.ldy = a->ldy;
         p.act = a->act;
         p.slope = a->slope;
+        p.drop_s = drop_s;
         p.BT = BT;
         p.bsum = packed + (int64_t)F_out * K;
         p.Z = a->Z;
@@ -2198,6 +2204,7 @@ int dense_bwd_f32_impl(const pg_layer_args_t* a, const float* packed, const pg_l
         p.ldy = a->ldy;
         p.act = a->act;
         p.slope = a->slope;
+        p.drop_s = drop_s;
         p.BT = BT;
         p.bsum = packed + (int64_t)F_out * K;
         p.Z = a->Z;
@@ -2331,6 +2338,9 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
     PG_REQUIRE(g->dY && g->dpre && g->dgate && g->gates && g->dW && g->work, "null gradient buffer");
     PG_REQUIRE(!a->act || a->Y, "act needs the forward output Y");
     PG_REQUIRE(!a->W_res || g->dres, "W_res needs dres");
+    uint32_t drop_thr = 0;
+    float drop_s = 0.f;
+    if (const int rc = pg::drop_params(a, drop_thr, drop_s, false)) return rc;
     const bool proj = a->W_res != nullptr;
     // the staged weight gradient (wgrad_bfs_kernel) where its tiles fit; PG_FLAG_WGRAD_BF16_TILED keeps the 128 x 128
     // tiles of wgrad_bf16_kernel
@@ -2388,6 +2398,7 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         p.ldy = a->ldy;
         p.act = a->act;
         p.slope = a->slope;
+        p.drop_s = drop_s;
         p.BT = BT;
         p.bsum = packed + (int64_t)F_out * K;
         p.Z = Zb;

@@ -132,8 +132,12 @@ class DirectGCNLayer(nn.Module):
                 self.bias_undirected, self.bias_undirected_shared, *C)
 
     def fused_forward(self, x, graph, original_indices=None, res_x=None, W_res=None, b_res=None, act=False,
-                      fused_norm: bool = False):
-        """Layer output (+ optional residual and leaky_relu) from a prepared CSRGraph."""
+                      fused_norm: bool = False, drop=None):
+        """Layer output (+ optional residual and leaky_relu) from a prepared CSRGraph. drop = (p, seed): the dropout
+        the model applies to the layer's output (protgram_directgcn.py:216), fused into the dense epilogue (act only;
+        seed a device int64 [1])."""
+        if drop is not None and not act:
+            raise ValueError("fused dropout needs the activation")
         M = x.size(0)
         rows = None
         if self.use_vector_coeffs:
@@ -158,15 +162,15 @@ class DirectGCNLayer(nn.Module):
             Z = ops.spmm3_gated(graph, x, prm, gate_mode)
             if Z is not None:
                 return ops.layer_dense(Z, prm, gate_mode, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
-                                       act=act, pregated=True)
+                                       act=act, pregated=True, drop=drop)
         if (ops.SPAN_BACKWARD and torch.is_grad_enabled() and x.requires_grad
                 and ops.PropagateDense.supports(graph, x, self.out_channels, res_x, W_res, rows, fused_norm)):
             # training through a layer whose input needs its gradient: the input's whole gradient (diagonal term and
             # identity residual from the dense backward, off-diagonal part accumulated into it) in two launches
             return ops.PropagateDense.apply(x, graph, res_x is not None, constant, gate_mode, act, ops.LEAKY_SLOPE,
-                                            *params)
+                                            drop, *params)
         Z = ops.Propagate3.apply(x, graph, fused_norm)
-        return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, gate_mode, act, ops.LEAKY_SLOPE,
+        return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, gate_mode, act, ops.LEAKY_SLOPE, drop,
                                     *params)
 
     def forward(self, x: torch.Tensor,
@@ -266,13 +270,22 @@ class ProtGramDirectGCN(nn.Module):
             h = h.to(torch.bfloat16)
         elif self.compute_dtype != torch.float32:
             raise ValueError("compute_dtype must be torch.float32 or torch.bfloat16")
-        for conv, res in zip(self.convs, self.res_projs):
+        # the dropout after each layer: fused into the dense epilogue (ops.FUSED_DROPOUT; one device draw of the
+        # layers' seeds per forward), else F.dropout
+        p = float(self.dropout) if self.training else 0.0
+        seeds = None
+        if ops.FUSED_DROPOUT and 0.0 < p < 1.0:
+            seeds = torch.randint(0, 1 << 62, (len(self.convs),), device=x.device, dtype=torch.int64)
+        for i, (conv, res) in enumerate(zip(self.convs, self.res_projs)):
+            drop = (p, seeds[i:i + 1]) if seeds is not None else None
             if isinstance(res, nn.Linear):
                 h = conv.fused_forward(h, g, original_indices, res_x=h, W_res=res.weight, b_res=res.bias, act=True,
-                                       fused_norm=self.fused_norm)
+                                       fused_norm=self.fused_norm, drop=drop)
             else:
-                h = conv.fused_forward(h, g, original_indices, res_x=h, act=True, fused_norm=self.fused_norm)
-            h = F.dropout(h, p=self.dropout, training=self.training)
+                h = conv.fused_forward(h, g, original_indices, res_x=h, act=True, fused_norm=self.fused_norm,
+                                       drop=drop)
+            if drop is None:
+                h = F.dropout(h, p=self.dropout, training=self.training)
         return h
 
     def head_train_args(self):

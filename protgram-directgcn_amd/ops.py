@@ -21,6 +21,11 @@ from .graph import CSRGraph, ShapedAdjacency
 
 LEAKY_SLOPE = 0.01  # F.leaky_relu default, protgram_directgcn.py:215
 
+# training-mode dropout after each layer (protgram_directgcn.py:216) fused into the dense epilogue: a counter-based
+# draw (pg::drop_hash) instead of a separate dropout pass and its mask; the backward reads the mask off the layer
+# output. False: F.dropout (torch's generator stream).
+FUSED_DROPOUT = True
+
 # training on complete n-gram graphs: PropagateDense (the span dense backward + the off-diagonal transposed kernel)
 # for layers whose input needs its gradient; False: Propagate3 + LayerDense (the 4x4-block transposed kernel)
 SPAN_BACKWARD = True
@@ -611,9 +616,9 @@ _PACK_KEYS = ("W_main_in", "W_main_out", "W_undirected", "W_shared", "b_main_in"
 
 
 def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None,
-                act: bool = False, slope: float = LEAKY_SLOPE, Y=None, M: Optional[int] = None):
+                act: bool = False, slope: float = LEAKY_SLOPE, Y=None, M: Optional[int] = None, drop=None):
     """pg_layer_args_t for the forward block; returns (args, keep-alive list). Z=None (gate-only uses) takes the
-    row count from M."""
+    row count from M. drop = (p, seed): the fused layer dropout (seed: device int64 [1]; None in the backward)."""
     if Z is None:
         M, F_in = int(M), prm["W_main_in"].size(1)
     else:
@@ -647,6 +652,13 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
         a.res_x, a.ld_res = _p(rx), rx.stride(0)
     a.W_res = c(W_res)
     a.act, a.slope = int(bool(act)), float(slope)
+    if drop is not None and drop[0] > 0:
+        a.drop_p = float(drop[0])
+        if drop[1] is not None:
+            if drop[1].dtype != torch.int64 or not drop[1].is_cuda or drop[1].numel() < 1:
+                raise ValueError("the dropout seed must be a device int64 tensor")
+            keep.append(drop[1])
+            a.drop_seed = _p(drop[1])
     if Y is not None:
         Yc = Y.detach().contiguous()
         keep.append(Yc)
@@ -656,17 +668,19 @@ def _layer_args(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
 
 def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
                 act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                out: Optional[torch.Tensor] = None, pregated: bool = False, packs: Optional[list] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, pregated: bool = False, packs: Optional[list] = None,
+                drop=None) -> torch.Tensor:
     """pg_directgcn_dense_f32: gated contraction of the aggregates + epilogue (see the header). bf16 Z ->
     pg_directgcn_dense_bf16 (bf16 output; `packs`, when given, receives its packed weights (fp32, bf16) so that the
-    backward of the same step reuses them)."""
+    backward of the same step reuses them). drop = (p, seed [1] int64 on the device): the layer's dropout after the
+    activation, fused into the epilogue (pg::drop_hash; act required)."""
     lib = load_library()
     _require_gpu(Z)
     if _is_bf16(Z):
-        Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs)
+        Y = _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs, drop)
         if Y is None:
             Y = layer_dense(Z.float(), prm, gate_mode, rows, constant, None if res_x is None else res_x.float(),
-                            W_res, b_res, act, slope, flags).to(torch.bfloat16)
+                            W_res, b_res, act, slope, flags, drop=drop).to(torch.bfloat16)
         if out is not None:
             out.copy_(Y)
             return out
@@ -679,7 +693,7 @@ def layer_dense(Z, prm: dict, gate_mode: int, rows=None, constant=None, res_x=No
         Y = out
     else:
         Y = torch.empty(M, F_out, device=Z.device, dtype=torch.float32)
-    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope, drop=drop)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
     if pregated:
@@ -748,7 +762,8 @@ def layer_dense_ngram_rows(Z, prm: dict, gate_mode: int, Kn1: int, m0: int, cons
     return Y
 
 
-def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs=None):
+def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope, flags, packs=None,
+                      drop=None):
     lib = load_library()
     packed, p16 = pack_weights_bf16(prm, W_res, b_res)
     if packs is not None:
@@ -756,7 +771,7 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
     M = Z.size(0)
     F_out = prm["W_main_in"].size(0)
     Y = torch.empty(M, F_out, device=Z.device, dtype=torch.bfloat16)
-    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, constant, res_x, W_res, act, slope, drop=drop)
     a.Y, a.ldy = _p(Y), Y.stride(0)
     fl = default_flags() if flags is None else flags
     ev = _ev_start(Z, "DENSE")
@@ -771,7 +786,8 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
 
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
                          act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
-                         need_dZ: bool = True, packs: Optional[list] = None, span: Optional[tuple] = None):
+                         need_dZ: bool = True, packs: Optional[list] = None, span: Optional[tuple] = None,
+                         drop_p: float = 0.0):
     """pg_directgcn_dense_bwd_f32 (any shape; bf16 operands: pg_directgcn_dense_bwd_bf16, None when F_in / F_out
     are not multiples of 8 -- the caller then runs the fp32 kernels on widened copies). Returns a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
@@ -779,7 +795,8 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
       dB [F_out, K] (grad of the packed segment weights W_main_q + W_shared, W_res), dbsum [4, F_out].
     packs: the bf16 forward's packed weights of the same parameters (LayerDense: saved by its forward), else packed
     here. span = (wdiag [M, 3], e_res): pg_directgcn_dense_bwd_span_f32 (fp32 only), which also returns
-    E [M, F_in] = sum_q wdiag[:, q] dZ_q (+ dpre when e_res); None when it does not take the shape."""
+    E [M, F_in] = sum_q wdiag[:, q] dZ_q (+ dpre when e_res); None when it does not take the shape.
+    drop_p: the forward's fused dropout (Y is its output; the mask is read off Y, pg::act_grad)."""
     lib = load_library()
     _require_gpu(dY, Z, Y)
     M, F_in = Z.size(0), Z.size(1) // 3
@@ -792,7 +809,8 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
         Y = _bf16c(Y)
     else:
         packed = pack_weights(prm, W_res, b_res)
-    a, keep = _layer_args(Z, prm, gate_mode, rows, None, res_x, W_res, act, slope, Y=Y)
+    a, keep = _layer_args(Z, prm, gate_mode, rows, None, res_x, W_res, act, slope, Y=Y,
+                          drop=(drop_p, None) if drop_p else None)
     dev = Z.device
     K = (4 if W_res is not None else 3) * F_in
     act_dt = torch.bfloat16 if bf else torch.float32
@@ -994,14 +1012,15 @@ class LayerDense(torch.autograd.Function):
 
     @staticmethod
     @_fwd32
-    def forward(ctx, Z, res_x, constant, W_res, b_res, rows, gate_mode, act, slope, *params):
+    def forward(ctx, Z, res_x, constant, W_res, b_res, rows, gate_mode, act, slope, drop, *params):
         prm = dict(zip(_DENSE_KEYS, params))
         # the bf16 kernels' packed weights are kept for the backward (the parameters are saved tensors: autograd
         # refuses a backward after an in-place change to them, so the packed copies cannot go stale before it)
         ctx.packs = []
         Y = layer_dense(Z, prm, gate_mode, rows=rows, constant=constant, res_x=res_x, W_res=W_res, b_res=b_res,
-                        act=act, slope=slope, packs=ctx.packs)
+                        act=act, slope=slope, packs=ctx.packs, drop=drop)
         ctx.gate_mode, ctx.act, ctx.slope = gate_mode, act, slope
+        ctx.drop_p = drop[0] if drop is not None else 0.0
         ctx.has_res, ctx.has_const = res_x is not None, constant is not None
         ctx.save_for_backward(Z, res_x if res_x is not None else Z.new_empty(0),
                               constant if constant is not None else Z.new_empty(0),
@@ -1021,18 +1040,19 @@ class LayerDense(torch.autograd.Function):
         rows = rows if ctx.has_rows else None
         packs, ctx.packs = ctx.packs, None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
-                                   act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], packs=packs)
+                                   act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], packs=packs,
+                                   drop_p=ctx.drop_p)
         if out is None:  # bf16 shapes the bf16 kernels do not take: the fp32 kernels on widened copies
             out = layer_dense_backward(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows=rows,
                                        res_x=None if res_x is None else res_x.float(), W_res=W_res, act=ctx.act,
-                                       slope=ctx.slope, need_dZ=ctx.needs_input_grad[0])
+                                       slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], drop_p=ctx.drop_p)
             for k in ("dpre", "dZ", "dres"):
                 if out[k] is not None:
                     out[k] = out[k].to(torch.bfloat16)
         grads, d_const, d_res, d_wres, d_bres = _dense_grads(out, prm, ctx.gate_mode, rows, Z, constant, res_x, W_res,
-                                                             lambda i: ctx.needs_input_grad[9 + i],
+                                                             lambda i: ctx.needs_input_grad[10 + i],
                                                              ctx.needs_input_grad[2])
-        return (out["dZ"], d_res, d_const, d_wres, d_bres, None, None, None, None, *grads)
+        return (out["dZ"], d_res, d_const, d_wres, d_bres, None, None, None, None, None, *grads)
 
 
 def _dense_grads(out, prm, gate_mode, rows, Z, constant, res_x, W_res, need, need_const):
@@ -1098,15 +1118,17 @@ class PropagateDense(torch.autograd.Function):
     term (+ the identity residual's dpre) from its accumulators, and the off-diagonal transposed middle-tile kernel
     (pg_spmm3t_ngram_mid_offdiag_f32, 657 MB at B(20,4) F = 128) accumulates into E: the input's whole gradient in
     two launches, where Propagate3 + LayerDense run the 4x4-block transposed kernel (1,050 MB) and autograd adds the
-    residual's gradient in a third pass. Inputs: (x, g, res, constant, gate_mode, act, slope, *params) with
-    res = the layer's residual is x itself (identity)."""
+    residual's gradient in a third pass. Inputs: (x, g, res, constant, gate_mode, act, slope, drop, *params) with
+    res = the layer's residual is x itself (identity), drop = the fused layer dropout (p, seed) or None."""
 
     @staticmethod
-    def forward(ctx, x, g: CSRGraph, res: bool, constant, gate_mode, act, slope, *params):
+    def forward(ctx, x, g: CSRGraph, res: bool, constant, gate_mode, act, slope, drop, *params):
         prm = dict(zip(_DENSE_KEYS, params))
         Z = spmm3(g, x)
-        Y = layer_dense(Z, prm, gate_mode, constant=constant, res_x=x if res else None, act=act, slope=slope)
+        Y = layer_dense(Z, prm, gate_mode, constant=constant, res_x=x if res else None, act=act, slope=slope,
+                        drop=drop)
         ctx.g, ctx.res, ctx.gate_mode, ctx.act, ctx.slope = g, res, gate_mode, act, slope
+        ctx.drop_p = drop[0] if drop is not None else 0.0
         ctx.has_const = constant is not None
         ctx.save_for_backward(Z, Y, constant if constant is not None else Z.new_empty(0), *params)
         return Y
@@ -1118,15 +1140,15 @@ class PropagateDense(torch.autograd.Function):
         constant = constant if ctx.has_const else None
         g = ctx.g
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, act=ctx.act, slope=ctx.slope,
-                                   span=(g.ngram.diag3(), ctx.res))
+                                   span=(g.ngram.diag3(), ctx.res), drop_p=ctx.drop_p)
         if out is None:
             raise RuntimeError("PropagateDense: pg_directgcn_dense_bwd_span_f32 refused a shape supports_span accepted")
         dX = spmm3t_offdiag(g, out["dZ"], out=out["E"])
         if dX is None:
             raise RuntimeError("PropagateDense: the off-diagonal transposed kernel refused a shape supports_span accepted")
         grads, d_const, _, _, _ = _dense_grads(out, prm, ctx.gate_mode, None, Z, constant, None, None,
-                                               lambda i: ctx.needs_input_grad[7 + i], ctx.needs_input_grad[3])
-        return (dX if ctx.needs_input_grad[0] else None, None, None, d_const, None, None, None, *grads)
+                                               lambda i: ctx.needs_input_grad[8 + i], ctx.needs_input_grad[3])
+        return (dX if ctx.needs_input_grad[0] else None, None, None, d_const, None, None, None, None, *grads)
 
     @staticmethod
     def supports(g: CSRGraph, x: torch.Tensor, F_out: int, res_x, W_res, rows, fused_norm: bool,

@@ -283,7 +283,8 @@ def _layer_local_train(conv, part: NodeRangePartition, h_full, res: nn.Module, a
     else:
         rows = part.rows if vec else None
         constant = conv.constant if vec else None
-    return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, 0 if vec else 1, act, ops.LEAKY_SLOPE, *params)
+    return ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, rows, 0 if vec else 1, act, ops.LEAKY_SLOPE, None,
+                                *params)
 
 
 def sharded_forward_train(model, part: NodeRangePartition, x_full: torch.Tensor, group=None,
@@ -1517,7 +1518,7 @@ class MiddleTrainer:
                 constant = None
             W_res, b_res = (res.weight, res.bias) if isinstance(res, nn.Linear) else (None, None)
             h_own = ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, None, 0 if vec else 1, True,
-                                         ops.LEAKY_SLOPE, *params)
+                                         ops.LEAKY_SLOPE, None, *params)
             h_own = F.dropout(h_own, p=model.dropout, training=model.training)
             res_x = h_own
         return model.head(h_own, need_emb=need_emb)

@@ -552,8 +552,37 @@ def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
     """Autograd of the fused dense layer (pg_directgcn_dense_bwd_f32: the MFMA kernels, or its any-shape kernels
     when F_in / F_out are not multiples of 4) against float64 autograd of protgram_directgcn.py:100-133 + residual
     + leaky_relu."""
+    _dense_backward_check(pkg, cuda, M, Fin, Fout, proj, vec, rows)
+
+
+def _layer_drop_keep(seed: int, M: int, F: int, p: float):
+    """The fused layer dropout's draw restated on the host (pg_common.h, drop_hash): element e = m F + j is kept
+    when the top 24 bits of murmur3's 32-bit finalizer of (e * 0x9E3779B1 + seed_lo) ^ seed_hi reach p 2^24."""
+    e = np.arange(M * F, dtype=np.uint64)
+    x = ((e * np.uint64(0x9E3779B1) + np.uint64(seed & 0xFFFFFFFF)) & np.uint64(0xFFFFFFFF)) ^ np.uint64(seed >> 32)
+    for sh, mul in ((16, 0x85EBCA6B), (13, 0xC2B2AE35), (16, None)):
+        x ^= x >> np.uint64(sh)
+        if mul is not None:
+            x = (x * np.uint64(mul)) & np.uint64(0xFFFFFFFF)
+    thr = int(p * 16777216.0 + 0.5)
+    return torch.from_numpy((x >> np.uint64(8)) >= np.uint64(thr)).view(M, F)
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
+                                                      (64, 128, 96, False, True, True), (300, 18, 10, True, True, False),
+                                                      (2000, 256, 256, False, True, False)])
+def test_dense_fused_dropout_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+    """The layer dropout fused into the dense epilogue (drop = (p, seed), every forward kernel: the pipelined and
+    32-row split-bf16 kernels and the tiled one) and its gradient read off the stored output (pg::act_grad, every
+    dgrad kernel incl. the any-shape one): the same float64 autograd check with the kernel's mask restated on the
+    host, forward included (dropped elements exactly 0)."""
+    _dense_backward_check(pkg, cuda, M, Fin, Fout, proj, vec, rows, drop=0.5 if M % 2 else 0.3)
+
+
+def _dense_backward_check(pkg, cuda, M, Fin, Fout, proj, vec, rows, drop=0.0):
     from protgram_directgcn_amd import ops
     Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, vec, rows, 7 * M + Fin)
+    seed = 0x0123_4567_89AB_CDEF + M
     gate = 0 if vec else 1
     # float64 reference through autograd
     d = {k: v.double().requires_grad_(True) for k, v in prm.items()}
@@ -575,6 +604,9 @@ def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
     if xd is not None:
         y = y + (xd @ Wrd.t() + brd if proj else xd)
     y = torch.nn.functional.leaky_relu(y, 0.01)
+    if drop > 0:
+        keep = _layer_drop_keep(seed, M, Fout, drop)
+        y = y * keep.double() / (1.0 - drop)
     (y * dY.double()).sum().backward()
     # device path
     dv = {k: v.to(cuda).requires_grad_(True) for k, v in prm.items()}
@@ -583,9 +615,12 @@ def test_dense_backward_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
     cg = const.to(cuda).requires_grad_(True) if const is not None else None
     Wrg = W_res.to(cuda).requires_grad_(True) if proj else None
     brg = b_res.to(cuda).requires_grad_(True) if proj else None
-    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01,
+    dr = (drop, torch.tensor([seed], dtype=torch.int64, device=cuda)) if drop > 0 else None
+    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01, dr,
                                *[dv[k] for k in ops._DENSE_KEYS])
     assert_close(out, y.detach().float(), "forward", rtol=2e-5, atol=2e-5)
+    if drop > 0:
+        assert torch.equal(out.detach().cpu() == 0, ~keep), "dropped elements"
     out.backward(dY.to(cuda))
     assert_grad_close(Zg.grad, Zd.grad, "dZ")
     for k in ops._DENSE_KEYS:
@@ -839,7 +874,7 @@ def test_head_bf16_input_equals_widened(pkg, cuda, F, H, C):
 @pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(1000, 128, 128, False, True, False), (777, 64, 128, True, True, True),
                                                       (300, 32, 16, False, False, False), (5000, 256, 256, False, True, False),
                                                       (129, 16, 40, True, True, True), (300, 20, 12, True, True, False)])
-def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows, drop=0.0):
     """bf16-mode autograd of the dense layer (pg_directgcn_dense_bwd_bf16; the last case, F not a multiple of 8,
     runs the fp32 backward kernels on widened copies) against float64 autograd on the same bf16-valued activations, with the leaky_relu
     mask taken from the device's own (bf16) forward output -- near y = 0 a float64 forward can pick the
@@ -873,10 +908,17 @@ def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows
     cg = const.to(cuda).requires_grad_(True) if const is not None else None
     Wrg = W_res.to(cuda).requires_grad_(True) if proj else None
     brg = b_res.to(cuda).requires_grad_(True) if proj else None
-    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01,
+    seed = 0x7EDC_BA98_7654_3210 + M
+    dr = (drop, torch.tensor([seed], dtype=torch.int64, device=cuda)) if drop > 0 else None
+    out = ops.LayerDense.apply(Zg, xg, cg, Wrg, brg, None if r is None else r.to(cuda), gate, True, 0.01, dr,
                                *[dv[k] for k in ops._DENSE_KEYS])
     assert out.dtype == torch.bfloat16
-    mask = torch.where(out.detach().cpu().double() > 0, 1.0, 0.01)
+    o64 = out.detach().cpu().double()
+    mask = torch.where(o64 > 0, 1.0, 0.01)
+    if drop > 0:  # kept elements scaled, dropped ones exactly 0 (the device's mask against the host restatement)
+        keep = _layer_drop_keep(seed, M, Fout, drop)
+        assert not bool((o64[~keep] != 0).any()), "dropped elements"
+        mask = mask * keep.double() / (1.0 - drop)
     (y * mask * dYb.double()).sum().backward()  # leaky_relu' from the device's forward output
     out.backward(dYb.to(cuda))
     assert Zg.grad.dtype == torch.bfloat16
@@ -897,6 +939,14 @@ def test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows
     if proj:
         close(Wrg.grad, Wrd.grad, "dW_res")
         close(brg.grad, brd.grad, "db_res")
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,vec,rows", [(5000, 256, 256, False, True, False), (1000, 128, 256, True, True, True),
+                                                      (300, 20, 12, True, True, False)])
+def test_dense_fused_dropout_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows):
+    """bf16 mode with the fused layer dropout (dense_bf16_kernel's epilogue; the bf16 dgrad kernel, or the fp32 ones on
+    widened copies for F % 8 != 0), through the bf16 float64 autograd check."""
+    test_dense_backward_bf16_vs_float64(pkg, cuda, M, Fin, Fout, proj, vec, rows, drop=0.5)
 
 
 def test_model_bf16_training_step_close_to_fp32(pkg, cuda):
@@ -1470,3 +1520,58 @@ def test_train_step_fused_head_matches_framework_head(pkg, cuda):
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=2e-6)
     for k, v in runs[0][1].items():
         assert_grad_close(runs[1][1][k].cpu(), v.cpu(), f"param {k}")
+
+
+def test_model_fused_dropout_matches_masked_layers(pkg, cuda, monkeypatch):
+    """model.body() in training mode with the layer dropout fused into the dense epilogue (ops.FUSED_DROPOUT) against
+    the same layers run without dropout and multiplied by the host restatement of the kernel's mask
+    (_layer_drop_keep, seeds recorded from the body's one draw): at p = 0.5 the outputs are bit-identical, and the
+    gradients of every parameter and of x through both layers (projected-residual LayerDense, then PropagateDense with
+    the span backward) agree within fp32 rounding."""
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    gen = torch.Generator().manual_seed(99)
+    x = torch.randn(N, 64, generator=gen).to(cuda)
+    w = torch.randn(N, 128, generator=gen).to(cuda)
+    data = pkg.Data(x=x, graph=g)
+    torch.manual_seed(0)
+    m = pkg.ProtGramDirectGCN([64, 128, 128], N, 20, 3, 0, 512, 0.5, True).to(cuda).train()
+    drawn = []
+    randint = torch.randint
+
+    def rec(*a, **k):
+        t = randint(*a, **k)
+        drawn.append(t)
+        return t
+    monkeypatch.setattr(torch, "randint", rec)
+    assert ops.FUSED_DROPOUT
+    xg = x.clone().requires_grad_(True)
+    data.x = xg
+    h = m.body(data)
+    monkeypatch.setattr(torch, "randint", randint)
+    assert len(drawn) == 1 and drawn[0].numel() == 2
+    seeds = [int(v) for v in drawn[0].cpu()]
+    (h * w).sum().backward()
+    got = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+    got_x = xg.grad.clone()
+    m.zero_grad()
+    # reference: the same layers without dropout, then the restated mask
+    xr = x.clone().requires_grad_(True)
+    hr = xr
+    for i, (conv, res) in enumerate(zip(m.convs, m.res_projs)):
+        if isinstance(res, torch.nn.Linear):
+            hr = conv.fused_forward(hr, g, res_x=hr, W_res=res.weight, b_res=res.bias, act=True)
+        else:
+            hr = conv.fused_forward(hr, g, res_x=hr, act=True)
+        keep = _layer_drop_keep(seeds[i], N, 128, 0.5).to(cuda)
+        hr = hr * keep.float() * 2.0
+        if i == 0:
+            frac = float(keep.float().mean())
+            assert abs(frac - 0.5) < 0.01, frac
+    assert torch.equal(h.detach(), hr.detach())
+    (hr * w).sum().backward()
+    assert_grad_close(got_x, xr.grad, "dx")
+    for k, p in m.named_parameters():
+        if k in got:
+            assert_grad_close(got[k], p.grad, f"d{k}")

@@ -36,7 +36,8 @@ def _cpu_spmm3_gated(g, x, prm, gate_mode, flags=None, out=None):
 
 
 def _cpu_layer_dense_pregated(Z, prm, gate_mode, rows=None, constant=None, res_x=None, W_res=None, b_res=None,
-                              act=False, slope=0.01, flags=None, out=None, pregated=False, packs=None):
+                              act=False, slope=0.01, flags=None, out=None, pregated=False, packs=None, drop=None):
+    assert drop is None, "the CPU stand-in has no fused dropout"
     if not pregated:
         return _cpu_layer_dense_impl(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope)
     # pre-gated operand: sum_q Zg_q W_q^T + sum_q s_q b_q (the gates still scale the biases)

@@ -50,7 +50,8 @@ def _cpu_spmm3_t(g, G, flags=None):
 
 
 def _cpu_layer_dense(Z, prm, gate_mode, rows=None, constant=None, res_x=None, W_res=None, b_res=None, act=False,
-                     slope=0.01, flags=None, out=None, packs=None):
+                     slope=0.01, flags=None, out=None, packs=None, drop=None):
+    assert drop is None, "the CPU stand-in has no fused dropout"
     y = _cpu_layer_dense_impl(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, act, slope)
     if out is not None:
         out.copy_(y)
@@ -81,8 +82,9 @@ def _cpu_layer_dense_impl(Z, prm, gate_mode, rows=None, constant=None, res_x=Non
 
 
 def _cpu_layer_dense_backward(dY, Z, Y, prm, gate_mode, rows=None, res_x=None, W_res=None, b_res=None, act=False,
-                              slope=0.01, flags=None, need_dZ=True, packs=None):
+                              slope=0.01, flags=None, need_dZ=True, packs=None, drop_p=0.0):
     """CPU stand-in for ops.layer_dense_backward (pg_directgcn_dense_bwd_f32): the same outputs from torch ops."""
+    assert drop_p == 0.0, "the CPU stand-in has no fused dropout"
     M, F_in = Z.size(0), Z.size(1) // 3
     dpre = dY * torch.where(Y > 0, 1.0, slope) if act else dY
 

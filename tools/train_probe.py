@@ -24,6 +24,9 @@ NO_OPTS = [a for a in sys.argv[2:] if a.startswith("--no")]
 if "--no-span" in sys.argv:             # the 4x4-block transposed kernel instead of ops.PropagateDense
     from protgram_directgcn_amd import ops as _ops
     _ops.SPAN_BACKWARD = False
+if "--no-fdrop" in sys.argv:            # F.dropout after each layer instead of the dropout fused into the dense epilogue
+    from protgram_directgcn_amd import ops as _ops
+    _ops.FUSED_DROPOUT = False
 if "--no-head" in sys.argv:             # the framework ops for the prediction head instead of ops.head_train
     pkg.train.HEAD_FUSED = False
 dims = [128, 128, 128]

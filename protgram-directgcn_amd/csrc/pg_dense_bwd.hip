@@ -620,7 +620,7 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
     static_assert(A_F4 >= 1 && B_C >= 1 && BNC * XBK % (8 * NT) == 0, "tile shape");
     constexpr int IMG = XLDK;
     constexpr int MAIN_U16 = 3 * (BM + BNC) * IMG;
-    constexpr int PBYTES = BM * 3 * FB * 4;  // <G_q, Z_q> products per (row, q, feature)
+    constexpr int PBYTES = BM * (3 * FB + 4) * 4;  // the epilogue's G tile, then <G_q, Z_q> products per (row, q, feature)
     constexpr int SMEM_BYTES = MAIN_U16 * 2 > PBYTES ? MAIN_U16 * 2 : PBYTES;
     __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
     __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
@@ -673,11 +673,11 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
     float bd[A_F4][3];
 #pragma unroll
     for (int q = 0; q < A_F4; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
-    float dres[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dres[r] = 0.f;
     const int64_t mlast = p.M - 1;
     const int64_t bsplit = (int64_t)p.N * p.F_out;
+    // B a k-tile ahead in named registers (an array here stays in scratch memory)
+    static_assert(B_C == 3, "three B pieces per thread");
+    uint4 rb00, rb01, rb02, rb10, rb11, rb12, rb20, rb21, rb22;
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < A_F4; ++q) {
@@ -687,6 +687,25 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
             ra[q] = ld4(p.dY + m * p.lddy + k);
             if (p.act) ry[q] = ld4(p.Y + m * p.ldy + k);
         }
+        // B (the split packed weights, 295 KB at F = 128: L2-resident), a k-tile ahead like A
+        auto bsrc = [&](int q) {
+            const int idx = tid + NT * q;
+            const int c = idx >> 2;  // workgroup column: (wn_c, segment, lane)
+            const int n = (c % 96) / 32 * p.F_in + nt * FB + (c / 96) * 32 + (c % 32);
+            return BT3 + (int64_t)n * p.F_out + k0 + 8 * (idx & 3);
+        };
+        const uint16_t* b0 = bsrc(0);
+        const uint16_t* b1 = bsrc(1);
+        const uint16_t* b2 = bsrc(2);
+        rb00 = *reinterpret_cast<const uint4*>(b0);
+        rb01 = *reinterpret_cast<const uint4*>(b0 + bsplit);
+        rb02 = *reinterpret_cast<const uint4*>(b0 + 2 * bsplit);
+        rb10 = *reinterpret_cast<const uint4*>(b1);
+        rb11 = *reinterpret_cast<const uint4*>(b1 + bsplit);
+        rb12 = *reinterpret_cast<const uint4*>(b1 + 2 * bsplit);
+        rb20 = *reinterpret_cast<const uint4*>(b2);
+        rb21 = *reinterpret_cast<const uint4*>(b2 + bsplit);
+        rb22 = *reinterpret_cast<const uint4*>(b2 + 2 * bsplit);
     };
     auto stash = [&](int k0) {
 #pragma unroll
@@ -714,25 +733,24 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
             *reinterpret_cast<uint2*>(Aimg(1) + o) = s1;
             *reinterpret_cast<uint2*>(Aimg(2) + o) = s2;
         }
-        // B (the split packed weights, 295 KB at F = 128: L2-resident) straight from global memory into the images:
-        // no registers held across the MFMAs
-#pragma unroll
-        for (int q = 0; q < B_C; ++q) {
+        auto bdst = [&](int q) {
             const int idx = tid + NT * q;
-            const int c = idx >> 2;  // workgroup column: (wn_c, segment, lane)
-            const int n = (c % 96) / 32 * p.F_in + nt * FB + (c / 96) * 32 + (c % 32);
-            const int64_t gsrc = (int64_t)n * p.F_out + k0 + 8 * (idx & 3);
-            const int o = c * IMG + 8 * (idx & 3);
-            uint4 v[3];
-#pragma unroll
-            for (int spl = 0; spl < 3; ++spl) v[spl] = *reinterpret_cast<const uint4*>(BT3 + spl * bsplit + gsrc);
-#pragma unroll
-            for (int spl = 0; spl < 3; ++spl) *reinterpret_cast<uint4*>(Bimg(spl) + o) = v[spl];
-        }
+            return (idx >> 2) * IMG + 8 * (idx & 3);
+        };
+        const int o0 = bdst(0), o1 = bdst(1), o2 = bdst(2);
+        *reinterpret_cast<uint4*>(Bimg(0) + o0) = rb00;
+        *reinterpret_cast<uint4*>(Bimg(1) + o0) = rb01;
+        *reinterpret_cast<uint4*>(Bimg(2) + o0) = rb02;
+        *reinterpret_cast<uint4*>(Bimg(0) + o1) = rb10;
+        *reinterpret_cast<uint4*>(Bimg(1) + o1) = rb11;
+        *reinterpret_cast<uint4*>(Bimg(2) + o1) = rb12;
+        *reinterpret_cast<uint4*>(Bimg(0) + o2) = rb20;
+        *reinterpret_cast<uint4*>(Bimg(1) + o2) = rb21;
+        *reinterpret_cast<uint4*>(Bimg(2) + o2) = rb22;
+        (void)k0;
     };
 
     const int ntiles = p.F_out / XBK;
-    const int t_res = (nt * FB + wn * 32) / XBK;  // the k-tile whose A image holds dpre of this lane's feature
     fetch(0);
     stash(0);
     __syncthreads();
@@ -758,15 +776,6 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
                 acc[j] = mfma32_bf(a[1], b[j][0], acc[j]);
                 acc[j] = mfma32_bf(a[0], b[j][1], acc[j]);
                 acc[j] = mfma32_bf(a[0], b[j][0], acc[j]);
-            }
-        }
-        if (sp.e_res && t == t_res) {  // dpre of this lane's 16 rows at its feature: the exact sum of the three splits
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                const int o = rl * IMG + (f - t * XBK);
-                dres[r] = __uint_as_float((uint32_t)Aimg(0)[o] << 16) + __uint_as_float((uint32_t)Aimg(1)[o] << 16) +
-                          __uint_as_float((uint32_t)Aimg(2)[o] << 16);
             }
         }
         if (t + 1 < ntiles) {
@@ -796,32 +805,67 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
         }
     }
 
-    // epilogue from the accumulators: dZ_q = s_q G_q, E = sum_q Wdiag_q dZ_q (+ dpre), products G_q Z_q into LDS
-    float* P = reinterpret_cast<float*>(smem);  // [BM][3][FB]; the k-loop ended with a barrier
+    // epilogue through LDS: the accumulators are parked as T [BM][3 x 64] (the k-loop ended with a barrier); thread
+    // item (row rl, features 4c..4c+3 of the block) reads G_q for q = in, out, und, writes dZ_q = s_q G_q and
+    // E = sum_q Wdiag_q dZ_q (+ dpre, recomputed from dY and Y: the value the k-loop split exactly) as float4 row pieces,
+    // and leaves its products G_q Z_q in its own T slots for the per-row gate partials (summed in feature order)
+    constexpr int TLD = BNC + 4;
+    constexpr int C4 = FB / 4;
+    constexpr int ITEMS = BM * C4 / NT;
+    static_assert(BM * TLD * 4 <= SMEM_BYTES && BM * C4 % NT == 0, "epilogue tile");
+    (void)f;
+    float* T = reinterpret_cast<float*>(smem);
+    const int c4 = tid % C4;
+    const int fo = nt * FB + 4 * c4;  // this thread's first feature
+    float4 zv[ITEMS][3], dy[ITEMS], yy[ITEMS];
 #pragma unroll
-    for (int r0 = 0; r0 < 16; r0 += 4) {
-        float zq[4][3];
+    for (int u = 0; u < ITEMS; ++u) {  // loads first: their latency overlaps the parking of the accumulators
+        const int rl = (tid + NT * u) / C4;
+        const int64_t m = min(m0 + rl, mlast);
 #pragma unroll
-        for (int r = r0; r < r0 + 4; ++r) {
-            const int64_t m = min(m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh, mlast);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) zq[r - r0][j] = p.Z[m * p.ldz + j * p.F_in + f];
+        for (int q = 0; q < 3; ++q) zv[u][q] = ld4(p.Z + m * p.ldz + q * p.F_in + fo);
+        if (sp.e_res) {
+            dy[u] = ld4(p.dY + m * p.lddy + fo);
+            yy[u] = p.act ? ld4(p.Y + m * p.ldy + fo) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    }
 #pragma unroll
-        for (int r = r0; r < r0 + 4; ++r) {
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
             const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            const int64_t m = m0 + rl;
-            float e = 0.f;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const float gv = acc[j][r];
-                const float dz = Sg[rl * 4 + j] * gv;
-                if (m < p.M && p.dZ) p.dZ[m * p.lddz + j * p.F_in + f] = dz;
-                e = __fmaf_rn(Wd[rl * 3 + j], dz, e);
-                P[(rl * 3 + j) * FB + wn * 32 + li] = gv * zq[r - r0][j];
-            }
-            if (m < p.M) sp.E[m * sp.lde + f] = sp.e_res ? e + dres[r] : e;
+            T[rl * TLD + j * FB + wn * 32 + li] = acc[j][r];
         }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+        const int rl = (tid + NT * u) / C4;
+        const int64_t m = m0 + rl;
+        float4 g[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) g[q] = ld4(&T[rl * TLD + q * FB + 4 * c4]);
+        float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float sq = Sg[rl * 4 + q], wq = Wd[rl * 3 + q];
+            const float4 dz = make_float4(sq * g[q].x, sq * g[q].y, sq * g[q].z, sq * g[q].w);
+            if (m < p.M && p.dZ) st4(p.dZ + m * p.lddz + q * p.F_in + fo, dz);
+            e = make_float4(__fmaf_rn(wq, dz.x, e.x), __fmaf_rn(wq, dz.y, e.y), __fmaf_rn(wq, dz.z, e.z),
+                            __fmaf_rn(wq, dz.w, e.w));
+            st4(&T[rl * TLD + q * FB + 4 * c4], make_float4(g[q].x * zv[u][q].x, g[q].y * zv[u][q].y,
+                                                            g[q].z * zv[u][q].z, g[q].w * zv[u][q].w));
+        }
+        if (sp.e_res) {
+            float4 d = dy[u];
+            if (p.act) {
+                d.x = pg::act_grad(d.x, yy[u].x, p.slope, p.drop_s);
+                d.y = pg::act_grad(d.y, yy[u].y, p.slope, p.drop_s);
+                d.z = pg::act_grad(d.z, yy[u].z, p.slope, p.drop_s);
+                d.w = pg::act_grad(d.w, yy[u].w, p.slope, p.drop_s);
+            }
+            e = make_float4(e.x + d.x, e.y + d.y, e.z + d.z, e.w + d.w);
+        }
+        if (m < p.M) st4(sp.E + m * sp.lde + fo, e);
     }
     __syncthreads();
     // gate partials: thread (row tid / 4, q = tid % 4 < 3) sums its row's 64 products of segment q in feature order
@@ -830,7 +874,7 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_span_kernel(DgradP p, const 
         const int64_t m = m0 + rl;
         if (q < 3 && m < p.M) {
             float ds = lead ? Bd[rl * 3 + q] : 0.f;
-            const float* row = P + (rl * 3 + q) * FB;
+            const float* row = T + rl * TLD + q * FB;
             for (int c = 0; c < FB; ++c) ds += row[c];
             p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds;
         }

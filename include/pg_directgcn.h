@@ -81,6 +81,9 @@ typedef struct pg_edge1 {
                                              default, PG_FLAG_WGRAD_F32MFMA opts out) */
 #define PG_FLAG_WGRAD_BF16_TILED (1u << 11) /* bf16 dense backward: the 128 x 128-tile weight-gradient kernel instead of
                                                the staged 128 x 384 one (default where F_in, F_out % 128 == 0) */
+#define PG_FLAG_DGRAD_BF16_TILED (1u << 10) /* bf16 dense backward: the input-gradient kernel that recomputes dpre per
+                                               128-column n-tile instead of the resident-A one (default where
+                                               F_out <= 256, F_out % 64 == 0; bit-identical results) */
 #define PG_FLAG_WGRAD_F32MFMA (1u << 18)  /* fp32 dense backward: the fp32-MFMA weight-gradient kernel instead of the
                                              split-bf16 one (default where F_in % 128 == 0, F_out % 128 == 0 and no
                                              projected residual) */

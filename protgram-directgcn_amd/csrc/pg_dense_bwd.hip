@@ -23,8 +23,10 @@
 //   (32 consecutive floats per half: conflict-free). Each split writes a partial; reduce_splits_kernel
 //   sums them in split order (deterministic, no atomics).
 #include <algorithm>
+#include <type_traits>
 
 #include "pg_bf16_util.h"
+
 #include "pg_common.h"
 #include "pg_split3.h"
 
@@ -1595,6 +1597,276 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
     }
 }
 
+// Resident-A form of dgrad_bf16_kernel (round 5, the default where F_out <= 256 and F_out % 64 == 0): one 256-thread
+// workgroup owns 64 rows for ALL n-tiles. dpre of its rows (the A operand, 64 x F_out bf16) is computed once into LDS
+// (dgrad_bf16_kernel recomputes it from dY and Y for each of the N / 128 n-tiles), then the workgroup walks the
+// n-tiles with the B k-tiles double-buffered a tile ahead (crossing n-tile boundaries) and the Z rows of each n-tile's
+// epilogue loaded during its last k-tile. Same products in the same order, same per-thread bias-dot order, same
+// epilogue: every output is bit-identical to dgrad_bf16_kernel's (PG_FLAG_DGRAD_BF16_TILED keeps that kernel).
+constexpr int RB_BM = 64, RB_NW = 4, RB_FMAX = 256;
+__global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
+    using namespace pgbf;
+    constexpr int BM = RB_BM, BN = 128, NW = RB_NW, NT = 64 * NW;
+    constexpr int WN = 2, WM = NW / WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    static_assert(TM == 1 && TN == 2, "wave tile");
+    constexpr int LDA = RB_FMAX + 8;                 // resident A row (bf16): 528 B, conflict-free ds_read_b128
+    constexpr int A_C = BM * BKB / 8 / NT;           // 16-B pieces of one A k-tile per thread (2)
+    constexpr int B_C = BN * BKB / 8 / NT;           // of one B k-tile (4)
+    constexpr int KT_MAX = RB_FMAX / BKB;
+    constexpr int TLD = BN + 4;
+    constexpr int B_BYTES = 2 * BN * LDKB * 2;
+    static_assert(BM * TLD * 4 <= B_BYTES, "the epilogue tile aliases the B buffers");
+    constexpr int C4 = BN / 4;
+    constexpr int ITER = BM * C4 / NT;               // epilogue items per thread (8)
+    __shared__ __attribute__((aligned(16))) uint16_t As[BM * LDA];
+    __shared__ __attribute__((aligned(16))) unsigned char bsm[B_BYTES];
+    __shared__ __attribute__((aligned(16))) float Sg[BM * 4];
+    __shared__ float Bd[BM * 3];
+    uint16_t* const Bs = reinterpret_cast<uint16_t*>(bsm);
+    float* const T = reinterpret_cast<float*>(bsm);
+
+    const int ntn = (p.N + BN - 1) / BN;
+    const int KT = p.F_out / BKB;
+    const int64_t m0 = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0) * BM;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave / WN, wn = wave % WN;
+    const int li = lane & 31, lh = lane >> 5;
+    const int64_t mlast = p.M - 1;
+
+    if (tid < BM) {
+        const int64_t m = m0 + tid;
+        float4 sv = make_float4(0.f, 0.f, 0.f, 1.f);
+        if (m < p.M) {
+            float ci, co, cd, cu, ca;
+            gate_values(p.g, m, ci, co, cd, cu, ca);
+            const float cad = ca * cd;
+            sv.x = cad * ci;
+            sv.y = cad * co;
+            sv.z = ca * cu;
+            st4(p.gates + m * 4, sv);
+        }
+        st4(&Sg[tid * 4], sv);
+    }
+
+    // B k-tile g = nt * KT + kt -> registers, two tiles ahead in two named sets (an array of registers here stays in
+    // scratch memory): tile g + 1 waits in one set while tile g + 2 loads into the other
+    static_assert(B_C == 4, "four B pieces per thread");
+    struct B4 {
+        uint4 a, b, c, d;
+    };
+    B4 S0, S1;
+    auto loadB = [&](int g) __attribute__((always_inline)) {
+        const int nt = g / KT, k0 = (g - nt * KT) * BKB;
+        auto src = [&](int q) {
+            const int idx = tid + NT * q;
+            const int n = min(nt * BN + (idx >> 3), p.N - 1);
+            return reinterpret_cast<const uint4*>(p.BT + (int64_t)n * p.F_out + k0 + 8 * (idx & 7));
+        };
+        B4 r;
+        r.a = *src(0);
+        r.b = *src(1);
+        r.c = *src(2);
+        r.d = *src(3);
+        return r;
+    };
+    auto stashB = [&](B4 r, int buf) __attribute__((always_inline)) {
+        uint16_t* Bb = Bs + buf * BN * LDKB;
+        auto dst = [&](int q) {
+            const int idx = tid + NT * q;
+            return reinterpret_cast<uint4*>(&Bb[(idx >> 3) * LDKB + 8 * (idx & 7)]);
+        };
+        *dst(0) = r.a;
+        *dst(1) = r.b;
+        *dst(2) = r.c;
+        *dst(3) = r.d;
+    };
+
+    // A = dpre of the 64 rows, all k-tiles' loads in flight at once; the bias dots <dpre, bsum_q> accumulate per
+    // thread over the k-tiles in order, as in dgrad_bf16_kernel (thread (row, 8-column piece) = (idx >> 3, idx & 7))
+    {
+        uint4 ra[KT_MAX][A_C], ry[KT_MAX][A_C];
+#pragma unroll
+        for (int t = 0; t < KT_MAX; ++t)
+#pragma unroll
+            for (int q = 0; q < A_C; ++q) {
+                const int idx = tid + NT * q;
+                const int64_t m = min(m0 + (idx >> 3), mlast);
+                const int k = (t < KT ? t : 0) * BKB + 8 * (idx & 7);
+                ra[t][q] = *reinterpret_cast<const uint4*>(p.dY + m * p.lddy + k);
+                if (p.act) ry[t][q] = *reinterpret_cast<const uint4*>(p.Y + m * p.ldy + k);
+            }
+        S0 = loadB(0);
+        float bd[A_C][3];
+#pragma unroll
+        for (int q = 0; q < A_C; ++q) bd[q][0] = bd[q][1] = bd[q][2] = 0.f;
+#pragma unroll
+        for (int t = 0; t < KT_MAX; ++t) {
+            if (t >= KT) break;
+#pragma unroll
+            for (int q = 0; q < A_C; ++q) {
+                const int idx = tid + NT * q;
+                const int k = t * BKB + 8 * (idx & 7);
+                const int64_t m = m0 + (idx >> 3);
+                float d[8];
+                unpack8(ra[t][q], d);
+                if (p.act) {
+                    float y[8];
+                    unpack8(ry[t][q], y);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) d[e] = pg::act_grad(d[e], y[e], p.slope, p.drop_s);
+                }
+                const uint4 v = pack8(d);
+                if (m < p.M) {
+                    *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
+                    float dr[8];
+                    unpack8(v, dr);
+#pragma unroll
+                    for (int sg = 0; sg < 3; ++sg) {
+                        const float4 b0 = ld4(p.bsum + sg * p.F_out + k), b1 = ld4(p.bsum + sg * p.F_out + k + 4);
+                        bd[q][sg] += dr[0] * b0.x + dr[1] * b0.y + dr[2] * b0.z + dr[3] * b0.w + dr[4] * b1.x +
+                                     dr[5] * b1.y + dr[6] * b1.z + dr[7] * b1.w;
+                    }
+                }
+                *reinterpret_cast<uint4*>(&As[(idx >> 3) * LDA + k]) = v;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < A_C; ++q) {
+#pragma unroll
+            for (int sg = 0; sg < 3; ++sg) {
+                float v = bd[q][sg];
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                bd[q][sg] = v;
+            }
+            const int idx = tid + NT * q;
+            if ((idx & 7) == 0) {
+                Bd[(idx >> 3) * 3 + 0] = bd[q][0];
+                Bd[(idx >> 3) * 3 + 1] = bd[q][1];
+                Bd[(idx >> 3) * 3 + 2] = bd[q][2];
+            }
+        }
+    }
+    const int G = ntn * KT;
+    if (G > 1) S1 = loadB(1);
+    stashB(S0, 0);
+    __syncthreads();
+
+    const int c4 = tid % C4;
+    f32x16 acc[TN];
+    uint2 zv[ITER];
+    auto epilogue = [&](int nt) __attribute__((always_inline)) {  // the B buffers are free: T aliases them
+        const int n0 = nt * BN;
+        const int j = n0 + 4 * c4;
+        const int seg = j < p.N ? j / p.F_in : 4;
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int rl = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                T[rl * TLD + wn * TN * 32 + jj * 32 + li] = acc[jj][r];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < ITER; ++u) {
+            const int rl = (tid + NT * u) / C4;
+            const int64_t mm = m0 + rl;
+            float part = 0.f;
+            if (mm < p.M && seg < 4) {
+                const float4 gv = ld4(&T[rl * TLD + 4 * c4]);
+                if (seg < 3) {
+                    const float sc = Sg[rl * 4 + seg];
+                    if (p.dZ)
+                        *reinterpret_cast<uint2*>(p.dZ + mm * p.lddz + j) =
+                            pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
+                    part = dot4(gv, unpack4(zv[u]));
+                } else {
+                    *reinterpret_cast<uint2*>(p.dres + mm * p.lddres + (j - 3 * p.F_in)) = pack4(gv);
+                }
+            }
+            T[rl * TLD + 4 * c4] = part;
+        }
+        __syncthreads();
+        if (tid < BM && m0 + tid < p.M) {
+            const int64_t m = m0 + tid;
+            float ds[3] = {0.f, 0.f, 0.f};
+            if (nt == 0) {
+                ds[0] = Bd[tid * 3 + 0];
+                ds[1] = Bd[tid * 3 + 1];
+                ds[2] = Bd[tid * 3 + 2];
+            }
+            for (int c = 0; c < C4; ++c) {
+                const int jj = n0 + 4 * c;
+                if (jj >= p.N) break;
+                const int q = jj / p.F_in;
+                if (q < 3) ds[q] += T[tid * TLD + 4 * c];
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
+        }
+        __syncthreads();  // T is read before the next n-tile's first B k-tile overwrites it
+    };
+    // tile g: MFMAs on buffer g & 1 (tile g, stashed); tile g + 2 loads into one register set while tile g + 1 goes
+    // from the other to the other buffer -- after the epilogue when g ends an n-tile (even g: load S0, stash S1)
+    auto step = [&](int g, auto odd) __attribute__((always_inline)) {  // odd: tile g + 2 loads into S1, g + 1 is in S0
+        const int nt = g / KT, kt = g - nt * KT;
+        if (kt == 0) {
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[jj][r] = 0.f;
+        }
+        if (g + 2 < G) {
+            if constexpr (decltype(odd)::value) S1 = loadB(g + 2);
+            else S0 = loadB(g + 2);
+        }
+        if (kt == KT - 1) {  // this n-tile's Z rows for the epilogue
+            const int j = nt * BN + 4 * c4;
+            const bool zseg = j < p.N && j / p.F_in < 3;
+#pragma unroll
+            for (int u = 0; u < ITER; ++u) {
+                const int64_t m = min(m0 + (tid + NT * u) / C4, mlast);
+                zv[u] = zseg ? *reinterpret_cast<const uint2*>(p.Z + m * p.ldz + j) : make_uint2(0u, 0u);
+            }
+        }
+        const uint16_t* Bb = Bs + (g & 1) * BN * LDKB;
+#pragma unroll
+        for (int kk = 0; kk < BKB / 16; ++kk) {
+            const bf16x8 a = __builtin_bit_cast(
+                bf16x8, *reinterpret_cast<const uint4*>(&As[(wm * 32 + li) * LDA + kt * BKB + kk * 16 + 8 * lh]));
+            bf16x8 b[TN];
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+                b[jj] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
+                                                      &Bb[(wn * TN * 32 + jj * 32 + li) * LDKB + kk * 16 + 8 * lh]));
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+                acc[jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[jj], acc[jj], 0, 0, 0);
+        }
+        auto stash_next = [&]() __attribute__((always_inline)) {
+            if constexpr (decltype(odd)::value) stashB(S0, (g + 1) & 1);
+            else stashB(S1, (g + 1) & 1);
+        };
+        if (kt + 1 < KT) {
+            stash_next();
+            __syncthreads();
+        } else {
+            __syncthreads();
+            epilogue(nt);
+            if (g + 1 < G) {
+                stash_next();
+                __syncthreads();
+            }
+        }
+    };
+    for (int g = 0; g < G; g += 2) {
+        step(g, std::false_type{});
+        if (g + 1 < G) step(g + 1, std::true_type{});
+    }
+}
+
 struct WgradB {
     int64_t M;
     int P, N, F_in;
@@ -2457,8 +2729,13 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         p.gates = g->gates;
         p.dsp = dsp;
         p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
-        const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
-        hipLaunchKernelGGL((dgrad_bf16_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
+        if (F_out <= RB_FMAX && F_out % BKB == 0 && !(flags & PG_FLAG_DGRAD_BF16_TILED)) {
+            const int64_t nb = (a->M + RB_BM - 1) / RB_BM;
+            hipLaunchKernelGGL(dgrad_bf16r_kernel, dim3((unsigned)nb), dim3(64 * RB_NW), 0, s, p);
+        } else {
+            const int64_t nb = ((a->M + DG_BM - 1) / DG_BM) * pl.ntn;
+            hipLaunchKernelGGL((dgrad_bf16_kernel<DG_BM, DG_BN, DG_NW>), dim3((unsigned)nb), dim3(64 * DG_NW), 0, s, p);
+        }
     }
     {
         const int nb = (int)std::min<int64_t>((a->M + 255) / 256, 2048);

@@ -1575,3 +1575,34 @@ def test_model_fused_dropout_matches_masked_layers(pkg, cuda, monkeypatch):
     for k, p in m.named_parameters():
         if k in got:
             assert_grad_close(got[k], p.grad, f"d{k}")
+
+
+@pytest.mark.parametrize("M,Fin,Fout,proj,rows,drop", [(5000, 256, 256, False, False, 0.0), (1000, 128, 256, True, True, 0.0),
+                                                       (3001, 256, 128, False, False, 0.5), (777, 64, 192, True, False, 0.3),
+                                                       (70, 256, 256, False, True, 0.0)])
+def test_dgrad_bf16_resident_matches_tiled(pkg, cuda, M, Fin, Fout, proj, rows, drop):
+    """The resident-A bf16 input gradient (dgrad_bf16r_kernel: dpre of 64 rows computed once for all n-tiles, the
+    default where F_out <= 256 and F_out % 64 == 0) against the per-n-tile kernel (PG_FLAG_DGRAD_BF16_TILED): every
+    output of the bf16 dense backward bit-identical, with and without the fused dropout."""
+    from protgram_directgcn_amd import ops
+    from protgram_directgcn_amd._lib import PG_FLAG_DGRAD_BF16_TILED, default_flags
+    Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, True, rows, 31 * M + Fout)
+    dv = {k: v.to(cuda) for k, v in prm.items()}
+    Zb, dYb = Z.to(torch.bfloat16).to(cuda), dY.to(torch.bfloat16).to(cuda)
+    xb = xres.to(torch.bfloat16).to(cuda) if xres is not None else None
+    rg = r.to(cuda) if r is not None else None
+    Wr = W_res.to(cuda) if proj else None
+    br = b_res.to(cuda) if proj else None
+    dr = (drop, torch.tensor([1234567 + M], dtype=torch.int64, device=cuda)) if drop > 0 else None
+    Y = ops.layer_dense(Zb, dv, 0, rows=rg, constant=const.to(cuda), res_x=xb, W_res=Wr, b_res=br, act=True, drop=dr)
+    assert Y.dtype == torch.bfloat16
+    outs = []
+    for fl in (default_flags(), default_flags() | PG_FLAG_DGRAD_BF16_TILED):
+        o = ops.layer_dense_backward(dYb, Zb, Y, dv, 0, rows=rg, res_x=xb, W_res=Wr, b_res=br, act=True, flags=fl,
+                                     drop_p=drop)
+        assert o is not None
+        outs.append(o)
+    for k in ("dpre", "dZ", "dres", "dgate", "dB", "dbsum"):
+        if outs[0][k] is None:
+            continue
+        assert torch.equal(outs[0][k], outs[1][k]), k

@@ -40,8 +40,10 @@ for F in (128, 256):
         return round(e0.elapsed_time(e1) / 20, 4)
 
     res[f"bwd_bf16_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(dY, Z, Y, prm, 0, act=True, packs=packs))
-    res[f"bwd_f32_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(dYf, Zf, Yf, prm, 0, act=True))
     from protgram_directgcn_amd import _lib
+    res[f"bwd_bf16_dgradtiled_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(
+        dY, Z, Y, prm, 0, act=True, packs=packs, flags=ops.default_flags() | _lib.PG_FLAG_DGRAD_BF16_TILED))
+    res[f"bwd_f32_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(dYf, Zf, Yf, prm, 0, act=True))
     res[f"bwd_f32_wgradf32mfma_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(
         dYf, Zf, Yf, prm, 0, act=True, flags=ops.default_flags() | _lib.PG_FLAG_WGRAD_F32MFMA))
     res[f"bwd_f32_dgradf32mfma_F{F}_ms"] = timed(lambda: ops.layer_dense_backward(

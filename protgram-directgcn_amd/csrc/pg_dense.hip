@@ -791,7 +791,8 @@ __device__ __forceinline__ int a_unit16(int s, int r, int g) { return 64 * s + 4
 // the wave's MFMA phase instead of all at the top of the iteration (stamps: issuing the five or seven pieces at once
 // took ~1,750 of an iteration's ~7,300 cycles, the memory pipeline pushing back); the constant / residual pieces stay
 // first, so the counted vmcnt waits are unchanged.
-template <bool PRE, bool IL>
+// DROP: the fused layer dropout (training); the inference instantiations carry no trace of it.
+template <bool PRE, bool IL, bool DROP>
 __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     constexpr int F_IN = 128, K = 384;
     constexpr int CH = K / 4;    // fp32 16-B chunks per row
@@ -817,8 +818,8 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
     const int wave = tid >> 6, lane = tid & 63;
     const int lc = lane & 15, kg = lane >> 4;
     const int col = 16 * wave + lc;
-    const bool mfma_first = wave < 4;
-    const uint64_t dseed = drop_seed_of(p);  // waves w and w + 4 share a SIMD
+    const bool mfma_first = wave < 4;  // waves w and w + 4 share a SIMD
+    const uint64_t dseed = DROP ? drop_seed_of(p) : 0ull;
     const int64_t T = (p.M + BM - 1) / BM;
     DSTAMP_INIT;
     {
@@ -1077,7 +1078,7 @@ __global__ __launch_bounds__(512) void dense_x3p_kernel(DenseP p) {
                 for (int e = 0; e < 4; ++e) {
                     const float qv = epi_sum(o[e], s0, s1, s2, B0[e], B1[e], B2[e], BR[e], C4[e], R4[e]);
                     y[e] = (p.act && !(qv > 0.f)) ? qv * p.slope : qv;
-                    if (p.drop_s != 0.f) y[e] = drop_apply(p, dseed, m0 + er, 4 * ej + e, y[e]);
+                    if (DROP) y[e] = drop_apply(p, dseed, m0 + er, 4 * ej + e, y[e]);
                 }
                 if (!DEXP(2)) {
                     const int64_t yr = p.map_y ? ngram_row(p, m0 + er) : m0 + er;
@@ -1248,12 +1249,15 @@ static int dense_launch(const pg_layer_args_t* a, const float* packed, uint32_t 
             const int64_t T16 = (a->M + 15) / 16;
             const unsigned g16 = (unsigned)(T16 < ncu ? T16 : ncu);
             const bool il = (flags & PG_FLAG_DENSE_NO_IL) == 0;
-            if (p.pregated) {
-                if (il) hipLaunchKernelGGL((dense_x3p_kernel<true, true>), dim3(g16), dim3(512), 0, s, p);
-                else hipLaunchKernelGGL((dense_x3p_kernel<true, false>), dim3(g16), dim3(512), 0, s, p);
+            if (p.drop_s != 0.f) {
+                if (p.pregated) hipLaunchKernelGGL((dense_x3p_kernel<true, true, true>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<false, true, true>), dim3(g16), dim3(512), 0, s, p);
+            } else if (p.pregated) {
+                if (il) hipLaunchKernelGGL((dense_x3p_kernel<true, true, false>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<true, false, false>), dim3(g16), dim3(512), 0, s, p);
             } else {
-                if (il) hipLaunchKernelGGL((dense_x3p_kernel<false, true>), dim3(g16), dim3(512), 0, s, p);
-                else hipLaunchKernelGGL((dense_x3p_kernel<false, false>), dim3(g16), dim3(512), 0, s, p);
+                if (il) hipLaunchKernelGGL((dense_x3p_kernel<false, true, false>), dim3(g16), dim3(512), 0, s, p);
+                else hipLaunchKernelGGL((dense_x3p_kernel<false, false, false>), dim3(g16), dim3(512), 0, s, p);
             }
         } else {
             if (p.rawW)

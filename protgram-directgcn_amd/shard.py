@@ -1501,6 +1501,14 @@ class MiddleTrainer:
         X, res_x = h, h.index_select(0, mp.own)
         L = len(model.convs)
         h_own = None
+        # the layer dropout fused into the dense epilogue (ops.FUSED_DROPOUT, as ProtGramDirectGCN.body): one draw of
+        # the layers' seeds per step, salted by the rank's first middle so that ranks (whose launches count their own
+        # rows from 0) draw independent masks
+        p_drop = float(model.dropout) if model.training else 0.0
+        seeds = None
+        if ops.FUSED_DROPOUT and 0.0 < p_drop < 1.0 and x_full.is_cuda:
+            seeds = torch.randint(0, 1 << 62, (L,), device=x_full.device, dtype=torch.int64)
+            seeds ^= (mp.m0 + 1) << 40
         for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
             if i == 0:
                 Z = _MidPropagate.apply(X, mp)  # the input carries no gradient
@@ -1517,9 +1525,11 @@ class MiddleTrainer:
             else:
                 constant = None
             W_res, b_res = (res.weight, res.bias) if isinstance(res, nn.Linear) else (None, None)
+            drop = (p_drop, seeds[i:i + 1]) if seeds is not None else None
             h_own = ops.LayerDense.apply(Z, res_x, constant, W_res, b_res, None, 0 if vec else 1, True,
-                                         ops.LEAKY_SLOPE, None, *params)
-            h_own = F.dropout(h_own, p=model.dropout, training=model.training)
+                                         ops.LEAKY_SLOPE, drop, *params)
+            if drop is None:
+                h_own = F.dropout(h_own, p=model.dropout, training=model.training)
             res_x = h_own
         return model.head(h_own, need_emb=need_emb)
 

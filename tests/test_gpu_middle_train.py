@@ -226,3 +226,58 @@ def test_middle_trainer_hip_graph_matches_eager(pkg, cuda, bf16):
         res.append((losses, [p.detach().clone() for p in tr.params]))
     assert res[0][0] == res[1][0], res
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bf16", [False, True])
+def test_middle_trainer_fused_dropout_matches_masked(pkg, cuda, bf16, monkeypatch):
+    """MiddleTrainer.forward in training mode with the layer dropout fused into the rank's dense launches
+    (ops.FUSED_DROPOUT, seeds salted by the rank's first middle) against the same forward with F.dropout replaced by
+    the host restatement of the kernel's mask on those seeds: at p = 0.5 the log-probs are bit-identical (rank 0 of 2
+    at 3-gram, the collectives no-ops; the decoder's own dropout set to 0)."""
+    from protgram_directgcn_amd import ops, shard
+    from test_gpu_configs import _model
+    from test_gpu_parity import _layer_drop_keep
+    n, dims = 3, [64, 64, 32]
+    N, s_, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s_, d, c, device=cuda)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(8)).to(cuda)
+    mp_ = shard.middle_partition(g, 0, 2)
+
+    def trainer():
+        m = _model(pkg, dims, N, n).to(cuda).train()
+        m.decoder_fc[2].p = 0.0
+        if bf16:
+            m.compute_dtype = torch.bfloat16
+        return shard.MiddleTrainer(m, mp_, l2_lambda=0.0, comm=_NoComm())
+
+    assert ops.FUSED_DROPOUT
+    randint, drawn = torch.randint, []
+
+    def rec(*a, **k):
+        t = randint(*a, **k)
+        drawn.append(t)
+        return t
+    monkeypatch.setattr(torch, "randint", rec)
+    with torch.no_grad():
+        lp, _ = trainer().forward(x, need_emb=False)
+    monkeypatch.setattr(torch, "randint", randint)
+    assert len(drawn) == 1
+    seeds = [int(v) for v in drawn[0].cpu()]  # salted in place by the trainer
+    calls = []
+    dropout = torch.nn.functional.dropout
+
+    def masked(inp, p=0.5, training=True, inplace=False):
+        if p == 0.0 or not training:
+            return inp
+        i = len(calls)
+        calls.append(i)
+        keep = _layer_drop_keep(seeds[i], inp.size(0), inp.size(1), p).to(inp.device)
+        return inp * keep.to(inp.dtype) * (1.0 / (1.0 - p))
+    monkeypatch.setattr(ops, "FUSED_DROPOUT", False)
+    monkeypatch.setattr(torch.nn.functional, "dropout", masked)
+    with torch.no_grad():
+        lp_ref, _ = trainer().forward(x, need_emb=False)
+    monkeypatch.setattr(torch.nn.functional, "dropout", dropout)
+    assert len(calls) == len(dims) - 1
+    assert torch.equal(lp, lp_ref)

@@ -83,7 +83,11 @@ typedef struct pg_edge1 {
                                                the staged 128 x 384 one (default where F_in, F_out % 128 == 0) */
 #define PG_FLAG_DGRAD_BF16_TILED (1u << 10) /* bf16 dense backward: the input-gradient kernel that recomputes dpre per
                                                128-column n-tile instead of the resident-A one (default where
-                                               F_out <= 256, F_out % 64 == 0; bit-identical results) */
+                                               F_out <= 256, F_out % 64 == 0 and M >= 256 rows per CU; bit-identical
+                                               results) */
+#define PG_FLAG_DGRAD_BF16_RESIDENT (1u << 9) /* bf16 dense backward: the resident-A input-gradient kernel at any M its
+                                                 F_out takes (below 256 rows per CU its 64-row workgroups underfill
+                                                 the GPU, so the default there is the per-n-tile kernel) */
 #define PG_FLAG_WGRAD_F32MFMA (1u << 18)  /* fp32 dense backward: the fp32-MFMA weight-gradient kernel instead of the
                                              split-bf16 one (default where F_in % 128 == 0, F_out % 128 == 0 and no
                                              projected residual) */

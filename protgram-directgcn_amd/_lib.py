@@ -22,6 +22,7 @@ PG_FLAG_DENSE_X3 = 1 << 16
 PG_FLAG_WGRAD_F32MFMA = 1 << 18
 PG_FLAG_WGRAD_BF16_TILED = 1 << 11
 PG_FLAG_DGRAD_BF16_TILED = 1 << 10
+PG_FLAG_DGRAD_BF16_RESIDENT = 1 << 9
 PG_FLAG_DGRAD_F32MFMA = 1 << 17
 PG_FLAG_NO_NGRAM = 1 << 20
 PG_FLAG_NGRAM_BLOCK4 = 1 << 21

@@ -2729,7 +2729,15 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         p.gates = g->gates;
         p.dsp = dsp;
         p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
-        if (F_out <= RB_FMAX && F_out % BKB == 0 && !(flags & PG_FLAG_DGRAD_BF16_TILED)) {
+        // resident-A kernel: 64-row workgroups, two per CU; below 256 rows per CU (a P = 8 rank's 20,000 rows: 313
+        // workgroups) they underfill the GPU and the per-n-tile kernel's N / 128 times as many workgroups run faster
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        const bool big = a->M >= (int64_t)256 * ncu;
+        if (F_out <= RB_FMAX && F_out % BKB == 0 && !(flags & PG_FLAG_DGRAD_BF16_TILED) &&
+            (big || (flags & PG_FLAG_DGRAD_BF16_RESIDENT))) {
             const int64_t nb = (a->M + RB_BM - 1) / RB_BM;
             hipLaunchKernelGGL(dgrad_bf16r_kernel, dim3((unsigned)nb), dim3(64 * RB_NW), 0, s, p);
         } else {

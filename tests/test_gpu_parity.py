@@ -1582,10 +1582,11 @@ def test_model_fused_dropout_matches_masked_layers(pkg, cuda, monkeypatch):
                                                        (70, 256, 256, False, True, 0.0)])
 def test_dgrad_bf16_resident_matches_tiled(pkg, cuda, M, Fin, Fout, proj, rows, drop):
     """The resident-A bf16 input gradient (dgrad_bf16r_kernel: dpre of 64 rows computed once for all n-tiles, the
-    default where F_out <= 256 and F_out % 64 == 0) against the per-n-tile kernel (PG_FLAG_DGRAD_BF16_TILED): every
-    output of the bf16 dense backward bit-identical, with and without the fused dropout."""
+    default where F_out <= 256, F_out % 64 == 0 and M >= 256 rows per CU; forced here by PG_FLAG_DGRAD_BF16_RESIDENT)
+    against the per-n-tile kernel (PG_FLAG_DGRAD_BF16_TILED): every output of the bf16 dense backward bit-identical,
+    with and without the fused dropout."""
     from protgram_directgcn_amd import ops
-    from protgram_directgcn_amd._lib import PG_FLAG_DGRAD_BF16_TILED, default_flags
+    from protgram_directgcn_amd._lib import PG_FLAG_DGRAD_BF16_RESIDENT, PG_FLAG_DGRAD_BF16_TILED, default_flags
     Z, xres, prm, const, r, W_res, b_res, dY = _dense_case(M, Fin, Fout, proj, True, rows, 31 * M + Fout)
     dv = {k: v.to(cuda) for k, v in prm.items()}
     Zb, dYb = Z.to(torch.bfloat16).to(cuda), dY.to(torch.bfloat16).to(cuda)
@@ -1597,7 +1598,7 @@ def test_dgrad_bf16_resident_matches_tiled(pkg, cuda, M, Fin, Fout, proj, rows, 
     Y = ops.layer_dense(Zb, dv, 0, rows=rg, constant=const.to(cuda), res_x=xb, W_res=Wr, b_res=br, act=True, drop=dr)
     assert Y.dtype == torch.bfloat16
     outs = []
-    for fl in (default_flags(), default_flags() | PG_FLAG_DGRAD_BF16_TILED):
+    for fl in (default_flags() | PG_FLAG_DGRAD_BF16_RESIDENT, default_flags() | PG_FLAG_DGRAD_BF16_TILED):
         o = ops.layer_dense_backward(dYb, Zb, Y, dv, 0, rows=rg, res_x=xb, W_res=Wr, b_res=br, act=True, flags=fl,
                                      drop_p=drop)
         assert o is not None

@@ -523,6 +523,16 @@ int64_t pg_gemm_at_b_workspace(int64_t M, int64_t P, int64_t N);
 int pg_gemm_at_b_f32(int64_t M, int64_t P, int64_t N, const float* A, int64_t lda, const float* B, int64_t ldb,
                      float* out, float* work, int64_t work_floats, void* stream);
 
+/* The dense backward's weight and bias gradients laid out as the layer's parameters take them (the autograd of
+ * protgram_directgcn.py:100-133 in nn.Linear / bias shapes), one launch instead of a transpose copy, two adds and a
+ * bias copy: from dB [F_out, S * F_in] and dbsum [>= 3, F_out] (pg_directgcn_dense_bwd_*'s dW) writes
+ * out = [S][F_out][F_in] (the gradients of W_main_in, W_main_out, W_undirected (, W_res): segment q of each row),
+ * then [F_out][F_in] = (seg0 + seg1) + seg2 (W_shared: fp32 adds in that order), then [2][3][F_out] (b_main_q and
+ * b_*_shared_q both receive dbsum[q]). out: (S + 1) F_out F_in + 6 F_out floats; S = 3 or 4. Needs F_in % 4 == 0
+ * and 16-B aligned dB, out (else PG_ERR_UNSUPPORTED). */
+int pg_dense_grads_layout_f32(int64_t F_out, int64_t F_in, int32_t S, const float* dB, const float* dbsum, float* out,
+                              void* stream);
+
 /* Fused prediction head (protgram_directgcn.py:218-222, eval mode): per row m of h [M, F]
  *   logp[m] = log_softmax(W2 relu(W1 h[m] + b1) + b2)      W1 [H, F], W2 [C, H] (nn.Linear layout)
  *   emb[m]  = h[m] / (||h[m]||_2 + eps)                      (models_utils.py:139-147)

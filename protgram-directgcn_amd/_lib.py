@@ -142,6 +142,7 @@ SIGNATURES = {
     "pg_adam_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                    ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pg_multi_sum_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
+    "pg_dense_grads_layout_f32": (ctypes.c_int, [c_i64, c_i64, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp]),
     "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "pg_gemm_at_b_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "pg_directgcn_head_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,

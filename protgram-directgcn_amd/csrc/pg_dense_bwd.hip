@@ -1867,6 +1867,37 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
     }
 }
 
+// pg_dense_grads_layout_f32: thread i < F_out F_in / 4 moves one float4 of every segment and writes W_shared's sum;
+// the next 6 F_out threads the bias pairs
+__global__ __launch_bounds__(256) void grads_layout_kernel(int F_out, int F_in, int S, const float* dB,
+                                                           const float* dbsum, float* out) {
+    const int64_t nw4 = (int64_t)F_out * F_in / 4, plane = (int64_t)F_out * F_in;
+    const int64_t total = nw4 + 6 * (int64_t)F_out;
+    const int K = S * F_in;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        if (i < nw4) {
+            const int n = (int)(i / (F_in / 4)), k = 4 * (int)(i % (F_in / 4));
+            const float* row = dB + (int64_t)n * K + k;
+            const float4 a = ld4(row), b = ld4(row + F_in), c = ld4(row + 2 * F_in);
+            const int64_t o = (int64_t)n * F_in + k;
+            st4(out + o, a);
+            st4(out + plane + o, b);
+            st4(out + 2 * plane + o, c);
+            if (S == 4) st4(out + 3 * plane + o, ld4(row + 3 * F_in));
+            float4 w;
+            w.x = __fadd_rn(__fadd_rn(a.x, b.x), c.x);
+            w.y = __fadd_rn(__fadd_rn(a.y, b.y), c.y);
+            w.z = __fadd_rn(__fadd_rn(a.z, b.z), c.z);
+            w.w = __fadd_rn(__fadd_rn(a.w, b.w), c.w);
+            st4(out + S * plane + o, w);
+        } else {
+            const int j = (int)(i - nw4);  // [2][3][F_out]
+            const int q = (j / F_out) % 3, n = j % F_out;
+            out[(S + 1) * plane + j] = dbsum[(int64_t)q * F_out + n];
+        }
+    }
+}
+
 struct WgradB {
     int64_t M;
     int P, N, F_in;
@@ -2601,6 +2632,19 @@ int64_t pg_gemm_at_b_workspace(int64_t M, int64_t P, int64_t N) {
     if (M < 0 || P <= 0 || N <= 0) return -1;
     const SplitPlan sp = split_rows(M, ((P + 127) / 128) * ((N + 127) / 128));
     return (int64_t)sp.splits * up4(P * N + 4 * P);
+}
+
+int pg_dense_grads_layout_f32(int64_t F_out, int64_t F_in, int32_t S, const float* dB, const float* dbsum, float* out,
+                              void* stream) {
+    PG_REQUIRE(F_out > 0 && F_in > 0 && F_out < (1 << 20) && F_in < (1 << 20) && (S == 3 || S == 4), "bad shape");
+    PG_REQUIRE(dB && dbsum && out, "null pointer");
+    if (F_in % 4 || !pg::aligned16(dB) || !pg::aligned16(out))
+        return pg::set_error(PG_ERR_UNSUPPORTED, "pg_dense_grads_layout_f32: needs F_in %% 4 == 0 and aligned buffers");
+    const int64_t n4 = F_out * F_in / 4 + 6 * F_out;
+    const int nb = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(grads_layout_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (int)F_out, (int)F_in, (int)S,
+                       dB, dbsum, out);
+    return pg::check_launch("pg_dense_grads_layout_f32");
 }
 
 int pg_gemm_at_b_f32(int64_t M, int64_t P, int64_t N, const float* A, int64_t lda, const float* B, int64_t ldb,

@@ -1055,6 +1055,25 @@ class LayerDense(torch.autograd.Function):
         return (out["dZ"], d_res, d_const, d_wres, d_bres, None, None, None, None, None, *grads)
 
 
+def dense_grads_layout(dB: torch.Tensor, dbsum: torch.Tensor, F_in: int):
+    """(Wg [S, F_out, F_in] segment-major weight gradients, W_shared's (Wg0 + Wg1) + Wg2 [F_out, F_in], the bias pairs
+    [2, 3, F_out]) from the dense backward's dB [F_out, S F_in] and dbsum: one pg_dense_grads_layout_f32 launch on
+    the GPU (views of one buffer), the same values as the torch ops it replaces (which CPU tensors still take)."""
+    F_out, S = dB.size(0), dB.size(1) // F_in
+    if dB.is_cuda and dB.dtype == torch.float32 and dB.is_contiguous() and dbsum.is_contiguous() and F_in % 4 == 0:
+        buf = torch.empty((S + 1) * F_out * F_in + 6 * F_out, device=dB.device, dtype=torch.float32)
+        rc = load_library().pg_dense_grads_layout_f32(F_out, F_in, S, _p(dB), _p(dbsum), _p(buf), _stream(dB))
+        if rc != _lib.PG_ERR_UNSUPPORTED:
+            check(rc, "pg_dense_grads_layout_f32")
+            plane = F_out * F_in
+            return (buf[:S * plane].view(S, F_out, F_in), buf[S * plane:(S + 1) * plane].view(F_out, F_in),
+                    buf[(S + 1) * plane:].view(2, 3, F_out))
+    Wg = dB.view(F_out, S, F_in).transpose(0, 1).contiguous()
+    ws = Wg[0] + Wg[1]
+    ws += Wg[2]
+    return Wg, ws, dbsum[:3].unsqueeze(0).expand(2, 3, F_out).contiguous()
+
+
 def _dense_grads(out, prm, gate_mode, rows, Z, constant, res_x, W_res, need, need_const):
     """The parameter gradients of LayerDense / PropagateDense from the dense backward's outputs: (grads in _DENSE_KEYS
     order, d_constant, d_res, d_W_res, d_b_res); need(i) says whether parameter i of _DENSE_KEYS needs its gradient."""
@@ -1065,12 +1084,9 @@ def _dense_grads(out, prm, gate_mode, rows, Z, constant, res_x, W_res, need, nee
     # instead of copying it: column slices of dB break the parameters' layout contract (one strided copy each), and
     # a bias sum shared by two parameters is copied for one of them. One copy lays dB out by segment
     # ([segments, F_out, F_in]); W_shared = (W_in' + W_out') + W_und' as before; one copy doubles the bias sums.
-    Wg = dB.view(F_out, dB.size(1) // F_in, F_in).transpose(0, 1).contiguous()
+    Wg, ws, bb = dense_grads_layout(dB, dbsum, F_in)
     g = {"W_main_in": Wg[0], "W_main_out": Wg[1], "W_undirected": Wg[2]}
-    ws = Wg[0] + Wg[1]
-    ws += Wg[2]
     g["W_shared"] = ws
-    bb = dbsum[:3].unsqueeze(0).expand(2, 3, F_out).contiguous()
     g["b_main_in"], g["b_dir_shared_in"] = bb[0, 0], bb[1, 0]
     g["b_main_out"], g["b_dir_shared_out"] = bb[0, 1], bb[1, 1]
     g["b_undirected"], g["b_undirected_shared"] = bb[0, 2], bb[1, 2]

@@ -1607,3 +1607,19 @@ def test_dgrad_bf16_resident_matches_tiled(pkg, cuda, M, Fin, Fout, proj, rows, 
         if outs[0][k] is None:
             continue
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("F_out,F_in,S", [(128, 128, 3), (256, 128, 4), (40, 16, 3), (12, 20, 4)])
+def test_dense_grads_layout_matches_torch(pkg, cuda, F_out, F_in, S):
+    """pg_dense_grads_layout_f32 (the dense backward's weight and bias gradients in the parameters' layout, one
+    launch) against the torch ops it replaces, run on the same values on the CPU: bit-identical segments, W_shared's
+    (seg0 + seg1) + seg2 and bias pairs."""
+    from protgram_directgcn_amd import ops
+    gen = torch.Generator().manual_seed(F_out * 7 + S)
+    dW = torch.randn(F_out * S * F_in + 4 * F_out, generator=gen)
+    dB, dbsum = dW[:F_out * S * F_in].view(F_out, S * F_in), dW[F_out * S * F_in:].view(4, F_out)
+    ref = ops.dense_grads_layout(dB, dbsum, F_in)  # CPU tensors: the torch ops
+    dWg = dW.to(cuda)
+    got = ops.dense_grads_layout(dWg[:F_out * S * F_in].view(F_out, S * F_in), dWg[F_out * S * F_in:].view(4, F_out), F_in)
+    for a, b, what in zip(got, ref, ("segments", "W_shared", "bias pairs")):
+        assert a.shape == b.shape and torch.equal(a.cpu(), b), what

@@ -392,6 +392,9 @@ typedef struct pg_layer_grad_args {
     float* gates;
     float* dW;
     float* work; int64_t work_floats;
+    /* optional (bf16 backward only; NULL: not written): dpre as fp32, the same bf16-rounded values -- the per-node
+     * constant's gradient in its fp32 parameter dtype without a conversion pass */
+    float* dpre_f32; int64_t ldp_f32;
 } pg_layer_grad_args_t;
 
 int64_t pg_directgcn_dense_bwd_workspace(const pg_layer_args_t* args);

@@ -66,7 +66,7 @@ class LayerGradArgs(ctypes.Structure):
     """pg_layer_grad_args_t"""
     _fields_ = [("dY", c_vp), ("lddy", c_i64), ("dpre", c_vp), ("ldp", c_i64), ("dZ", c_vp), ("lddz", c_i64),
                 ("dres", c_vp), ("lddres", c_i64), ("dgate", c_vp), ("gates", c_vp), ("dW", c_vp),
-                ("work", c_vp), ("work_floats", c_i64)]
+                ("work", c_vp), ("work_floats", c_i64), ("dpre_f32", c_vp), ("ldp_f32", c_i64)]
 
 
 # symbol -> (restype, argtypes); every symbol declared in include/pg_directgcn.h

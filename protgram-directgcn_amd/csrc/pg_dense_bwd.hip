@@ -1353,6 +1353,8 @@ struct DgradB {
     float* gates;
     float* dsp;
     int remap;
+    float* dpre32;  // optional fp32 copy of dpre (the rounded values), or null
+    int64_t ldp32;
 };
 
 // Reproducibility (round 5). With packed-FP32 VALU math (v_pk_fma_f32 / v_pk_mul_f32, formed by the SLP vectoriser
@@ -1461,6 +1463,10 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
                     *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
                     float dr[8];
                     unpack8(v, dr);  // the rounded gradient, as the products below see it
+                    if (p.dpre32) {
+                        st4(p.dpre32 + m * p.ldp32 + k, make_float4(dr[0], dr[1], dr[2], dr[3]));
+                        st4(p.dpre32 + m * p.ldp32 + k + 4, make_float4(dr[4], dr[5], dr[6], dr[7]));
+                    }
 #pragma unroll
                     for (int sg = 0; sg < 3; ++sg) {
                         const float4 b0 = ld4(p.bsum + sg * p.F_out + k), b1 = ld4(p.bsum + sg * p.F_out + k + 4);
@@ -1721,6 +1727,10 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                     *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
                     float dr[8];
                     unpack8(v, dr);
+                    if (p.dpre32) {
+                        st4(p.dpre32 + m * p.ldp32 + k, make_float4(dr[0], dr[1], dr[2], dr[3]));
+                        st4(p.dpre32 + m * p.ldp32 + k + 4, make_float4(dr[4], dr[5], dr[6], dr[7]));
+                    }
 #pragma unroll
                     for (int sg = 0; sg < 3; ++sg) {
                         const float4 b0 = ld4(p.bsum + sg * p.F_out + k), b1 = ld4(p.bsum + sg * p.F_out + k + 4);
@@ -2773,6 +2783,10 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         p.gates = g->gates;
         p.dsp = dsp;
         p.remap = (flags & PG_FLAG_NO_XCD_REMAP) ? 0 : 1;
+        PG_REQUIRE(!g->dpre_f32 || (g->ldp_f32 >= F_out && g->ldp_f32 % 4 == 0 && pg::aligned16(g->dpre_f32)),
+                   "dpre_f32 needs ldp_f32 >= F_out, a multiple of 4, and a 16-B aligned buffer");
+        p.dpre32 = g->dpre_f32;
+        p.ldp32 = g->ldp_f32;
         // resident-A kernel: 64-row workgroups, two per CU; below 256 rows per CU (a P = 8 rank's 20,000 rows: 313
         // workgroups) they underfill the GPU and the per-n-tile kernel's N / 128 times as many workgroups run faster
         int dev = 0, ncu = 256;

@@ -787,7 +787,7 @@ def _layer_dense_bf16(Z, prm, gate_mode, rows, constant, res_x, W_res, b_res, ac
 def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=None, W_res=None, b_res=None,
                          act: bool = False, slope: float = LEAKY_SLOPE, flags: Optional[int] = None,
                          need_dZ: bool = True, packs: Optional[list] = None, span: Optional[tuple] = None,
-                         drop_p: float = 0.0):
+                         drop_p: float = 0.0, dpre_f32: bool = False):
     """pg_directgcn_dense_bwd_f32 (any shape; bf16 operands: pg_directgcn_dense_bwd_bf16, None when F_in / F_out
     are not multiples of 8 -- the caller then runs the fp32 kernels on widened copies). Returns a dict with
       dpre [M, F_out], dZ [M, 3F_in], dres [M, F_in] (projected residual) or None,
@@ -796,7 +796,8 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
     packs: the bf16 forward's packed weights of the same parameters (LayerDense: saved by its forward), else packed
     here. span = (wdiag [M, 3], e_res): pg_directgcn_dense_bwd_span_f32 (fp32 only), which also returns
     E [M, F_in] = sum_q wdiag[:, q] dZ_q (+ dpre when e_res); None when it does not take the shape.
-    drop_p: the forward's fused dropout (Y is its output; the mask is read off Y, pg::act_grad)."""
+    drop_p: the forward's fused dropout (Y is its output; the mask is read off Y, pg::act_grad). dpre_f32 (bf16 only):
+    also return dpre as fp32 ("dpre_f32": the same rounded values, written by the dgrad kernel)."""
     lib = load_library()
     _require_gpu(dY, Z, Y)
     M, F_in = Z.size(0), Z.size(1) // 3
@@ -834,6 +835,10 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
         g.dres, g.lddres = _p(dres), dres.stride(0)
     g.dgate, g.gates, g.dW = _p(dgate), _p(gates), _p(dW)
     g.work, g.work_floats = _p(work), work.numel()
+    dpre32 = None
+    if bf and dpre_f32:
+        dpre32 = torch.empty(M, F_out, device=dev, dtype=torch.float32)
+        g.dpre_f32, g.ldp_f32 = _p(dpre32), dpre32.stride(0)
     fl = default_flags() if flags is None else flags
     E = None
     if span is not None:
@@ -855,7 +860,7 @@ def layer_dense_backward(dY, Z, Y, prm: dict, gate_mode: int, rows=None, res_x=N
         return None
     check(rc, name)
     del keep
-    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "E": E,
+    return {"dpre": dpre, "dZ": dZ, "dres": dres, "dgate": dgate, "E": E, "dpre_f32": dpre32,
             "dB": dW[:F_out * K].view(F_out, K), "dbsum": dW[F_out * K:].view(4, F_out)}
 
 
@@ -1041,7 +1046,9 @@ class LayerDense(torch.autograd.Function):
         packs, ctx.packs = ctx.packs, None
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
                                    act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], packs=packs,
-                                   drop_p=ctx.drop_p)
+                                   drop_p=ctx.drop_p,
+                                   dpre_f32=constant is not None and ctx.needs_input_grad[2]
+                                   and constant.dtype == torch.float32)
         if out is None:  # bf16 shapes the bf16 kernels do not take: the fp32 kernels on widened copies
             out = layer_dense_backward(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows=rows,
                                        res_x=None if res_x is None else res_x.float(), W_res=W_res, act=ctx.act,
@@ -1106,7 +1113,9 @@ def _dense_grads(out, prm, gate_mode, rows, Z, constant, res_x, W_res, need, nee
             g[name] = full
     d_const = None
     if constant is not None and need_const:
-        dp = dpre.to(constant.dtype)
+        dp = out.get("dpre_f32")  # the bf16 backward's own fp32 copy (the same values as the conversion below)
+        if dp is None or dp.dtype != constant.dtype:
+            dp = dpre.to(constant.dtype)
         if rows is None and constant.size(0) == M:
             d_const = dp  # every row of the constant receives exactly its dpre row (no zero-fill + add pass)
         else:

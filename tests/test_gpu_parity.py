@@ -1600,10 +1600,12 @@ def test_dgrad_bf16_resident_matches_tiled(pkg, cuda, M, Fin, Fout, proj, rows, 
     outs = []
     for fl in (default_flags() | PG_FLAG_DGRAD_BF16_RESIDENT, default_flags() | PG_FLAG_DGRAD_BF16_TILED):
         o = ops.layer_dense_backward(dYb, Zb, Y, dv, 0, rows=rg, res_x=xb, W_res=Wr, b_res=br, act=True, flags=fl,
-                                     drop_p=drop)
+                                     drop_p=drop, dpre_f32=True)
         assert o is not None
+        # the kernel's fp32 copy of dpre (the per-node constant's gradient): exactly the bf16 values widened
+        assert o["dpre_f32"] is not None and torch.equal(o["dpre_f32"], o["dpre"].float())
         outs.append(o)
-    for k in ("dpre", "dZ", "dres", "dgate", "dB", "dbsum"):
+    for k in ("dpre", "dZ", "dres", "dgate", "dB", "dbsum", "dpre_f32"):
         if outs[0][k] is None:
             continue
         assert torch.equal(outs[0][k], outs[1][k]), k

@@ -82,7 +82,7 @@ def _cpu_layer_dense_impl(Z, prm, gate_mode, rows=None, constant=None, res_x=Non
 
 
 def _cpu_layer_dense_backward(dY, Z, Y, prm, gate_mode, rows=None, res_x=None, W_res=None, b_res=None, act=False,
-                              slope=0.01, flags=None, need_dZ=True, packs=None, drop_p=0.0):
+                              slope=0.01, flags=None, need_dZ=True, packs=None, drop_p=0.0, dpre_f32=False):
     """CPU stand-in for ops.layer_dense_backward (pg_directgcn_dense_bwd_f32): the same outputs from torch ops."""
     assert drop_p == 0.0, "the CPU stand-in has no fused dropout"
     M, F_in = Z.size(0), Z.size(1) // 3

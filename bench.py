@@ -272,19 +272,28 @@ def main():
     # per-kernel launch durations: HIP events recorded on each launch's stream around every propagation, dense and
     # head launch of eager runs of the same step right after the timed region (graph replays carry no per-launch
     # events; the kernels are the same). rocprofv3's kernel trace of the same command agrees (profiles/).
+    # The eager steps themselves are bracketed by events on the current stream too (eager_ms_per_step): the
+    # per-kernel times are checked against the step of the same mode (their sum cannot exceed it).
     ops.SPMM_EVENTS, ops.DENSE_EVENTS, ops.HEAD_EVENTS = [], [], []
+    step_evs = []
     for _ in range(args.kernel_reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         eager_step()
+        e1.record()
+        step_evs.append((e0, e1))
     torch.cuda.synchronize()
     evs = {"propagation": ops.SPMM_EVENTS, "dense": ops.DENSE_EVENTS, "head": ops.HEAD_EVENTS}
     ops.SPMM_EVENTS = ops.DENSE_EVENTS = ops.HEAD_EVENTS = None
     kms = {k: [e0.elapsed_time(e1) for e0, e1 in v] for k, v in evs.items()}
-    t_local = torch.tensor([elapsed] + [sum(v) / max(1, len(v)) for v in kms.values()], dtype=torch.float64,
+    eager_ms = sum(e0.elapsed_time(e1) for e0, e1 in step_evs) / max(1, len(step_evs))
+    t_local = torch.tensor([elapsed, eager_ms] + [sum(v) / max(1, len(v)) for v in kms.values()], dtype=torch.float64,
                            device=dev)
     if world > 1:
         dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
     elapsed = float(t_local[0])
-    avg_ms = dict(zip(kms, (float(v) for v in t_local[1:].tolist())))
+    eager_ms = float(t_local[1])
+    avg_ms = dict(zip(kms, (float(v) for v in t_local[2:].tolist())))
     spmm_avg_ms = avg_ms["propagation"]
     ms_per_step = elapsed / args.steps * 1e3
     edges_per_step = 3 * g.nnz * L
@@ -396,7 +405,9 @@ def main():
                                                                                      mid_run.graphs is not None))
                                       else "eager launches")
                           + f"; per-kernel: HIP events around each launch of {args.kernel_reps} eager steps "
-                            "after the timed region, on the launch stream")
+                            "after the timed region, on the launch stream (eager_ms_per_step: those steps' own "
+                            "duration, the bound their per-kernel times sum under)")
+    roofline["eager_ms_per_step"] = round(eager_ms, 6)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

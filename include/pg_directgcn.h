@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 2  /* 2: pg_layer_args_t gained drop_p / drop_seed (fused layer dropout) */
+#define PG_ABI_VERSION 3  /* 2: pg_layer_args_t gained drop_p / drop_seed (fused layer dropout); 3: pg_adam_f32 hyper */
 
 #define PG_OK 0
 #define PG_ERR_ARG (-1)
@@ -497,10 +497,14 @@ typedef struct pg_adam_desc {
 
 /* sq_partial (optional, [nchunks]): per-chunk sums of p^2 of the parameters BEFORE the update -- the value of the
  * trainer's L2 term (protgram_directgcn_trainer.py:96) from the pass that reads p anyway; written on skipped
- * (found_inf) steps too. pg_multi_sum_f32 adds n partials in fixed order (deterministic). */
+ * (found_inf) steps too. pg_multi_sum_f32 adds n partials in fixed order (deterministic).
+ * hyper (optional): device double[2] = {lr, weight_decay}. When given, the kernel reads the learning rate and the
+ * decay there at run time (lr argument ignored; decay = hyper[1] + weight_decay argument), so a step captured in a
+ * HIP graph follows the schedule the caller writes into it between replays (ReduceLROnPlateau,
+ * protgram_directgcn_trainer.py:84, :102). Same arithmetic as the by-value form: the same bits. */
 int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
                 double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
-                const float* found_inf, float* sq_partial, void* stream);
+                const float* found_inf, float* sq_partial, const double* hyper, void* stream);
 int pg_multi_sum_f32(int64_t n, const float* x, float* out, void* stream);
 
 /* Training step of the prediction head (decoder_fc -> log_softmax -> nll_loss, protgram_directgcn.py:218-222 and

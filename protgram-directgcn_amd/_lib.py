@@ -140,7 +140,7 @@ SIGNATURES = {
     "pg_multi_sqsum_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "pg_multi_axpy_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, c_f32, c_vp, c_vp]),
     "pg_adam_f32": (ctypes.c_int, [ctypes.c_int, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                                   ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                   ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pg_multi_sum_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp]),
     "pg_dense_grads_layout_f32": (ctypes.c_int, [c_i64, c_i64, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp]),
     "pg_gemm_at_b_workspace": (c_i64, [c_i64, c_i64, c_i64]),
@@ -176,7 +176,7 @@ def load_library():
         if fn is None:
             raise NativeLibraryError(f"{_LIB_PATH} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.pg_abi_version() != 2:
+    if lib.pg_abi_version() != 3:
         raise NativeLibraryError("ABI version mismatch")
     _lib = lib
     return lib

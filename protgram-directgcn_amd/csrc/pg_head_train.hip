@@ -197,7 +197,11 @@ __global__ __launch_bounds__(NT) void head_train_kernel(HeadTrainP p) {
             const int row = 8 * wave + (lane >> 3), part = lane & 7;
             const int64_t m = m0 + row;
             const bool ok = m < p.M;
-            const int yv = ok ? (int)p.y[m] : -1;
+            const int64_t yl = ok ? p.y[m] : -1;
+            const int yv = (int)yl;
+            // a label outside [0, C) makes the loss NaN (F.nll_loss raises on it; ops.head_train checks the labels
+            // on the host once per label tensor, this covers what that check cannot see, e.g. a captured step)
+            if (ok && part == 0 && (yl < 0 || yl >= p.C)) lossp += __builtin_nanf("");
             float x[TC / 8];
             float mx = -INFINITY;
 #pragma unroll

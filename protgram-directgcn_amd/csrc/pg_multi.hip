@@ -105,6 +105,9 @@ __global__ __launch_bounds__(256) void axpy_chunks_kernel(int ntens, const pg_te
 //   g  = grad * inv_scale (+ weight_decay * p)
 //   m  = lerp(m, g, 1 - beta1) ; v = v * beta2 + (1 - beta2) * g * g
 //   p += (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps),   bc_k = 1 - beta_k^t  (t = step + 1, in double)
+// hyper (optional): device double[2] = {lr, weight_decay}, read at run time instead of the by-value lr (and added to
+// the by-value weight_decay, the trainer's folded L2 gradient 2*l2_lambda): a HIP-graph replay then follows a
+// learning-rate schedule written into it between replays (ReduceLROnPlateau, protgram_directgcn_trainer.py:84,102).
 // Skipped when *found_inf != 0 (GradScaler's device-side flag; no host sync). sq_partial (optional): chunk b's
 // sum of p^2 BEFORE the update into sq_partial[b] -- the trainer's L2 value from the pass that reads p anyway
 // (computed on skipped steps too, as the reference's loss includes it).
@@ -122,7 +125,7 @@ __device__ __forceinline__ float block_sum256(float s) {
 __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc_t* d, const int64_t* chunk_ptr,
                                                    double lr, double beta1, double beta2, float eps, float weight_decay,
                                                    const float* step, const float* grad_scale, const float* found_inf,
-                                                   float* sq_partial) {
+                                                   float* sq_partial, const double* hyper, double wd_extra) {
     const bool skip = found_inf && found_inf[0] != 0.f;
     if (skip && !sq_partial) return;
     const int64_t b = blockIdx.x;
@@ -133,6 +136,10 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
         else hi = mid;
     }
     const pg_adam_desc_t t = d[lo];
+    if (hyper) {  // the same double arithmetic the host does for the by-value form: bit-identical updates
+        lr = hyper[0];
+        weight_decay = (float)(hyper[1] + wd_extra);
+    }
     const double tt = (double)step[0] + 1.0;
     const double bc1 = 1.0 - pow(beta1, tt), bc2 = 1.0 - pow(beta2, tt);
     const float step_size = (float)((lr / bc1) * -1.0);
@@ -234,14 +241,15 @@ int pg_multi_sum_f32(int64_t n, const float* x, float* out, void* stream) {
 
 int pg_adam_f32(int ntens, const pg_adam_desc_t* descs, const int64_t* chunk_ptr, int64_t nchunks, double lr,
                 double beta1, double beta2, double eps, double weight_decay, float* step, const float* grad_scale,
-                const float* found_inf, float* sq_partial, void* stream) {
+                const float* found_inf, float* sq_partial, const double* hyper, void* stream) {
     PG_REQUIRE(ntens >= 0 && nchunks >= 0 && step, "bad arguments");
     PG_REQUIRE(beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && lr >= 0 && eps >= 0, "bad hyper-parameters");
     hipStream_t s = (hipStream_t)stream;
     if (nchunks > 0) {
         PG_REQUIRE(descs && chunk_ptr, "null pointer");
         hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(256), 0, s, ntens, descs, chunk_ptr, lr, beta1, beta2,
-                           (float)eps, (float)weight_decay, (const float*)step, grad_scale, found_inf, sq_partial);
+                           (float)eps, hyper ? 0.f : (float)weight_decay, (const float*)step, grad_scale, found_inf,
+                           sq_partial, hyper, weight_decay);
     }
     hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(1), 0, s, step, found_inf);
     return pg::check_launch("pg_adam_f32");

@@ -892,6 +892,24 @@ def head(h: torch.Tensor, W1, b1, W2, b2, eps: float):
     return logp, emb
 
 
+_LABELS_OK: dict = {}  # (data_ptr, numel, _version, C) of label tensors already checked
+
+
+def _check_labels(y: torch.Tensor, C: int):
+    """Raise like F.nll_loss on a label outside [0, C) (protgram_directgcn_trainer.py:95). One host sync per label
+    tensor (cached by address, size and version; the trainer's labels are fixed), none inside a HIP-graph capture,
+    where the kernel's NaN loss is the signal."""
+    key = (y.data_ptr(), y.numel(), y._version, C)
+    if key in _LABELS_OK or y.numel() == 0 or torch.cuda.is_current_stream_capturing():
+        return
+    lo, hi = torch.aminmax(y)
+    if int(lo) < 0 or int(hi) >= C:
+        raise IndexError(f"head_train: label out of range [0, {C}): min {int(lo)}, max {int(hi)}")
+    if len(_LABELS_OK) > 64:
+        _LABELS_OK.clear()
+    _LABELS_OK[key] = True
+
+
 def head_train(h: torch.Tensor, W1, b1, W2, b2, y: torch.Tensor, weight: float = 1.0, drop_p: float = 0.0,
                seed: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None):
     """pg_head_train_f32: the prediction head's training step (decoder Linear -> ReLU -> Dropout -> Linear,
@@ -916,6 +934,7 @@ def head_train(h: torch.Tensor, W1, b1, W2, b2, y: torch.Tensor, weight: float =
     work = torch.empty(max(nwork, 4), device=dev, dtype=torch.float32)
     if drop_p > 0 and seed is None:
         raise ValueError("head_train: dropout needs a seed tensor")
+    _check_labels(y, C)
     rc = lib.pg_head_train_f32(M, Fd, H, C, _p(h), h.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), _p(y),
                                float(weight) / max(M, 1), float(drop_p), _p(seed), _p(scale), _p(dh), dh.stride(0),
                                _p(grads), _p(loss), _p(work), work.numel(), _stream(h))
@@ -973,6 +992,8 @@ def _bwd32(fn):
         with torch.autocast("cuda", enabled=False):
             return fn(ctx, *grads)
     return backward
+
+
 class Propagate3(torch.autograd.Function):
     """x [N, F] -> Z [N, 3F] = [A_in x | A_out x | A_und x]; backward = transposed propagation."""
 
@@ -1147,6 +1168,7 @@ class PropagateDense(torch.autograd.Function):
     res = the layer's residual is x itself (identity), drop = the fused layer dropout (p, seed) or None."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, x, g: CSRGraph, res: bool, constant, gate_mode, act, slope, drop, *params):
         prm = dict(zip(_DENSE_KEYS, params))
         Z = spmm3(g, x)
@@ -1159,6 +1181,7 @@ class PropagateDense(torch.autograd.Function):
         return Y
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dY):
         Z, Y, constant, *params = ctx.saved_tensors
         prm = dict(zip(_DENSE_KEYS, params))

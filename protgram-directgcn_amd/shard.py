@@ -1508,7 +1508,7 @@ class MiddleTrainer:
         seeds = None
         if ops.FUSED_DROPOUT and 0.0 < p_drop < 1.0 and x_full.is_cuda:
             seeds = torch.randint(0, 1 << 62, (L,), device=x_full.device, dtype=torch.int64)
-            seeds ^= (mp.m0 + 1) << 40
+            seeds ^= ((mp.m0 + 1) * 0x9E3779B97F4A7C15) & ((1 << 62) - 1)  # a 62-bit hash of m0: no int64 overflow
         for i, (conv, res) in enumerate(zip(model.convs, model.res_projs)):
             if i == 0:
                 Z = _MidPropagate.apply(X, mp)  # the input carries no gradient
@@ -1568,6 +1568,14 @@ class MiddleTrainer:
             self._y.copy_(y_own)
         if self._xb is not None:
             self._bf16_input(self._x)  # refreshed outside the graph when x changed (no-op otherwise)
+        # train.Adam's lr / weight_decay are device scalars refreshed here, outside the graph, so a schedule that
+        # changed the learning rate since the last replay (train.fit's ReduceLROnPlateau) takes effect now; another
+        # optimizer whose settings changed is captured again
+        if not self._train.replay_ready(self.opt, self._snap):
+            torch.cuda.synchronize()
+            self._graph = self._keep = None
+            self._capture(self._x, self._y)
+            return self._loss
         self._graph.replay()
         return self._loss
 
@@ -1579,8 +1587,12 @@ class MiddleTrainer:
         self._keep = None
         self._eager_steps = 0
 
+    CHECK = True  # train.check_deferred before the first replay of every capture
+
     def _capture(self, x_full, y_own):
         self._x, self._y = x_full, y_own
+        if isinstance(self.opt, self._train.Adam):
+            self.opt.refresh_hyper()
         self._train.prepare_capture(x_full.device)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -1590,7 +1602,9 @@ class MiddleTrainer:
         # device descriptor lists (and their pinned staging copies, which captured uploads re-read)
         self._keep = (list(getattr(self.opt, "_tl_cache", {}).values()) + list(self._train._LISTS.values()) +
                       self._train.flush_deferred())
-        self._graph = g
+        if self.CHECK:  # every table written after the capture reads back, every address in it is a live block
+            self._train.check_deferred(self._keep)
+        self._graph, self._snap = g, self._train.hyper_snapshot(self.opt)
         g.replay()  # the step the capture recorded
 
     def _step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:

@@ -28,6 +28,10 @@ from . import ops
 from ._lib import check, load_library
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 _DEFERRED: list = []  # (device tensor, host array) uploads of a capture in progress, written after it ends
 _ARENA: dict = {}     # device -> [int64 tensor, next free index]: where a capture's uploads live (prepare_capture)
 
@@ -216,6 +220,40 @@ class Adam(torch.optim.Optimizer):
         # moments sit where they sat before (persistent gradient buffers, or the caching allocator handing the same
         # blocks back) reuses the uploaded descriptors -- no host-side table and no host-to-device copy per step
         self._tl_cache: dict = {}
+        # per parameter group: [device float64 {lr, weight_decay}, the host values last written into it]. The kernel
+        # reads the learning rate from there at run time, so a HIP-graph replay of the step follows a schedule that
+        # changes group["lr"] between replays (ReduceLROnPlateau, protgram_directgcn_trainer.py:84, :102)
+        self._hyper: dict = {}
+
+    def refresh_hyper(self):
+        """Write every group's current ``lr`` / ``weight_decay`` into its device scalars (one fill launch per changed
+        value, stream-ordered, no host sync). Eager steps call it themselves; the owner of a captured step calls it
+        before every replay (GraphedTrainStep, shard.MiddleTrainer). betas and eps stay as captured."""
+        if _capturing():
+            raise RuntimeError("train.Adam.refresh_hyper inside a HIP-graph capture would bake the values into it")
+        for gi, group in enumerate(self.param_groups):
+            h = self._hyper.get(gi)
+            if h is None:
+                continue
+            want = (float(group["lr"]), float(group["weight_decay"]))
+            if want[0] < 0 or want[1] < 0:
+                raise ValueError("invalid Adam hyper-parameters")
+            for k in range(2):
+                if h[1] is None or h[1][k] != want[k]:
+                    h[0][k].fill_(want[k])
+            h[1] = want
+
+    def _hyper_ptr(self, gi: int, dev) -> ctypes.c_void_p:
+        h = self._hyper.get(gi)
+        if h is None or h[0].device != dev:
+            if _capturing():
+                raise RuntimeError("train.Adam: a parameter group's first step cannot be inside a HIP-graph capture")
+            self._hyper[gi] = [torch.zeros(2, dtype=torch.float64, device=dev), None]
+        if not _capturing():
+            self.refresh_hyper()
+        elif self._hyper[gi][1] != (float(self.param_groups[gi]["lr"]), float(self.param_groups[gi]["weight_decay"])):
+            raise RuntimeError("train.Adam: lr / weight_decay changed without refresh_hyper() before this capture")
+        return ctypes.c_void_p(self._hyper[gi][0].data_ptr())
 
     def _tensor_list(self, fields) -> TensorList:
         key = tuple((t.data_ptr(), t.numel()) for f in fields for t in f)
@@ -283,7 +321,7 @@ class Adam(torch.optim.Optimizer):
         want_sq = getattr(self, "_want_sqsum", False)
         sq_parts = []
         group_parts: List[list] = []
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             group_parts.append([])
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -305,6 +343,7 @@ class Adam(torch.optim.Optimizer):
             dev = ps[0].device
             gs = grad_scale.to(dev) if grad_scale is not None else None
             fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
+            hyper = self._hyper_ptr(gi, dev)
             for members, step in self._cohorts(ps):
                 grads = [p.grad.contiguous() for p in members]
                 tl = self._tensor_list((members, grads, [self.state[p]["exp_avg"] for p in members],
@@ -315,11 +354,12 @@ class Adam(torch.optim.Optimizer):
                 check(lib.pg_adam_f32(len(members), ctypes.c_void_p(tl.desc.data_ptr()),
                                       ctypes.c_void_p(tl.chunk_ptr.data_ptr()), tl.nchunks, float(group["lr"]),
                                       float(b1), float(b2), float(group["eps"]),
-                                      float(group["weight_decay"]) + float(getattr(self, "_l2_extra", 0.0)),
+                                      float(getattr(self, "_l2_extra", 0.0)),  # added to hyper[1] in-kernel
                                       ctypes.c_void_p(step.data_ptr()),
                                       ctypes.c_void_p(gs.data_ptr()) if gs is not None else None,
                                       ctypes.c_void_p(fi.data_ptr()) if fi is not None else None,
-                                      ctypes.c_void_p(tl.partial.data_ptr()) if want_sq else None, _stream(dev)),
+                                      ctypes.c_void_p(tl.partial.data_ptr()) if want_sq else None, hyper,
+                                      _stream(dev)),
                       "pg_adam_f32")
             for p in ps:  # written in place by the kernel: let autograd / version-keyed caches see it
                 torch.autograd.graph.increment_version(p)
@@ -420,6 +460,25 @@ def _finish_step(model, params, optimizer, loss, l2_lambda, scaler, scaled, back
     return total + l2_lambda * l2 if l2 is not None else total
 
 
+def hyper_snapshot(optimizer) -> tuple:
+    """The host-side hyper-parameters a captured optimizer launch bakes in (every group's scalar settings)."""
+    return tuple(tuple(sorted((k, v) for k, v in g.items() if k != "params" and isinstance(v, (int, float, tuple))))
+                 for g in optimizer.param_groups)
+
+
+def replay_ready(optimizer, snapshot: tuple) -> bool:
+    """Before replaying a captured step: True when the graph still applies the optimizer's current settings.
+    train.Adam reads lr / weight_decay from device scalars, which this refreshes (outside the graph); any other
+    optimizer's captured launches carry the capture-time values, so a changed lr (or other setting) means the
+    step must be captured again (False)."""
+    if isinstance(optimizer, Adam):
+        optimizer.refresh_hyper()
+        snap = hyper_snapshot(optimizer)
+        strip = lambda sn: tuple(tuple(kv for kv in g if kv[0] not in ("lr", "weight_decay")) for g in sn)
+        return strip(snap) == strip(snapshot)
+    return hyper_snapshot(optimizer) == snapshot
+
+
 class GraphedTrainStep:
     """train_step(model, data, y, optimizer, l2_lambda, scaler) replayed from a HIP graph: `WARM` eager steps (the
     caches the step builds on first use: the COO -> CSR conversion and tile plans, Adam's state and descriptor lists,
@@ -428,22 +487,36 @@ class GraphedTrainStep:
     the GPU idle between the backward's launches (host-side autograd work); the replay does not. Dropout draws fresh
     masks per replay (the capture registers the default generator's Philox offset). The inputs are static: `data.x`
     and `y` are read where they were at capture (copy new values into them). Returns the loss as the graph's static
-    device scalar, overwritten by the next call. A step that cannot be captured (a host sync inside it) falls back to
-    eager steps, with a message on stderr."""
+    device scalar, overwritten by the next call.
+
+    Learning-rate schedules: with train.Adam the replay reads lr / weight_decay from the optimizer's device scalars,
+    refreshed before every replay, so ReduceLROnPlateau (fit(), trainer :84, :102) acts on the next step exactly as
+    in eager steps; any other optimizer is captured again when one of its settings changes.
+
+    Safety: before the first replay every descriptor table written after the capture is read back and every address
+    it holds is checked against the allocator's live blocks (check_deferred; CHECK = False skips it). A step that
+    cannot be captured raises (RuntimeError); with eager_fallback=True it runs eagerly instead and the reason is
+    kept in `failed`."""
     WARM = 3
-    CHECK = False  # check_deferred before the first replay (debug)
+    CHECK = True  # check_deferred before the first replay of every capture
 
     def __init__(self, model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None,
-                 weight: float = 1.0):
+                 weight: float = 1.0, eager_fallback: bool = False):
         self.args = (model, data, y, optimizer)
         self.kw = dict(l2_lambda=l2_lambda, scaler=scaler, weight=weight)
         self._graph, self._loss, self._keep, self._eager = None, None, None, 0
+        self._snap = None
+        self.eager_fallback = bool(eager_fallback)
         self.failed = None
+        self.captures = 0
 
     def __call__(self) -> torch.Tensor:
         if self._graph is not None:
-            self._graph.replay()
-            return self._loss
+            if replay_ready(self.args[3], self._snap):
+                self._graph.replay()
+                return self._loss
+            self.close(keep_warm=True)  # a setting the graph baked in changed: capture this step again
+            return self._capture()
         if self.failed is not None or self._eager < self.WARM:
             self._eager += 1
             return train_step(*self.args, **self.kw)
@@ -452,17 +525,21 @@ class GraphedTrainStep:
     def _capture(self) -> torch.Tensor:
         import sys
         opt = self.args[3]
+        if isinstance(opt, Adam):
+            opt.refresh_hyper()
         prepare_capture(self.args[2].device)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 loss = train_step(*self.args, **self.kw)
-        except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
+        except Exception as e:  # noqa: BLE001 -- re-raised unless the caller asked for the eager fallback
             _DEFERRED.clear()
             _CAPTURED_LISTS.clear()
             _ARENA.clear()
             self.failed = repr(e)[:300]
+            if not self.eager_fallback:
+                raise RuntimeError(f"GraphedTrainStep: HIP graph capture failed: {self.failed}") from e
             print(f"[GraphedTrainStep] HIP graph capture failed ({self.failed}); running eager steps", file=sys.stderr)
             torch.cuda.synchronize()
             return train_step(*self.args, **self.kw)
@@ -471,11 +548,63 @@ class GraphedTrainStep:
         self._keep = list(getattr(opt, "_tl_cache", {}).values()) + list(_LISTS.values()) + flush_deferred()
         if self.CHECK:
             check_deferred(self._keep)
-        self._graph, self._loss = g, loss
+        self._graph, self._loss, self._snap = g, loss, hyper_snapshot(opt)
+        self.captures += 1
         g.replay()  # the step the capture recorded
         return loss
 
-    def close(self):
-        """Drop the graph (later calls capture again after WARM eager steps)."""
+    def close(self, keep_warm: bool = False):
+        """Drop the graph (later calls capture again, after WARM eager steps unless keep_warm)."""
         torch.cuda.synchronize()
-        self._graph, self._loss, self._keep, self._eager = None, None, None, 0
+        self._graph, self._loss, self._keep = None, None, None
+        if not keep_warm:
+            self._eager = 0
+
+
+class EarlyStopper:
+    """The reference trainer's early stopper (protgram_directgcn_trainer.py:48-65): stop once the loss has not
+    improved on the best by more than min_delta for `patience` consecutive checks."""
+
+    def __init__(self, patience: int = 1, min_delta: float = 0):
+        self.patience = patience
+        self.min_delta = min_delta
+        self.counter = 0
+        self.best_loss = float("inf")
+
+    def early_stop(self, validation_loss: float) -> bool:
+        if validation_loss < self.best_loss - self.min_delta:
+            self.best_loss = validation_loss
+            self.counter = 0
+            return False
+        self.counter += 1
+        return self.counter >= self.patience
+
+
+def fit(step, optimizer, epochs: int, *, use_lr_scheduler: bool = True, lr_patience: int = 10,
+        lr_factor: float = 0.5, use_early_stopping: bool = True, es_patience: int = 25, es_min_delta: float = 1e-5,
+        scheduler=None, on_epoch=None) -> List[dict]:
+    """The reference's full-batch epoch loop (protgram_directgcn_trainer.py:76-108) around any step callable that
+    returns the step's total loss as a device scalar: ``train_step`` (eager), a ``GraphedTrainStep``, or a bound
+    ``shard.MiddleTrainer.step`` / ``ShardedTrainer.step`` (all ranks see the same all-reduced loss, so they take
+    the same scheduler and stopping decisions). Per epoch: step -> ``scheduler.step(loss)`` (ReduceLROnPlateau
+    'min', the trainer's patience / factor, config.py:77-79) -> early stop on ``loss.item()`` (EarlyStopper, config.py
+    :81-83). The defaults are the reference configuration's. `scheduler` replaces the default ReduceLROnPlateau (any
+    object with step(metric)). Returns one record per epoch: loss (float) and the learning rates the step used."""
+    if scheduler is None and use_lr_scheduler:
+        scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, "min", patience=lr_patience,
+                                                               factor=lr_factor)
+    stopper = EarlyStopper(patience=es_patience, min_delta=es_min_delta) if use_early_stopping else None
+    history = []
+    for epoch in range(1, epochs + 1):
+        lrs = [float(g["lr"]) for g in optimizer.param_groups]
+        loss = step()
+        value = float(loss)  # the reference's one host sync per epoch (scheduler.step(loss), loss.item())
+        history.append(dict(epoch=epoch, loss=value, lr=lrs))
+        if scheduler is not None:
+            scheduler.step(value)
+        if on_epoch is not None:
+            on_epoch(history[-1])
+        if stopper is not None and stopper.early_stop(value):
+            history[-1]["stopped"] = True
+            break
+    return history

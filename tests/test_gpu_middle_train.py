@@ -230,6 +230,41 @@ def test_middle_trainer_hip_graph_matches_eager(pkg, cuda, bf16):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("bf16", [False, True])
+def test_middle_trainer_hip_graph_follows_lr_schedule(pkg, cuda, bf16):
+    """VERDICT r05 item 1 for config 5's fast path: train.fit (the reference loop's ReduceLROnPlateau + EarlyStopper,
+    protgram_directgcn_trainer.py:76-108) around MiddleTrainer.step, the scheduler forced to halve the learning rate
+    after every epoch. With graphs=True the step is captured once and every replay reads the refreshed device lr: the
+    losses, learning rates and parameters equal the eager steps' bit for bit (rank 0 of 2 at 3-gram, the collectives
+    no-ops). Early stopping ends both runs at the same epoch."""
+    from protgram_directgcn_amd import shard, train
+    from test_gpu_configs import _labels, _model
+    n, dims = 3, [64, 64, 32]
+    N, s_, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s_, d, c, device=cuda)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(5)).to(cuda)
+    y = _labels(N, n).to(cuda)
+    mp_ = shard.middle_partition(g, 0, 2)
+    res = []
+    for graphs in (False, True):
+        m = _model(pkg, dims, N, n).to(cuda).eval()
+        if bf16:
+            m.compute_dtype = torch.bfloat16
+        tr = shard.MiddleTrainer(m, mp_, lr=1e-2, l2_lambda=1e-3, comm=_NoComm(), graphs=graphs)
+        sched = torch.optim.lr_scheduler.ReduceLROnPlateau(tr.opt, "min", patience=0, factor=0.5, threshold=0.99)
+        yo = y[mp_.own]
+        hist = train.fit(lambda: tr.step(x, yo), tr.opt, 9, scheduler=sched, es_patience=7, es_min_delta=0.0)
+        torch.cuda.synchronize()
+        assert (tr._graph is not None) == graphs
+        res.append((hist, [p.detach().clone() for p in tr.params]))
+        tr.close()
+    lrs = [h["lr"][0] for h in res[0][0]]
+    assert lrs[:4] == [1e-2 * 0.5 ** i for i in range(4)], lrs
+    assert res[0][0] == res[1][0], res
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bf16", [False, True])
 def test_middle_trainer_fused_dropout_matches_masked(pkg, cuda, bf16, monkeypatch):
     """MiddleTrainer.forward in training mode with the layer dropout fused into the rank's dense launches
     (ops.FUSED_DROPOUT, seeds salted by the rank's first middle) against the same forward with F.dropout replaced by

@@ -1091,6 +1091,75 @@ def test_graphed_train_step_matches_eager(pkg, cuda, amp, adam):
         assert torch.equal(runs[1][1][k], v), k
 
 
+@pytest.mark.parametrize("amp,adam", [(False, True), (True, True), (False, False)])
+def test_graphed_train_step_follows_lr_schedule(pkg, cuda, amp, adam):
+    """the reference loop's ReduceLROnPlateau (protgram_directgcn_trainer.py:84, :102) through
+    train.fit around a captured step. The scheduler is forced to halve the learning rate after every epoch (patience
+    0, a 99 % relative threshold no loss meets), so eight epochs run at eight learning rates: the GraphedTrainStep
+    (captured after its warm-up steps, train.Adam reading lr from its device scalars; torch SGD captured again at
+    every change) gives the same losses, learning rates and parameters, bit for bit, as eager train_step calls."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        opt = train.Adam(m.parameters(), lr=1e-2) if adam else torch.optim.SGD(m.parameters(), lr=5e-2)
+        scaler = torch.amp.GradScaler("cuda", enabled=amp)
+        sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "min", patience=0, factor=0.5, threshold=0.99)
+        if graphed:
+            st = train.GraphedTrainStep(m, data, y, opt, l2_lambda=1e-3, scaler=scaler)
+        else:
+            st = lambda: train.train_step(m, data, y, opt, l2_lambda=1e-3, scaler=scaler)  # noqa: E731
+        hist = train.fit(st, opt, 8, scheduler=sched, use_early_stopping=False)
+        if graphed:
+            assert st._graph is not None and st.failed is None
+            # train.Adam: one capture, the replays read the refreshed device lr; SGD: captured again per change
+            assert st.captures == (1 if adam else 8 - train.GraphedTrainStep.WARM), st.captures
+            st.close()
+        runs.append((hist, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    lrs = [h["lr"][0] for h in runs[0][0]]
+    assert lrs == [lrs[0] * 0.5 ** i for i in range(8)], lrs  # the schedule did act every epoch
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    for k, v in runs[0][1].items():
+        assert torch.equal(runs[1][1][k], v), k
+
+
+def test_graphed_train_step_capture_failure_raises(pkg, cuda):
+    """a step that cannot be captured (here: a host sync inside it) raises instead of silently
+    running eager steps; eager_fallback=True keeps the old behaviour, with the reason in `failed`."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(2)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 32, generator=torch.Generator().manual_seed(3)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 20) % 20
+    data = pkg.Data(x=x, graph=g)
+    torch.manual_seed(0)
+    m = pkg.ProtGramDirectGCN([32, 32], N, 20, 2, 0, 512, 0.5, True).to(cuda).eval()
+    opt = train.Adam(m.parameters(), lr=1e-3)
+
+    class SyncingOpt(torch.optim.SGD):  # a host sync in the step: not capturable
+        def step(self, closure=None):
+            float(self.param_groups[0]["params"][0].sum())
+            return super().step(closure)
+
+    opt = SyncingOpt(m.parameters(), lr=1e-3)
+    st = train.GraphedTrainStep(m, data, y, opt)
+    for _ in range(train.GraphedTrainStep.WARM):
+        st()
+    with pytest.raises(RuntimeError, match="capture failed"):
+        st()
+    torch.cuda.synchronize()
+    st2 = train.GraphedTrainStep(m, data, y, opt, eager_fallback=True)
+    for _ in range(train.GraphedTrainStep.WARM + 2):
+        loss = st2()
+    assert st2.failed is not None and st2._graph is None and torch.isfinite(loss)
+
+
 @pytest.mark.parametrize("amp", [False, True])
 def test_train_step_adam_folded_l2_matches_reference_loop(pkg, cuda, amp):
     """train.train_step with train.Adam, where the L2 gradient 2*lambda*p rides in the Adam launch as extra weight

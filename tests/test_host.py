@@ -24,7 +24,26 @@ def test_library_exports_every_header_symbol(pkg):
         assert hasattr(lib, n), n
     from protgram_directgcn_amd import _lib
     assert names == set(_lib.SIGNATURES), "ctypes table out of sync with the header"
-    assert lib.pg_abi_version() == 2
+    assert lib.pg_abi_version() == 3
+
+
+def test_dgrad_kernels_have_no_packed_fp32_ops():
+    """packed-FP32 VALU ops (v_pk_fma_f32 / v_pk_mul_f32) next to the bf16 dgrad kernel's 32x32x16
+    MFMAs gave timing-dependent gate gradients; pg_dense_bwd.hip is built with -fno-slp-vectorize.
+    The built object's dgrad kernels must hold none (the Makefile runs the same check before linking), and the
+    audit itself must see such ops where they are legal (the head kernels use them)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import isa_check
+    build = os.path.join(REPO, "protgram-directgcn_amd", "build")
+    obj = os.path.join(build, "pg_dense_bwd.o")
+    if not os.path.exists(obj):
+        pytest.skip("library objects not built here (run __graft_entry__.build())")
+    found = isa_check.kernel_mnemonics(obj, r"dgrad")
+    assert len(found) >= 5 and all("dgrad" in k for k in found)
+    assert not any(found.values()), found
+    head = isa_check.kernel_mnemonics(os.path.join(build, "pg_head.o"), r".")
+    assert sum(head.values()) > 0, "the audit finds no packed-FP32 op anywhere: it would not catch one"
 
 
 def test_abi_argument_errors_without_gpu(pkg):
@@ -274,3 +293,66 @@ def test_ngram_plan_diag3_layout(pkg, n):
         ai, Mi, bi = i // Kn1, (i % Kn1) // K, i % K
         for kk in range(3):
             assert d3[i, kk].item() == ((Mi * K + ai) * K + bi) * 3 + kk, (i, kk)
+
+
+def test_fit_loop_matches_reference_epoch_logic(pkg):
+    """train.fit / train.EarlyStopper restate the reference's epoch loop (protgram_directgcn_trainer.py:48-65,
+    :76-108; config.py:77-83): ReduceLROnPlateau('min', patience, factor) stepped on every epoch's loss, then the
+    early stopper on loss.item(). Driven here by a scripted loss sequence (no GPU): the learning-rate history and the
+    stopping epoch equal a literal transcription of the reference loop over the same losses."""
+    from protgram_directgcn_amd import train
+
+    def reference_loop(losses, epochs, lr0, lr_pat, fac, es_pat, es_delta):
+        p = torch.nn.Parameter(torch.zeros(1))
+        opt = torch.optim.SGD([p], lr=lr0)
+        sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, "min", patience=lr_pat, factor=fac)
+        best, counter, lrs = float("inf"), 0, []
+        for epoch in range(1, epochs + 1):
+            lrs.append(opt.param_groups[0]["lr"])
+            loss = torch.tensor(losses[epoch - 1])
+            sched.step(loss)
+            v = loss.item()
+            if v < best - es_delta:
+                best, counter = v, 0
+            else:
+                counter += 1
+                if counter >= es_pat:
+                    break
+        return lrs
+
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        losses = list(np.float32(np.maximum.accumulate(rng.random(60))[::-1] * 3 + rng.random(60) * 0.2))
+        lr_pat, es_pat = int(rng.integers(0, 4)), int(rng.integers(1, 9))
+        want = reference_loop(losses, 60, 1e-3, lr_pat, 0.5, es_pat, 1e-5)
+        p = torch.nn.Parameter(torch.zeros(1))
+        opt = torch.optim.SGD([p], lr=1e-3)
+        it = iter(losses)
+        hist = train.fit(lambda: torch.tensor(next(it)), opt, 60, lr_patience=lr_pat, lr_factor=0.5,
+                         es_patience=es_pat, es_min_delta=1e-5)
+        assert [h["lr"][0] for h in hist] == want, trial
+        assert [h["loss"] for h in hist] == [float(v) for v in losses[:len(hist)]]
+        assert hist[-1].get("stopped", False) == (len(hist) < 60)
+    # the defaults are the reference configuration's (config.py:77-83)
+    import inspect
+    sig = inspect.signature(train.fit)
+    assert (sig.parameters["lr_patience"].default, sig.parameters["lr_factor"].default) == (10, 0.5)
+    assert (sig.parameters["es_patience"].default, sig.parameters["es_min_delta"].default) == (25, 1e-5)
+
+
+def test_adam_refresh_hyper_guards(pkg):
+    """train.Adam keeps lr / weight_decay in device scalars (read by pg_adam_f32 at run time, so HIP-graph replays
+    follow a schedule): refresh_hyper rejects negative values; groups without a device scalar yet are skipped."""
+    from protgram_directgcn_amd import train
+    p = torch.nn.Parameter(torch.zeros(4))
+    opt = train.Adam([p], lr=1e-3)
+    opt.refresh_hyper()  # nothing stepped yet: no device scalars, nothing to write
+    opt._hyper[0] = [torch.zeros(2, dtype=torch.float64), None]
+    opt.refresh_hyper()
+    assert opt._hyper[0][0].tolist() == [1e-3, 0.0] and opt._hyper[0][1] == (1e-3, 0.0)
+    opt.param_groups[0]["lr"] = 5e-4
+    opt.refresh_hyper()
+    assert opt._hyper[0][0].tolist() == [5e-4, 0.0]
+    opt.param_groups[0]["lr"] = -1.0
+    with pytest.raises(ValueError):
+        opt.refresh_hyper()

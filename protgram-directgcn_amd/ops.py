@@ -425,6 +425,27 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     return Z
 
 
+def spmm3t_ngram_acc_bf16(g: CSRGraph, G: torch.Tensor, dX: torch.Tensor, flags: Optional[int] = None):
+    """dX += sum_k A_k^T G[:, kF:(k+1)F] in place for bf16 G and dX on the 4x4-block transposed n-gram kernel
+    (pg_spmm3t_ngram_bf16 with accumulate: the sum in fp32, dX rounded once), or None when that kernel does not take
+    the call (the caller adds instead). Used by PropagateDense in bf16 mode: dX = the identity residual's dpre + the
+    transposed propagation, one launch and one rounding where autograd ran the kernel and a bf16 add."""
+    fl = default_flags() if flags is None else flags
+    if not (_is_bf16(G) and _is_bf16(dX) and G.is_contiguous() and dX.is_contiguous() and g.shared and g.symmetric
+            and G.size(0) == g.n_rows and dX.size(1) * 3 == G.size(1)
+            and _ngram_ok(g, dX, fl, (64, 128, 256), torch.bfloat16)):
+        return None
+    _require_gpu(G, dX)
+    _require_graph_on(g, G)
+    lib, ng, F = load_library(), g.ngram, dX.size(1)
+    rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, g.n_rows, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 1,
+                                  fl, _stream(G))
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_spmm3t_ngram_bf16")
+    return dX
+
+
 def spmm3_t(g: CSRGraph, G: torch.Tensor, flags: Optional[int] = None) -> torch.Tensor:
     """dX = sum_k A_k^T G[:, kF:(k+1)F] (transposed propagation, backward of spmm3). bf16 G -> bf16 dX.
     Same numerics note as spmm3: the n-gram tile kernels (symmetric graphs with a plan: the off-diagonal transposed
@@ -1171,9 +1192,11 @@ class PropagateDense(torch.autograd.Function):
     @_fwd32
     def forward(ctx, x, g: CSRGraph, res: bool, constant, gate_mode, act, slope, drop, *params):
         prm = dict(zip(_DENSE_KEYS, params))
+        ctx.bf16 = _is_bf16(x)
+        ctx.packs = [] if ctx.bf16 else None  # the bf16 kernels' packed weights, reused by the backward
         Z = spmm3(g, x)
         Y = layer_dense(Z, prm, gate_mode, constant=constant, res_x=x if res else None, act=act, slope=slope,
-                        drop=drop)
+                        drop=drop, packs=ctx.packs)
         ctx.g, ctx.res, ctx.gate_mode, ctx.act, ctx.slope = g, res, gate_mode, act, slope
         ctx.drop_p = drop[0] if drop is not None else 0.0
         ctx.has_const = constant is not None
@@ -1187,6 +1210,8 @@ class PropagateDense(torch.autograd.Function):
         prm = dict(zip(_DENSE_KEYS, params))
         constant = constant if ctx.has_const else None
         g = ctx.g
+        if ctx.bf16:
+            return PropagateDense._backward_bf16(ctx, dY, Z, Y, constant, prm)
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, act=ctx.act, slope=ctx.slope,
                                    span=(g.ngram.diag3(), ctx.res), drop_p=ctx.drop_p)
         if out is None:
@@ -1199,16 +1224,46 @@ class PropagateDense(torch.autograd.Function):
         return (dX if ctx.needs_input_grad[0] else None, None, None, d_const, None, None, None, None, *grads)
 
     @staticmethod
+    def _backward_bf16(ctx, dY, Z, Y, constant, prm):
+        """bf16 mode: the bf16 dense backward, then the transposed propagation accumulated into the identity
+        residual's dpre (spmm3t_ngram_acc_bf16: dX = dpre + sum_k A_k^T dZ_k in fp32, rounded once) -- the autograd
+        path (Propagate3 + LayerDense) ran the same kernel into a fresh buffer and added dpre in a separate bf16 pass."""
+        packs, ctx.packs = ctx.packs, None
+        dpre_f32 = constant is not None and ctx.needs_input_grad[3] and constant.dtype == torch.float32
+        out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, act=ctx.act, slope=ctx.slope, packs=packs,
+                                   drop_p=ctx.drop_p, dpre_f32=dpre_f32)
+        if out is None:
+            raise RuntimeError("PropagateDense: the bf16 dense backward refused a shape supports accepted")
+        grads, d_const, d_res, _, _ = _dense_grads(out, prm, ctx.gate_mode, None, Z, constant,
+                                                   Z.new_empty(0) if ctx.res else None, None,
+                                                   lambda i: ctx.needs_input_grad[8 + i], ctx.needs_input_grad[3])
+        dX = None
+        if ctx.needs_input_grad[0]:
+            if ctx.res:
+                # d_res is dpre itself; the constant's gradient (d_const) is its fp32 copy or a conversion made above
+                if d_const is not None and d_const.data_ptr() == d_res.data_ptr():
+                    d_res = d_res.clone()
+                dX = spmm3t_ngram_acc_bf16(ctx.g, out["dZ"], d_res)
+                if dX is None:
+                    dX = spmm3_t(ctx.g, out["dZ"]) + d_res
+            else:
+                dX = spmm3_t(ctx.g, out["dZ"])
+        return (dX, None, None, d_const, None, None, None, None, *grads)
+
+    @staticmethod
     def supports(g: CSRGraph, x: torch.Tensor, F_out: int, res_x, W_res, rows, fused_norm: bool,
                  flags: Optional[int] = None) -> bool:
         """Whether a layer call takes this path: fp32, a symmetric shared-pattern graph with a middle plan (the
         off-diagonal kernel's domain), F_in % 64 == 0, F_out % 32 == 0, an identity residual (res_x is x) or none,
         no row map, no fused normalisation."""
         fl = default_flags() if flags is None else flags
-        return (x.dtype == torch.float32 and x.is_cuda and not fused_norm and rows is None and W_res is None
-                and (res_x is None or res_x is x) and g.shared and g.symmetric and g.ngram is not None
-                and g.ngram.mplan is not None and g.n_rows == x.size(0) and x.size(1) % 64 == 0 and F_out % 32 == 0
-                and (res_x is None or x.size(1) == F_out) and not (fl & _lib.PG_FLAG_NO_NGRAM))
+        common = (x.is_cuda and not fused_norm and rows is None and W_res is None and (res_x is None or res_x is x)
+                  and g.shared and g.symmetric and g.ngram is not None and g.n_rows == x.size(0)
+                  and (res_x is None or x.size(1) == F_out) and not (fl & _lib.PG_FLAG_NO_NGRAM))
+        if _is_bf16(x):  # bf16: the 4x4-block transposed kernel's widths, the bf16 dense backward's (multiples of 8)
+            return common and x.size(1) in (64, 128, 256) and F_out % 8 == 0
+        return (common and x.dtype == torch.float32 and g.ngram.mplan is not None and x.size(1) % 64 == 0
+                and F_out % 32 == 0)
 
 
 class RowLinear(torch.autograd.Function):

@@ -193,7 +193,6 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
 
     # one step: train.train_step + train.Adam (GPU) vs torch.optim.Adam on the oracle's gradients (CPU)
     torch.optim.Adam(list(p.values()), lr=LR).step()
-    g_gpu = {k: prm.grad.detach().cpu() for k, prm in m.named_parameters()}
     m.zero_grad(set_to_none=True)
     opt = train.Adam(m.parameters(), lr=LR)
     p_pre = {k: prm.detach().cpu().clone() for k, prm in m.named_parameters()}
@@ -213,12 +212,15 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     # sums are ordered differently from the autograd path's g_gpu) plus the L2 gradient Adam folds in
     g_step = {k: prm.grad.detach().cpu() + 2 * LAM * p_pre[k] for k, prm in m.named_parameters()}
     fails = []
-    for k in g_step:  # those gradients against the oracle, as the autograd path's above (per-node rows at a kink aside)
-        got = g_step[k]
+    for k in g_step:  # those gradients against the oracle, as the autograd path's above
+        got, r32, r64 = g_step[k], p[k].grad, p64[k].grad
         if got.dim() >= 1 and got.size(0) == N:
-            got = torch.where(kink_rows.view(-1, *([1] * (got.dim() - 1))), p[k].grad, got)
+            # per-node rows whose decoder pre-activation is within fp32 rounding of ReLU's kink (at most 1e-3 N,
+            # asserted above) take the head kernel's own branch, which the oracle cannot be handed: excluded here
+            keep = ~kink_rows
+            got, r32, r64 = got[keep], r32[keep], r64[keep]
         try:
-            _grad_close_or_as_exact(got, p[k].grad, p64[k].grad, f"train_step grad {k}")
+            _grad_close_or_as_exact(got, r32, r64, f"train_step grad {k}")
         except AssertionError as ex:
             fails.append(str(ex).split("\n")[0])
     assert not fails, "\n".join(fails)
@@ -228,18 +230,46 @@ def test_config3_4gram_training_step_vs_oracle(pkg, cuda, monkeypatch):
     assert calls["pg_spmm3t_ngram_mid_offdiag_f32"] == len(m.convs) - 1, calls
     assert calls["pg_directgcn_dense_bwd_span_f32"] == len(m.convs) - 1 and calls["pg_spmm3t_ngram_f32"] == 0, calls
     assert abs(float(loss_s) - loss_r) <= 1e-5 * abs(loss_r)
+    # The Adam step in two parts, each with a tolerance stated in advance (none taken from the observed errors):
+    # (1) the update itself: the GPU parameters equal torch.optim.Adam (CPU, fp32) applied to the SAME gradients the
+    #     launch used (g_step: train_step's gradients + the folded L2 term) within 3 ulp of the update's operands
+    #     (max(|p|, lr, |p'|)), the kernel folding the L2 term by one FMA where torch adds a rounded product -- it restates
+    #     torch's arithmetic, so this isolates it from the gradients' own error;
+    # (2) against the oracle's step: a gradient within the stated gradient tolerance tol = 2e-5 max|g| + 1e-4 |g| of
+    #     the oracle's moves Adam's first update lr g / (|g| + eps) by at most lr eps tol / (|g| - tol + eps)^2 (up
+    #     to 2 lr where tol reaches |g|). Elements whose step gradient is outside tol -- accepted above only by the
+    #     float64 criterion, or rows at the decoder's ReLU kink -- are covered by (1) and that gradient check; they
+    #     are excluded here and their number is bounded.
     for k, prm in m.named_parameters():
+        ref1 = p_pre[k].clone().requires_grad_(True)
+        ref1.grad = g_step[k].clone()
+        torch.optim.Adam([ref1], lr=LR).step()
+        got = prm.detach().cpu()
+        # the update's roundings that may differ (the device sqrt, the division, the final add: 1 ulp each of the
+        # largest of p_pre, the step (|.| <= ~lr) and the result); plus the fold of the L2 gradient (one FMA in the
+        # kernel, a rounded product and a sum here: g differs by <= 2 ulp of its larger term), which the first update
+        # lr g / (|g| + eps) passes on with slope lr eps / (|g| + eps)^2
+        eps32 = torch.finfo(torch.float32).eps
+        ulp = 1.5 * eps32 * torch.maximum(torch.maximum(p_pre[k].abs(), got.abs()), torch.full_like(got, LR))
+        dg = 2 * eps32 * torch.maximum(g_step[k].abs(), (2 * LAM * p_pre[k]).abs()) + 2 * eps32 * g_step[k].abs()
+        fold = LR * 1e-8 * dg / (g_step[k].abs() + 1e-8) ** 2
+        d1 = (got - ref1.detach()).abs()
+        lim = 2 * ulp + fold + 1e-30
+        if not bool((d1 <= lim).all()):
+            i = int((d1 / lim).flatten().argmax())
+            f = lambda t: float(t.flatten()[i])  # noqa: E731
+            raise AssertionError(f"{k}: Adam update off by {f(d1):.3e} (limit {f(lim):.3e}) vs torch Adam at flat {i}: "
+                                 f"p_pre {f(p_pre[k]):.9e} grad {f(prm.grad.detach().cpu()):.9e} g_step {f(g_step[k]):.9e}"
+                                 f" got {f(got):.9e} torch {f(ref1.detach()):.9e}")
         gref = p[k].grad
-        # the gradient tolerance, or the actual GPU-vs-oracle gradient difference (of either GPU path) where larger
-        delta = torch.maximum(2e-5 * float(gref.abs().max()) + 1e-4 * gref.abs(),
-                              1.5 * torch.maximum((g_gpu[k] - gref).abs(), (g_step[k] - gref).abs()))
-        # Adam's first update is lr * g / (|g| + eps): a gradient within delta of the oracle's moves it by at most
-        # lr * eps * delta / (|g| - delta + eps)^2, or by up to 2 lr where the sign itself is within tolerance
-        sens = torch.where(gref.abs() > delta, LR * 1e-8 * delta / (gref.abs() - delta + 1e-8) ** 2,
+        tol = 2e-5 * float(gref.abs().max()) + 1e-4 * gref.abs()
+        inside = (g_step[k] - gref).abs() <= tol
+        assert int((~inside).sum()) <= max(8, 1e-3 * gref.numel()), (k, int((~inside).sum()))
+        sens = torch.where(gref.abs() > tol, LR * 1e-8 * tol / (gref.abs() - tol + 1e-8) ** 2,
                            torch.full_like(gref, 2 * LR))
-        err = (prm.detach().cpu() - p[k].detach()).abs()
-        bad = err > sens + 1e-6
-        assert not bool(bad.any()), f"{k}: {int(bad.sum())} parameters off, max |d| {float(err.max()):.3e}"
+        err = (got - p[k].detach()).abs()
+        bad = inside & (err > sens + 2 * ulp)
+        assert not bool(bad.any()), f"{k}: {int(bad.sum())} parameters off, max |d| {float(err[inside].max()):.3e}"
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -560,3 +590,88 @@ def test_config5_bf16_4gram_256_training_vs_fp32(pkg, cuda):
     scaler = torch.amp.GradScaler("cuda", enabled=True)
     ls = [float(train.train_step(m, data, y, opt, l2_lambda=LAM, scaler=scaler)) for _ in range(5)]
     assert all(np.isfinite(ls)) and ls[-1] < ls[0], ls
+
+
+# bf16 model-level tolerance, stated here and in DESIGN.md §10: against float64 autograd on the same
+# bf16-rounded input (fp32 parameters and edge weights, exact in float64), every element d of an output or gradient obeys
+#   |d| <= 2^-8 (C_REL |ref| + C_MAX max|ref|)      (max over the tensor)
+# bf16 mode rounds each stored tensor once (RNE, unit roundoff 2^-8 of the stored value): forward x, then per layer Z
+# and h (7 roundings on the path to the log-probs of a 3-layer model): (C_REL, C_MAX) = (8, 2). The backward also rounds
+# dZ (3F wide), dpre and the layer gradient dY per layer, and dY is a sum of the transposed propagation and the
+# residual's gradient: where those cancel, a rounding of 2^-8 of an addend is large against the result, so the per-node
+# gradients (the constant's is dpre itself, elementwise) carry errors proportional to the addends, not to the element:
+# (16, 16) for gradients. Measured on config 5 (profiles/r06_bf16_elementwise.txt): forward max |d| <= 1.4 x 2^-8
+# max|ref|, weight / bias / gate gradients <= 4, the per-node constants' gradients up to 10.4.
+BF16_TOL = {"forward": (8.0, 2.0), "grad": (16.0, 16.0)}
+
+
+def _bf16_close(got, ref, kind, what):
+    """(failure message or None, the largest |d| / 2^-8 max|ref|, the largest |d| / 2^-8 |ref| where |ref| >= max|ref|/16)
+    of one tensor against the stated bf16 tolerance."""
+    c_rel, c_max = BF16_TOL[kind]
+    got, ref = got.detach().double(), ref.detach().double()
+    mx = float(ref.abs().max())
+    bound = 2.0 ** -8 * (c_rel * ref.abs() + c_max * mx)
+    d = (got - ref).abs()
+    r_max = float(d.max()) / (2.0 ** -8 * mx + 1e-300)
+    big = ref.abs() >= mx / 16
+    r_rel = float((d[big] / (2.0 ** -8 * ref.abs()[big])).max()) if bool(big.any()) else 0.0
+    bad = d > bound
+    msg = None
+    if bool(bad.any()):
+        msg = (f"{what}: {int(bad.sum())} of {d.numel()} outside 2^-8 ({c_rel} |ref| + {c_max} max|ref|); max |d| "
+               f"{float(d.max()):.3e}, max|ref| {mx:.3e}")
+    return msg, round(r_max, 3), round(r_rel, 3)
+
+
+@pytest.mark.timeout(900)
+def test_config5_bf16_elementwise_vs_float64(pkg, cuda):
+    """Config 5's model in bf16 mode (4-gram, dims [128, 256, 256, 256], eval-mode dropout): log-probs, embeddings, the
+    input's gradient and EVERY parameter gradient of the trainer's loss (nll + 1e-7 sum ||p||^2), elementwise within
+    the stated bf16 tolerance of float64 autograd (the oracle, on the GPU) on the same bf16-rounded input. The GPU's
+    leaky_relu / ReLU branch choices are handed to the oracle (act_masks) as in config 3: a pre-activation within
+    bf16 rounding of 0 may sit on either side of the kink."""
+    n, dims = 4, [128, 256, 256, 256]
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    m = _model(pkg, dims, N, n).to(cuda).eval()
+    m.compute_dtype = torch.bfloat16
+    xb = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(1234)).to(torch.bfloat16).to(cuda)
+    y = _labels(N, n).to(cuda)
+    xd = xb.clone().requires_grad_(True)
+    h, masks = xd, []
+    for conv, res in zip(m.convs, m.res_projs):  # ProtGramDirectGCN.body (eval) written out, keeping the branches
+        if isinstance(res, torch.nn.Linear):
+            h = conv.fused_forward(h, g, None, res_x=h, W_res=res.weight, b_res=res.bias, act=True)
+        else:
+            h = conv.fused_forward(h, g, None, res_x=h, act=True)
+        assert h.dtype == torch.bfloat16
+        masks.append((h > 0).detach())
+    hook = m.decoder_fc[1].register_forward_hook(lambda mod, inp, out: masks.append((inp[0] > 0).detach()))
+    lp, emb = m.head(h)
+    hook.remove()
+    loss = Fn.nll_loss(lp, y) + LAM * sum(p.norm(2).pow(2) for p in m.parameters())
+    loss.backward()
+    torch.cuda.synchronize()
+
+    ei, w = _csr_coo(g)
+    ei = ei.to(cuda)
+    w64 = [t.to(cuda).double() for t in w]
+    p64 = {k: v.detach().double().requires_grad_(True) for k, v in m.state_dict().items()}
+    x64 = xb.double().requires_grad_(True)
+    lp64, emb64 = oc.model_forward(p64, dims, x64, ei, w64[0], ei, w64[1], ei, w64[2], n_gram_len=n,
+                                   prop=oc.propagate_chunked, act_masks=masks)
+    loss64 = Fn.nll_loss(lp64, y) + LAM * sum(v.norm(2).pow(2) for v in p64.values())
+    loss64.backward()
+    assert abs(float(loss) - float(loss64)) <= 2.0 ** -8 * 8.0 * abs(float(loss64)), (float(loss), float(loss64))
+    res = {"log_probs": _bf16_close(lp, lp64, "forward", "log_probs"),
+           "emb": _bf16_close(emb, emb64, "forward", "embeddings"),
+           "grad x": _bf16_close(xd.grad, x64.grad, "grad", "grad x")}
+    for k, prm in m.named_parameters():
+        res[k] = _bf16_close(prm.grad, p64[k].grad, "grad", f"grad {k}")
+    # the margins against the stated constants: max |d| / 2^-8 max|ref|, and max |d| / 2^-8 |ref| over the elements
+    # with |ref| >= max|ref| / 16
+    print("bf16 vs float64 (max |d| / 2^-8 max|ref|, max |d| / 2^-8 |ref| on large elements):",
+          {k: v[1:] for k, v in res.items()})
+    fails = [v[0] for v in res.values() if v[0]]
+    assert not fails, "\n".join(fails)

@@ -1507,6 +1507,63 @@ def test_propagate_dense_span_backward(pkg, cuda, n, F, res):
     assert_grad_close(out["E"], ref, "E = sum_q Wdiag_q dZ_q (+ dpre)")
 
 
+@pytest.mark.parametrize("n,F,res", [(3, 64, True), (3, 64, False), (4, 128, True), (3, 256, True)])
+def test_propagate_dense_bf16_backward(pkg, cuda, n, F, res):
+    """bf16 mode, a layer whose input needs its gradient (config 5's layers 2 and 3): ops.PropagateDense runs the
+    bf16 dense backward, then the 4x4-block transposed kernel ACCUMULATING into the identity residual's dpre (one fp32
+    sum, one rounding). Against the Propagate3 + LayerDense path (the same transposed kernel into a fresh buffer, then
+    autograd's bf16 add): every parameter gradient bit-identical (the same dense backward); the input gradient within
+    one bf16 rounding (unit roundoff 2^-8) of the float64 sum of its two terms (dpre + A^T dZ on the same dZ), and
+    within the old path's two roundings of it."""
+    from protgram_directgcn_amd import ops
+    N, s, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    torch.manual_seed(3)
+    conv = pkg.DirectGCNLayer(F, F, N, True).to(cuda)
+    with torch.no_grad():
+        gen = torch.Generator().manual_seed(9)
+        for name, p in conv.named_parameters():
+            if name.startswith("C_"):
+                p.copy_((torch.rand(p.shape, generator=gen) + 0.5).to(cuda))
+            elif "bias" in name:
+                p.copy_((torch.rand(p.shape, generator=gen) * 0.2 - 0.1).to(cuda))
+    x0 = torch.randn(N, F, generator=torch.Generator().manual_seed(4)).to(cuda).to(torch.bfloat16)
+    w = torch.randn(N, F, generator=torch.Generator().manual_seed(5)).to(cuda).to(torch.bfloat16)
+    assert ops.PropagateDense.supports(g, x0, F, x0 if res else None, None, None, False)
+    lib = ops.load_library()
+    got = {}
+    for span in (True, False):
+        ops.SPAN_BACKWARD = span
+        try:
+            x = x0.clone().requires_grad_(True)
+            for p in conv.parameters():
+                p.grad = None
+            y = conv.fused_forward(x, g, res_x=x if res else None, act=True)
+            assert y.dtype == torch.bfloat16
+            y.backward(w)
+            got[span] = {"x": x.grad.clone(), **{k: p.grad.clone() for k, p in conv.named_parameters()}}
+        finally:
+            ops.SPAN_BACKWARD = True
+    for k, v in got[False].items():
+        if k != "x":
+            assert torch.equal(got[True][k], v), k
+    # the input gradient from its two bf16 terms, in float64
+    Z = ops.spmm3(g, x0)
+    prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))
+    Y = ops.layer_dense(Z, prm, 0, constant=conv.constant.detach(), res_x=x0 if res else None, act=True)
+    out = ops.layer_dense_backward(w, Z, Y, prm, 0, act=True)
+    t32 = ops.spmm3_t(g, out["dZ"].float()).double()  # the fp32 transposed kernel on the same (exact) dZ values
+    dp = out["dpre"].double() if res else torch.zeros_like(t32)
+    ref = t32 + dp
+    gx, gx_old = got[True]["x"].double(), got[False]["x"].double()
+    # one bf16 rounding (unit roundoff 2^-8) of the fp32 sum, whose own order differs from t32's by fp32 rounding
+    noise = 1e-5 * (t32.abs() + dp.abs())
+    assert bool(((gx - ref).abs() <= 2.0 ** -8 * ref.abs() + noise).all()), float((gx - ref).abs().max())
+    # the autograd path rounds the propagation term, then the sum
+    assert bool(((gx - gx_old).abs() <= 2.0 ** -8 * (2 * ref.abs() + t32.abs()) + 2 * noise).all())
+    del lib
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # ops.head_train (round 5): the prediction head's training step in one kernel
 def _drop_keep(seed: int, M: int, H: int, p: float):

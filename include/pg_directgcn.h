@@ -520,6 +520,16 @@ int pg_head_train_f32(int64_t M, int64_t F, int64_t H, int64_t C, const float* h
                       float drop_p, const int64_t* seed, const float* grad_scale, float* dh, int64_t lddh,
                       float* grads, float* loss, float* work, int64_t work_floats, void* stream);
 
+/* The same step in the model's bf16 mode at F = 256, H = 128, C <= 32 (config 5's head): h and dh are bf16 rows (dh
+ * rounded once); the products run on the bf16 matrix cores with two-term bf16 splits of the fp32 operands (each
+ * product within ~2^-15 relative of fp32), fp32 sums; loss and grads fp32 as pg_head_train_f32. work:
+ * pg_head_train_bf16_workspace floats; other shapes: PG_ERR_UNSUPPORTED (-1 from the workspace query). */
+int64_t pg_head_train_bf16_workspace(int64_t M, int64_t F, int64_t H, int64_t C);
+int pg_head_train_bf16(int64_t M, int64_t F, int64_t H, int64_t C, const uint16_t* h, int64_t ldh, const float* W1,
+                       const float* b1, const float* W2, const float* b2, const int64_t* y, float loss_weight,
+                       float drop_p, const int64_t* seed, const float* grad_scale, uint16_t* dh, int64_t lddh,
+                       float* grads, float* loss, float* work, int64_t work_floats, void* stream);
+
 /* Weight gradient of a row-wise linear map over many rows: out[0 : P*N] = A^T B ([P, N], row-major,
  * the sum running over the M rows of A [M, P] and B [M, N]) and out[P*N : P*N+P] = column sums of A.
  * For y = x W^T + b with A = dy, B = x this is (dW, db) of nn.Linear; the decoder layers of

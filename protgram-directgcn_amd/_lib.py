@@ -150,6 +150,9 @@ SIGNATURES = {
     "pg_head_train_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "pg_head_train_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
                                          c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "pg_head_train_bf16_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "pg_head_train_bf16": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                          c_f32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
 }
 
 _lib = None

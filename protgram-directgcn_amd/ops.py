@@ -966,6 +966,41 @@ def head_train(h: torch.Tensor, W1, b1, W2, b2, y: torch.Tensor, weight: float =
     return loss, dh, (grads[:o1].view(H, Fd), grads[o1:o2], grads[o2:o3].view(C, H), grads[o3:])
 
 
+def head_train_bf16(h: torch.Tensor, W1, b1, W2, b2, y: torch.Tensor, weight: float = 1.0, drop_p: float = 0.0,
+                    seed: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None):
+    """pg_head_train_bf16: head_train for the model's bf16 mode at F = 256 (config 5): h bf16 [M, 256], W1 [128, 256],
+    C <= 32 classes. Returns (loss, dh bf16 [M, 256] = d(scale * loss)/dh rounded once, grads (dW1, db1, dW2, db2))
+    or None when the shape is not taken (the caller runs the framework ops on h.float())."""
+    lib = load_library()
+    _require_gpu(h, y)
+    if not _is_bf16(h) or h.dim() != 2:
+        return None
+    M, Fd = h.shape
+    H, C = W1.size(0), W2.size(0)
+    nwork = int(lib.pg_head_train_bf16_workspace(M, Fd, H, C))
+    if nwork < 0:
+        return None
+    h = _bf16c(h)
+    W1, b1, W2, b2 = (_f32c(t.detach()) for t in (W1, b1, W2, b2))
+    y = y.contiguous().to(torch.int64)
+    dev = h.device
+    dh = torch.empty(M, Fd, device=dev, dtype=torch.bfloat16)
+    grads = torch.empty(H * Fd + H + C * H + C, device=dev, dtype=torch.float32)
+    loss = torch.empty((), device=dev, dtype=torch.float32)
+    work = torch.empty(max(nwork, 4), device=dev, dtype=torch.float32)
+    if drop_p > 0 and seed is None:
+        raise ValueError("head_train_bf16: dropout needs a seed tensor")
+    _check_labels(y, C)
+    rc = lib.pg_head_train_bf16(M, Fd, H, C, _p(h), h.stride(0), _p(W1), _p(b1), _p(W2), _p(b2), _p(y),
+                                float(weight) / max(M, 1), float(drop_p), _p(seed), _p(scale), _p(dh), dh.stride(0),
+                                _p(grads), _p(loss), _p(work), work.numel(), _stream(h))
+    if rc == _lib.PG_ERR_UNSUPPORTED:
+        return None
+    check(rc, "pg_head_train_bf16")
+    o1, o2, o3 = H * Fd, H * Fd + H, H * Fd + H + C * H
+    return loss, dh, (grads[:o1].view(H, Fd), grads[o1:o2], grads[o2:o3].view(C, H), grads[o3:])
+
+
 def gemm_at_b(A: torch.Tensor, B: torch.Tensor):
     """pg_gemm_at_b_f32: (A^T B [P, N], column sums of A [P]) over the M rows, or None when the shape is not
     taken (P or N not a multiple of 4)."""

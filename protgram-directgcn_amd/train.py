@@ -396,14 +396,21 @@ def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, 
         # gradient (already scaled by the GradScaler's scale) from the kernel, the decoder parameters theirs
         with torch.amp.autocast("cuda", enabled=use_amp):
             h = model.body(data)
-        hf = h.float()
         W1, b1, W2, b2, p_drop = head
-        seed = torch.randint(0, 2 ** 62, (1,), device=hf.device, dtype=torch.int64) if p_drop > 0 else None
+        seed = torch.randint(0, 2 ** 62, (1,), device=h.device, dtype=torch.int64) if p_drop > 0 else None
         scale = None
         if scaled:
-            scaler.scale(torch.zeros((), device=hf.device))  # the scale tensor exists from here on
+            scaler.scale(torch.zeros((), device=h.device))  # the scale tensor exists from here on
             scale = scaler._scale
-        r = ops.head_train(hf, W1, b1, W2, b2, y, weight, p_drop, seed, scale) if hf.is_cuda else None
+        # bf16 mode at F = 256 (config 5): the kernel reads the bf16 h and returns its bf16 gradient (no widened copy
+        # either way); else the fp32 kernel on h.float() (F = 128)
+        r = None
+        if h.is_cuda and h.dtype == torch.bfloat16:
+            r = ops.head_train_bf16(h, W1, b1, W2, b2, y, weight, p_drop, seed, scale)
+            hf = h
+        if r is None:
+            hf = h.float()
+            r = ops.head_train(hf, W1, b1, W2, b2, y, weight, p_drop, seed, scale) if hf.is_cuda else None
         if r is not None:
             loss, dh, grads = r
             for prm, gr in zip((W1, b1, W2, b2), grads):

@@ -1623,6 +1623,108 @@ def test_head_train_vs_float64(pkg, cuda, M, drop, scaled, F):
         assert_grad_close(got.cpu(), ref.float(), f"head_train {what}")
 
 
+@pytest.mark.parametrize("M,drop,scaled", [(3001, 0.0, False), (16, 0.0, False), (1000, 0.5, False), (777, 0.5, True),
+                                           (20000, 0.25, False), (160000, 0.5, False)])
+def test_head_train_bf16_vs_float64(pkg, cuda, M, drop, scaled):
+    """ops.head_train_bf16 (config 5's head: bf16 h [M, 256], hidden 128, 20 classes) against float64 autograd on the
+    same bf16 h: loss, dh (bf16) and the four decoder gradients, with the dropout mask restated on the host and, when
+    scaled, a GradScaler-style loss scale on every gradient. Stated bounds: the kernel's products use
+    two-term bf16 splits (each within ~3 2^-16 of the exact product, fp32 sums), so the fp32 outputs obey
+    |d| <= 2^-12 (|ref| + max|ref|) and the loss 2^-12 relative; dh is rounded once to bf16:
+    |d| <= 2^-8 |ref| + 2^-12 max|ref|."""
+    from protgram_directgcn_amd import ops
+    F, H, C, weight = 256, 128, 20, 0.75
+    gen = torch.Generator().manual_seed(M)
+    h = torch.randn(M, F, generator=gen).to(torch.bfloat16)
+    W1, b1 = torch.randn(H, F, generator=gen) * 0.1, torch.randn(H, generator=gen) * 0.1
+    W2, b2 = torch.randn(C, H, generator=gen) * 0.2, torch.randn(C, generator=gen) * 0.1
+    y = torch.randint(0, C, (M,), generator=gen)
+    seed = 0x1234_5678_9abc_def0 + M
+    seed_t = torch.tensor([seed], dtype=torch.int64, device=cuda)
+    s = 1024.0 if scaled else 1.0
+    scale_t = torch.tensor(s, device=cuda) if scaled else None
+    r = ops.head_train_bf16(h.to(cuda), W1.to(cuda), b1.to(cuda), W2.to(cuda), b2.to(cuda), y.to(cuda), weight, drop,
+                            seed_t if drop > 0 else None, scale_t)
+    assert r is not None
+    z = functools.partial(torch.zeros, device=cuda)
+    assert ops.head_train_bf16(z(4, 128, dtype=torch.bfloat16), z(64, 128), z(64), z(C, 64), z(C), y[:4].to(cuda)) is None
+    loss, dh, grads = r
+    assert dh.dtype == torch.bfloat16
+    torch.cuda.synchronize()
+    ps = [t.double().to(cuda).requires_grad_(True) for t in (h, W1, b1, W2, b2)]
+    zr = ps[0] @ ps[1].t() + ps[2]
+    zr.retain_grad()
+    a = torch.relu(zr)
+    keep = _drop_keep(seed, M, H, drop).double().to(cuda) / (1.0 - drop) if drop > 0 else torch.ones_like(zr)
+    lp = torch.log_softmax((a * keep) @ ps[3].t() + ps[4], dim=1)
+    loss_r = torch.nn.functional.nll_loss(lp, y.to(cuda)) * weight
+    (loss_r * s).backward()
+    assert abs(float(loss) - float(loss_r)) <= 2.0 ** -12 * abs(float(loss_r)), (float(loss), float(loss_r))
+    # ReLU's kink: where the exact pre-activation is within the kernel's error of 0 (W1's two-term split leaves
+    # <= 2^-16 |W1| per element: band 2^-14 of the sum of the terms' magnitudes), the kernel's z can fall on the other
+    # side and switch that unit's whole term: dh, dW1 and db1 get the switched term's size as slack
+    with torch.no_grad():
+        hd = ps[0].detach()
+        band = 2.0 ** -14 * (hd.abs() @ ps[1].detach().abs().t() + ps[2].detach().abs())
+        amb = zr.detach().abs() <= band
+        gz = ((torch.log_softmax((a * keep) @ ps[3].t() + ps[4], 1).exp() - torch.nn.functional.one_hot(
+            y.to(cuda), C).double()) * (s * weight / M)) @ ps[3].detach() * keep  # d/da then through the dropout
+        gz_amb = (gz * amb).abs()
+        slack = {"dh": gz_amb @ ps[1].detach().abs(), "dW1": gz_amb.t() @ hd.abs(), "db1": gz_amb.sum(0)}
+        amb_rows = amb.any(1)
+    assert int(amb.sum()) <= max(8, 2e-3 * amb.numel()), int(amb.sum())
+    worst = {}
+    for got, ref, what in [(dh, ps[0].grad, "dh")] + [(g, q.grad, n) for g, q, n in
+                                                       zip(grads, ps[1:], ("dW1", "db1", "dW2", "db2"))]:
+        got, ref = got.double(), ref.detach()
+        mx = float(ref.abs().max())
+        bound = (2.0 ** -8 * ref.abs() + 2.0 ** -12 * mx) if what == "dh" else 2.0 ** -12 * (ref.abs() + mx)
+        bound = bound + slack.get(what, 0.0)
+        d = (got - ref).abs()
+        worst[what] = round(float((d / (2.0 ** -12 * (ref.abs() + mx))).max()), 3)
+        assert bool((d <= bound).all()), (what, float(d.max()), mx)
+    print(f"head_train_bf16 M={M}: max |d| / 2^-12 (|ref| + max|ref|):", worst, "kink rows", int(amb_rows.sum()))
+
+
+def test_train_step_bf16_fused_head_matches_framework_head(pkg, cuda):
+    """bf16 mode with a 256-wide last layer (config 5's head shape): train.train_step runs the prediction head in
+    pg_head_train_bf16 (bf16 h in, bf16 dh out) -- against the framework ops on h.float() (HEAD_FUSED = False): one SGD
+    step in eval mode (no dropout draw) from the same start, the loss within 2^-12 and every parameter gradient
+    within the bf16 model tolerance of test_gpu_configs (2^-8 (16 |ref| + 16 max|ref|)): the kernel's products are
+    within ~2^-15 of fp32's, and dh is rounded to bf16 either way."""
+    from protgram_directgcn_amd import ops, train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    lib = ops.load_library()
+    calls = []
+    real = lib.pg_head_train_bf16
+    runs = []
+    for fused in (False, True):
+        train.HEAD_FUSED = fused
+        try:
+            torch.manual_seed(0)
+            m = pkg.ProtGramDirectGCN([64, 256, 256], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+            m.compute_dtype = torch.bfloat16
+            opt = torch.optim.SGD(m.parameters(), lr=0.0)
+            lib.pg_head_train_bf16 = lambda *a: (calls.append(1), real(*a))[1]
+            loss = float(train.train_step(m, data, y, opt, l2_lambda=0.0))
+            runs.append((loss, {k: p.grad.detach().double().clone() for k, p in m.named_parameters()
+                                if p.grad is not None}))
+        finally:
+            train.HEAD_FUSED = True
+            lib.pg_head_train_bf16 = real
+    assert len(calls) == 1  # the fused run only
+    assert abs(runs[1][0] - runs[0][0]) <= 2.0 ** -12 * abs(runs[0][0]), (runs[0][0], runs[1][0])
+    assert set(runs[0][1]) == set(runs[1][1])
+    for k, ref in runs[0][1].items():
+        got = runs[1][1][k]
+        bound = 2.0 ** -8 * (16 * ref.abs() + 16 * float(ref.abs().max()))
+        assert bool(((got - ref).abs() <= bound).all()), (k, float((got - ref).abs().max()), float(ref.abs().max()))
+
+
 def test_train_step_fused_head_matches_framework_head(pkg, cuda):
     """train.train_step with the head in one kernel (HEAD_FUSED, the default) against the framework ops
     (HEAD_FUSED = False): 3 SGD steps with the L2 gradient (parameter updates linear in the gradients), eval mode (no

@@ -1492,6 +1492,10 @@ class MiddleTrainer:
     def forward(self, x_full: torch.Tensor, need_emb: bool = True):
         """(log_probs, emb) of the owned rows (middle-major) with autograd (emb None when need_emb is False: the step's
         loss reads only the log-probs)."""
+        return self.model.head(self.body(x_full), need_emb=need_emb)
+
+    def body(self, x_full: torch.Tensor) -> torch.Tensor:
+        """The layers over the owned rows (middle-major), with autograd: the input of the prediction head."""
         model, mp = self.model, self.mp
         h = model._apply_pe(x_full)
         if model.compute_dtype == torch.bfloat16:
@@ -1531,7 +1535,37 @@ class MiddleTrainer:
             if drop is None:
                 h_own = F.dropout(h_own, p=model.dropout, training=model.training)
             res_x = h_own
-        return model.head(h_own, need_emb=need_emb)
+        return h_own
+
+    def _fused_head(self, h_own: torch.Tensor, y_own: torch.Tensor):
+        """The prediction head's forward and backward in one kernel where it takes the shape (train.HEAD_FUSED; bf16
+        h at F = 256: ops.head_train_bf16, fp32 at F = 128: ops.head_train): the owned rows' nll summed and divided by
+        the global N (weight = own rows / N), the decoder's gradients assigned, h's gradient handed to autograd's
+        backward. Returns the nll (device scalar) or None (the caller runs the framework ops)."""
+        from . import ops
+        train, model, mp = self._train, self.model, self.mp
+        head = model.head_train_args() if train.HEAD_FUSED else None
+        if head is None or not h_own.is_cuda:
+            return None
+        W1, b1, W2, b2, p_drop = head
+        seed = None
+        if p_drop > 0:  # salted by the rank's first middle, as the layers' seeds
+            seed = torch.randint(0, 1 << 62, (1,), device=h_own.device, dtype=torch.int64)
+            seed ^= ((mp.m0 + 7) * 0xD1B54A32D192ED03) & ((1 << 62) - 1)
+        w = float(h_own.size(0)) / float(mp.n)
+        if h_own.dtype == torch.bfloat16:
+            r = ops.head_train_bf16(h_own, W1, b1, W2, b2, y_own, w, p_drop, seed)
+        else:
+            r = ops.head_train(h_own, W1, b1, W2, b2, y_own, w, p_drop, seed)
+        if r is None:
+            return None
+        loss, dh, grads = r
+        for prm, gr in zip((W1, b1, W2, b2), grads):
+            if prm.requires_grad:
+                prm.grad = gr
+                self._touched.add(id(prm))
+        torch.autograd.backward(h_own, grad_tensors=dh)
+        return loss
 
     WARM = 3
     _xb = None
@@ -1625,10 +1659,13 @@ class MiddleTrainer:
         for p in self.dense + self.node:
             p.grad = None
         self.flat.zero_()
-        lp, _ = self.forward(x_full, need_emb=False)
-        nll = -lp.float().gather(1, y_own.view(-1, 1)).sum() / mp.n
         self._touched = set()
-        nll.backward()
+        h_own = self.body(x_full)
+        nll = self._fused_head(h_own, y_own)  # the head in one kernel (config 5: bf16, F = 256)
+        if nll is None:
+            lp, _ = self.model.head(h_own, need_emb=False)
+            nll = -lp.float().gather(1, y_own.view(-1, 1)).sum() / mp.n
+            nll.backward()
         homes = [(p, h, False) for p, h in zip(self.dense, self._flat_views)]
         if self.graphs:
             homes += [(p, h, True) for p, h in zip(self.node, self._node_grads)]

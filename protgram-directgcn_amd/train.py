@@ -520,6 +520,10 @@ class GraphedTrainStep:
     def __call__(self) -> torch.Tensor:
         if self._graph is not None:
             if replay_ready(self.args[3], self._snap):
+                model, data = self.args[0], self.args[1]
+                x = getattr(data, "x", None)
+                if getattr(model, "_xb", None) is not None and x is not None:
+                    model.bf16_input(x)  # the bf16 mode's cached input, refreshed outside the graph if x changed
                 self._graph.replay()
                 return self._loss
             self.close(keep_warm=True)  # a setting the graph baked in changed: capture this step again

@@ -1130,6 +1130,40 @@ def test_graphed_train_step_follows_lr_schedule(pkg, cuda, amp, adam):
         assert torch.equal(runs[1][1][k], v), k
 
 
+def test_graphed_train_step_bf16_input_refresh(pkg, cuda):
+    """bf16 mode converts a step-invariant input once (ProtGramDirectGCN.bf16_input, cached by tensor and version); a
+    captured step reads that cached copy, so GraphedTrainStep refreshes it before each replay: after new values are
+    copied into data.x between replays, the replayed steps equal eager steps on the same inputs, bit for bit."""
+    from protgram_directgcn_amd import train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x0 = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    x1 = torch.randn(N, 64, generator=torch.Generator().manual_seed(99)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = pkg.ProtGramDirectGCN([64, 64, 64], N, 20, 3, 0, 512, 0.5, True).to(cuda).eval()
+        m.compute_dtype = torch.bfloat16
+        data = pkg.Data(x=x0.clone(), graph=g)
+        opt = train.Adam(m.parameters(), lr=1e-3)
+        st = train.GraphedTrainStep(m, data, y, opt) if graphed else (
+            lambda: train.train_step(m, data, y, opt))  # noqa: E731
+        losses = []
+        for i in range(8):
+            if i == 6:
+                data.x.copy_(x1)  # new input values in place (the captured graph's address)
+            losses.append(float(st()))
+        if graphed:
+            assert st._graph is not None
+            st.close()
+        runs.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+    assert runs[0][0] == runs[1][0], runs
+    assert runs[0][0][6] != runs[0][0][5]
+    for k, v in runs[0][1].items():
+        assert torch.equal(runs[1][1][k], v), k
+
+
 def test_graphed_train_step_capture_failure_raises(pkg, cuda):
     """a step that cannot be captured (here: a host sync inside it) raises instead of silently
     running eager steps; eager_fallback=True keeps the old behaviour, with the reason in `failed`."""

@@ -4,11 +4,16 @@ Same constructor and ``forward()`` signatures, parameter names (so ``state_dict`
 reference), parameter creation order (so ``torch.manual_seed`` gives the reference's init), and error
 behaviour. The arithmetic runs in the gfx950 kernels of ``libpgdgcn.so``:
 
-  layer forward = pg_spmm3_f32 (the 3 adjacencies in one CSR pass: replaces the 6 propagate calls)
+  layer forward = the 3 adjacencies in one pass (replaces the 6 propagate calls): pg_spmm3_ngram_mid_f32 on
+                  complete n-gram graphs (the mapped variant + a residual CSR pass on builder-produced levels),
+                  pg_spmm3_f32 (bit-exact CSR kernel) on any other graph
                 + pg_directgcn_dense_f32 (the 6 Linear calls, biases, gates, constant on MFMA)
 
-``ProtGramDirectGCN`` additionally fuses the residual and ``leaky_relu`` of each block into the dense
-kernel's epilogue. Decoder, log_softmax and the L2 normalisation are small [N, F] torch ops.
+``ProtGramDirectGCN`` additionally fuses the residual, ``leaky_relu`` and (training) the dropout of each block into
+the dense kernel's epilogue. In inference the decoder, log_softmax and the L2 normalisation run in one kernel
+(pg_directgcn_head_f32); in training ``train.train_step`` runs the head's forward and backward in one kernel
+(pg_head_train_f32 at F = 128, pg_head_train_bf16 in bf16 mode at F = 256), and autograd runs the framework ops
+(ops.row_linear, log_softmax) for every other shape.
 """
 from __future__ import annotations
 

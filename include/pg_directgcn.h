@@ -73,6 +73,11 @@ typedef struct pg_edge1 {
 /* SpMM variants: C (default) = per-row-group LDS record window; A = every lane loads the record
  * (PG_FLAG_BCAST_RECORDS); B = block-wide LDS staging of records (PG_FLAG_EDGE_LDS). */
 #define PG_FLAG_BCAST_RECORDS (1u << 7) /* SpMM variant A: every lane of a row group loads the record */
+/* 4x4-block transposed n-gram kernels (pg_spmm3t_ngram_*): features per lane (the column pieces of a plan block go to
+ * the waves of one workgroup; same bits in every variant). Default: 2 for bf16 at F = 256, F / 64 otherwise. */
+#define PG_FLAG_NGRAMT_WIDE (1u << 8)   /* F / 64 features per lane (one wave per plan block) */
+#define PG_FLAG_NGRAMT_HALVES (1u << 4) /* F / 128 features per lane (two 64 * (F / 128)-feature halves), F >= 128 */
+#define PG_FLAG_NGRAMT_NARROW (1u << 3) /* 1 feature per lane (F / 64 pieces of 64 features) */
 #define PG_FLAG_DENSE_PREGATED (1u << 14) /* dense kernels: Z from pg_spmm3_gated_f32 (segments already gated) */
 #define PG_FLAG_DENSE_TILED (1u << 15)    /* dense forward: the tiled fp32 kernel even where the split-bf16 W-stationary
                                             kernels apply (F_out = 128, K = 384 or 256, no row map: the default) */

@@ -16,6 +16,9 @@ PG_FLAG_NO_XCD_REMAP = 1 << 0
 PG_FLAG_EDGE_LDS = 1 << 1
 PG_FLAG_UNROLL4 = 1 << 2
 PG_FLAG_BCAST_RECORDS = 1 << 7
+PG_FLAG_NGRAMT_WIDE = 1 << 8
+PG_FLAG_NGRAMT_NARROW = 1 << 3
+PG_FLAG_NGRAMT_HALVES = 1 << 4
 PG_FLAG_DENSE_PREGATED = 1 << 14
 PG_FLAG_DENSE_TILED = 1 << 15
 PG_FLAG_DENSE_X3 = 1 << 16

@@ -47,6 +47,7 @@ struct NgramP {
     const uint16_t* Xb;  // bf16 mode (BF kernels): X / G and Z / dX as bf16 rows; sums stay fp32, one rounding
     uint16_t* Zb;
     int zk;              // forward: floats between the three output slices (= F, or the full width of a column half)
+    int pieces;          // transposed: column pieces of 64 * VEC features per plan block, one wave each (0 = 1)
 };
 
 template <int VEC>
@@ -297,7 +298,9 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t lb = pg::xcd_logical_block(blockIdx.x, gridDim.x, p.remap != 0);
-    const int64_t wb = lb * 4 + wave;
+    const int pc = p.pieces > 1 ? p.pieces : 1;  // the waves of a workgroup: 4 / pc plan blocks x pc column pieces
+    const int64_t wb = lb * (4 / pc) + wave / pc;
+    const int64_t coff = (int64_t)(wave % pc) * 64 * VEC;
     const int nA = p.K / PA, nB = p.K / PB;
     if (wb >= (p.n_rows / ((int64_t)p.K * p.K)) * nA * nB) return;
     const int64_t M = wb / (nA * nB);
@@ -308,8 +311,8 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
     const int64_t ldgv = p.ldx / VEC;
     const int Fv = p.F / VEC;
     auto gslice = [&](int64_t row, int k) -> V {  // this lane's VEC features of slice k of row `row`
-        if constexpr (BF) return ld_bf<VEC>(p.Xb + row * p.ldx + (int64_t)k * p.F + lane * VEC);
-        else return G[row * ldgv + (int64_t)k * Fv + lane];
+        if constexpr (BF) return ld_bf<VEC>(p.Xb + row * p.ldx + (int64_t)k * p.F + coff + lane * VEC);
+        else return G[row * ldgv + (int64_t)k * Fv + coff / VEC + lane];
     };
     V acc[R];
 #pragma unroll
@@ -335,30 +338,40 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
             for (int j = 0; j < PB; ++j)
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    fma_v<VEC>(acc[i * PB + j], wc[plan_slot(i, j, PB) * 3 + k], xo[j][k]);
-                    fma_v<VEC>(acc[i * PB + j], wc[3 * R + plan_slot(i, j, PB) * 3 + k], xi[i][k]);
+                    const int sl = plan_slot(i, j, PB);
+                    fma_v<VEC>(acc[i * PB + j], wc[sl * 3 + k], xo[j][k]);
+                    fma_v<VEC>(acc[i * PB + j], wc[3 * R + sl * 3 + k], xi[i][k]);
                 }
     }
     const float* __restrict__ ws = W + (int64_t)p.K * 6 * R;
+    // per a-row: its PB rows' diagonal sources and (accumulate) old dX values loaded before any of their stores, so
+    // a wave waits for 4 load round trips here instead of 16 (the stores may alias the loads)
 #pragma unroll
-    for (int i = 0; i < PA; ++i)
+    for (int i = 0; i < PA; ++i) {
+        V xs[PB][3], old[PB];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const int64_t row = (int64_t)(a0 + i) * p.Kn1 + M * p.K + b0 + j;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) xs[j][k] = gslice(row, k);
+            old[j] = zero_v<VEC>();
+            if (p.accumulate) {
+                if constexpr (BF) old[j] = ld_bf<VEC>(p.Zb + row * p.ldz + coff + lane * VEC);
+                else old[j] = reinterpret_cast<const V*>(p.Z + row * p.ldz + coff)[lane];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
             const int r = i * PB + j, sl = plan_slot(i, j, PB);
             const int64_t row = (int64_t)(a0 + i) * p.Kn1 + M * p.K + b0 + j;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) fma_v<VEC>(acc[r], ws[sl * 3 + k], gslice(row, k));
+            for (int k = 0; k < 3; ++k) fma_v<VEC>(acc[r], ws[sl * 3 + k], xs[j][k]);
             V v = acc[r];
-            if constexpr (BF) {
-                uint16_t* dst = p.Zb + row * p.ldz + lane * VEC;
-                if (p.accumulate) v = add_v<VEC>(ld_bf<VEC>(dst), v);
-                st_bf<VEC>(dst, v);
-            } else {
-                V* dst = reinterpret_cast<V*>(p.Z + row * p.ldz) + lane;
-                if (p.accumulate) v = add_v<VEC>(*dst, v);
-                *dst = v;
-            }
+            if (p.accumulate) v = add_v<VEC>(old[j], v);
+            if constexpr (BF) st_bf<VEC>(p.Zb + row * p.ldz + coff + lane * VEC, v);
+            else reinterpret_cast<V*>(p.Z + row * p.ldz + coff)[lane] = v;
         }
+    }
 }
 
 // Plan construction: one thread per CSR row scatters its entries into the row's slots (see the file comment).
@@ -418,7 +431,7 @@ bool pow_ok(int K, int n, int64_t n_rows, int64_t& Kn1, int64_t& Kn2) {
 template <int VEC, bool T, bool BF>
 int launch(const NgramP& p, hipStream_t s, bool gated) {
     const int64_t nwb = (p.n_rows / ((int64_t)p.K * p.K)) * (p.K / PLAN_PA) * (p.K / PLAN_PB);
-    const unsigned nb = (unsigned)((nwb + 3) / 4);
+    const unsigned nb = (unsigned)((nwb * (T && p.pieces > 1 ? p.pieces : 1) + 3) / 4);
     if constexpr (T) {
         hipLaunchKernelGGL((ngram_spmm3t_kernel<VEC, PLAN_PA, PLAN_PB, BF>), dim3(nb), dim3(256), 0, s, p);
     } else {
@@ -445,6 +458,23 @@ int run(NgramP p, bool transposed, bool gated, uint32_t flags, hipStream_t s, co
     const bool al = pg::aligned16(xp) && pg::aligned16(zp) && (p.ldx * eb) % 16 == 0 && (p.ldz * eb) % 16 == 0;
     if (!al || p.ldx < width) return pg::set_error(PG_ERR_UNSUPPORTED, "%s: needs 16-B aligned rows", name);
     int rc = PG_OK;
+    if (transposed && (p.F == 64 || p.F == 128 || p.F == 256)) {
+        // The 4-feature lane at F = 256 (R = 16 float4 accumulators + 24 float4 sources, 2 waves per SIMD) is latency
+        // bound; at 2 features per lane the two 128-feature halves of a plan block go to two waves of one workgroup,
+        // so both read a source row at about the same time (same FMAs per element, same bits:
+        // profiles/r06_tsplit_probe.json). PG_FLAG_NGRAMT_WIDE / _HALVES / _NARROW pick 4 / 2 / 1 features per lane.
+        int vec = (int)(p.F / 64);
+        if (p.F == 256 && BF) vec = 2;
+        if (flags & PG_FLAG_NGRAMT_WIDE) vec = (int)(p.F / 64);
+        if ((flags & PG_FLAG_NGRAMT_HALVES) && p.F >= 128) vec = (int)(p.F / 128);
+        if (flags & PG_FLAG_NGRAMT_NARROW) vec = 1;
+        p.pieces = (int)(p.F / (64 * vec));
+        rc = vec == 4 ? launch<4, true, BF>(p, s, false)
+             : vec == 2 ? launch<2, true, BF>(p, s, false)
+                        : launch<1, true, BF>(p, s, false);
+        if (rc) return rc;
+        return pg::check_launch(name);
+    }
     switch (p.F) {
         case 64:
             if constexpr (BF) rc = launch<1, true, BF>(p, s, false);

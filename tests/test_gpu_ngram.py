@@ -92,7 +92,11 @@ def test_ngram_spmm3t_vs_csr(pkg, cuda, n, keep, F):
     got = ops.spmm3_t(g, G, flags=mid)
     assert_close(got, ref, f"transposed middle-tile n={n} F={F}")
     if F in (64, 128, 256):
-        assert_close(ops.spmm3_t(g, G), ref, f"block4 (default) n={n} F={F}")
+        from protgram_directgcn_amd._lib import PG_FLAG_NGRAMT_HALVES, PG_FLAG_NGRAMT_NARROW, PG_FLAG_NGRAMT_WIDE
+        b4 = ops.spmm3_t(g, G)
+        assert_close(b4, ref, f"block4 (default) n={n} F={F}")
+        for vf in (PG_FLAG_NGRAMT_WIDE, PG_FLAG_NGRAMT_HALVES, PG_FLAG_NGRAMT_NARROW):  # features per lane: same bits
+            assert torch.equal(ops.spmm3_t(g, G, flags=ops.default_flags() | vf), b4), vf
     # the off-diagonal part alone: ref minus sum_k Diag_k G_k
     d3 = g.ngram.diag3()
     assert d3.shape == (N, 3)
@@ -164,6 +168,24 @@ def test_ngram_transposed_bf16(pkg, cuda, n, keep, F, kernel):
         ng = g.ngram
         rc = lib.pg_spmm3t_ngram_mid_bf16(ng.K, ng.n, N, ng.mplan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
                                           dX.data_ptr(), dX.stride(0), 1, ops.default_flags(), ops._stream(dX))
+        assert rc == 0
+        d = (dX.float() - want).abs()
+        bad = d > 2.0 ** -7 * want.abs() + 2.0 ** -7 * ref32.abs() + 1e-6
+        assert not bool(bad.any()), ("accumulate", int(bad.sum()), float(d.max()))
+    if kernel == "block4":
+        # every features-per-lane variant (column pieces of a plan block on the waves of one workgroup) gives the
+        # default's bits; then accumulate through the C ABI on a strided G
+        from protgram_directgcn_amd._lib import PG_FLAG_NGRAMT_HALVES, PG_FLAG_NGRAMT_NARROW, PG_FLAG_NGRAMT_WIDE
+        for vf in (PG_FLAG_NGRAMT_WIDE, PG_FLAG_NGRAMT_HALVES, PG_FLAG_NGRAMT_NARROW):
+            assert torch.equal(ops.spmm3_t(g, G, flags=fl | vf), got), vf
+        lib = load_library()
+        Gw = torch.zeros(N, 3 * F + 8, dtype=torch.bfloat16, device=cuda)
+        Gw[:, :3 * F] = G
+        dX = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda).to(torch.bfloat16)
+        want = dX.float() + ref32
+        ng = g.ngram
+        rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, N, ng.plan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
+                                      dX.data_ptr(), dX.stride(0), 1, fl, ops._stream(dX))
         assert rc == 0
         d = (dX.float() - want).abs()
         bad = d > 2.0 ** -7 * want.abs() + 2.0 ** -7 * ref32.abs() + 1e-6

@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 3  /* 2: pg_layer_args_t gained drop_p / drop_seed (fused layer dropout); 3: pg_adam_f32 hyper */
+#define PG_ABI_VERSION 4  /* 2: pg_layer_args_t gained drop_p / drop_seed (fused layer dropout); 3: pg_adam_f32 hyper;
+                             4: pg_adam_desc_t gained gtype (bf16 gradients) */
 
 #define PG_OK 0
 #define PG_ERR_ARG (-1)
@@ -265,6 +266,13 @@ int pg_spmm3t_ngram_f32(int K, int n, int64_t n_rows, const float* plan, const f
                         float* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
 int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg, int64_t F,
                          uint16_t* dX, int64_t lddx, int accumulate, uint32_t flags, void* stream);
+/* pg_spmm3t_ngram_add_bf16: dX = C + sum_k A_k G[:, kF:(k+1)F] (bf16 rows, the sum in fp32, rounded once): the
+ * accumulate form of pg_spmm3t_ngram_bf16 with the addend C read from its own rows (C may equal dX), so the caller's
+ * C survives -- the bf16 layer backward's dpre, which is both the identity residual's gradient and the per-node
+ * constant's (protgram_directgcn.py:101-112, :213-215). */
+int pg_spmm3t_ngram_add_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg,
+                             int64_t F, const uint16_t* C, int64_t ldc, uint16_t* dX, int64_t lddx, uint32_t flags,
+                             void* stream);
 
 /* N-gram MIDDLE-tile propagation on the fp32 matrix cores (pg_ngram_mid.hip; replaces, on graphs over all K^n
  * n-grams, the six propagate calls of protgram_directgcn.py:101-112, like pg_spmm3_ngram_f32, and is the default
@@ -494,10 +502,11 @@ int pg_multi_axpy_f32(int ntens, const pg_tensor_desc_t* descs, const int64_t* c
  * device scale (gradients are multiplied by 1/scale) and inf flag (update skipped), or NULL. */
 typedef struct pg_adam_desc {
     float* p;
-    const float* g;
+    const void* g;  /* fp32, or bf16 (uint16 bits) when gtype == 1 */
     float* m;
     float* v;
     int64_t numel;
+    int64_t gtype;  /* 0: fp32 gradient; 1: bf16 gradient, widened exactly (ABI 4) */
 } pg_adam_desc_t;
 
 /* sq_partial (optional, [nchunks]): per-chunk sums of p^2 of the parameters BEFORE the update -- the value of the

@@ -116,6 +116,8 @@ SIGNATURES = {
                                                 ctypes.c_int, c_u32, c_vp]),
     "pg_spmm3t_ngram_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
                                             ctypes.c_int, c_u32, c_vp]),
+    "pg_spmm3t_ngram_add_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp,
+                                                c_i64, c_vp, c_i64, c_u32, c_vp]),
     "pg_spmm3t_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
                                      c_vp]),
     "pg_spmm1_f32": (ctypes.c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, ctypes.c_int, c_u32,
@@ -182,7 +184,7 @@ def load_library():
         if fn is None:
             raise NativeLibraryError(f"{_LIB_PATH} does not export {name}")
         fn.restype, fn.argtypes = res, args
-    if lib.pg_abi_version() != 3:
+    if lib.pg_abi_version() != 4:
         raise NativeLibraryError("ABI version mismatch")
     _lib = lib
     return lib

@@ -9,6 +9,7 @@
 //   pg_adam_f32        -- Adam over the list in one launch, optionally with the L2 value of the pre-update
 //                         parameters as per-chunk partials (pg_multi_sum_f32 adds them in fixed order).
 // A list is a device array of pg_tensor_desc_t; work is split into fixed 16K-element chunks.
+#include "pg_bf16_util.h"
 #include "pg_common.h"
 
 namespace {
@@ -158,8 +159,14 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
         p = p + step_size * (m / denom);
     };
     // 16-B accesses when all four arrays allow it (the same per-element arithmetic), scalar tail
-    const bool vec = ((reinterpret_cast<uintptr_t>(t.g) | reinterpret_cast<uintptr_t>(t.p) |
-                       reinterpret_cast<uintptr_t>(t.m) | reinterpret_cast<uintptr_t>(t.v)) & 15) == 0;
+    // a bf16 gradient (gtype 1: the bf16 dense backward's dpre, the per-node constant's gradient) is widened
+    // exactly -- the same fp32 values as its fp32 copy -- and read in 8-B pieces of four
+    const bool gbf = t.gtype == 1;
+    const float* gf = static_cast<const float*>(t.g);
+    const uint16_t* gb = static_cast<const uint16_t*>(t.g);
+    const bool vec = ((reinterpret_cast<uintptr_t>(t.g) & (gbf ? 7 : 15)) |
+                      ((reinterpret_cast<uintptr_t>(t.p) | reinterpret_cast<uintptr_t>(t.m) |
+                        reinterpret_cast<uintptr_t>(t.v)) & 15)) == 0;
     int64_t i0 = beg;
     float sq = 0.f;
     if (skip) {  // L2 value only
@@ -172,7 +179,8 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
         const int64_t n4 = (end - beg) >> 2;
         for (int64_t k = threadIdx.x; k < n4; k += 256) {
             const int64_t i = beg + 4 * k;
-            const float4 g = *reinterpret_cast<const float4*>(t.g + i);
+            const float4 g = gbf ? pgbf::unpack4(*reinterpret_cast<const uint2*>(gb + i))
+                                 : *reinterpret_cast<const float4*>(gf + i);
             float4 p = *reinterpret_cast<const float4*>(t.p + i);
             float4 m = *reinterpret_cast<const float4*>(t.m + i);
             float4 v = *reinterpret_cast<const float4*>(t.v + i);
@@ -190,7 +198,7 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
     for (int64_t i = i0 + threadIdx.x; i < end; i += 256) {
         float p = t.p[i], m = t.m[i], v = t.v[i];
         sq += p * p;
-        upd(t.g[i], p, m, v);
+        upd(gbf ? __uint_as_float((uint32_t)gb[i] << 16) : gf[i], p, m, v);
         t.p[i] = p;
         t.m[i] = m;
         t.v[i] = v;

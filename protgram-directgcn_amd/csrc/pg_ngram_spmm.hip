@@ -48,6 +48,9 @@ struct NgramP {
     uint16_t* Zb;
     int zk;              // forward: floats between the three output slices (= F, or the full width of a column half)
     int pieces;          // transposed: column pieces of 64 * VEC features per plan block, one wave each (0 = 1)
+    const float* C;      // transposed, accumulate: the addend rows (null: Z itself, in place)
+    const uint16_t* Cb;
+    int64_t ldc;
 };
 
 template <int VEC>
@@ -356,8 +359,9 @@ __global__ __launch_bounds__(256) void ngram_spmm3t_kernel(NgramP p) {
             for (int k = 0; k < 3; ++k) xs[j][k] = gslice(row, k);
             old[j] = zero_v<VEC>();
             if (p.accumulate) {
-                if constexpr (BF) old[j] = ld_bf<VEC>(p.Zb + row * p.ldz + coff + lane * VEC);
-                else old[j] = reinterpret_cast<const V*>(p.Z + row * p.ldz + coff)[lane];
+                if constexpr (BF) old[j] = ld_bf<VEC>(p.Cb ? p.Cb + row * p.ldc + coff + lane * VEC
+                                                           : p.Zb + row * p.ldz + coff + lane * VEC);
+                else old[j] = reinterpret_cast<const V*>(p.C ? p.C + row * p.ldc + coff : p.Z + row * p.ldz + coff)[lane];
             }
         }
 #pragma unroll
@@ -610,6 +614,33 @@ int pg_spmm3t_ngram_bf16(int K, int n, int64_t n_rows, const float* plan, const 
     p.F = (int)F;
     p.accumulate = accumulate ? 1 : 0;
     return run<true>(p, true, false, flags, (hipStream_t)stream, "pg_spmm3t_ngram_bf16");
+}
+
+int pg_spmm3t_ngram_add_bf16(int K, int n, int64_t n_rows, const float* plan, const uint16_t* G, int64_t ldg,
+                             int64_t F, const uint16_t* C, int64_t ldc, uint16_t* dX, int64_t lddx, uint32_t flags,
+                             void* stream) {
+    int64_t Kn1 = 0, Kn2 = 0;
+    PG_REQUIRE(pow_ok(K, n, n_rows, Kn1, Kn2) && K % PLAN_PA == 0 && K % PLAN_PB == 0, "bad n-gram shape");
+    PG_REQUIRE(plan && G && C && dX, "null pointer");
+    PG_REQUIRE(ldg >= 3 * F && ldc >= F && lddx >= F, "leading dimensions too small");
+    PG_REQUIRE(pg::aligned16(C) && (ldc * 2) % 16 == 0, "pg_spmm3t_ngram_add_bf16: needs 16-B aligned rows");
+    NgramP p{};
+    p.K = K;
+    p.n = n;
+    p.Kn1 = Kn1;
+    p.Kn2 = Kn2;
+    p.n_rows = n_rows;
+    p.plan = plan;
+    p.blk = blk_floats(K, PLAN_PA, PLAN_PB);
+    p.Xb = G;
+    p.ldx = ldg;
+    p.Zb = dX;
+    p.ldz = lddx;
+    p.Cb = C;
+    p.ldc = ldc;
+    p.F = (int)F;
+    p.accumulate = 1;
+    return run<true>(p, true, false, flags, (hipStream_t)stream, "pg_spmm3t_ngram_add_bf16");
 }
 
 }  // extern "C"

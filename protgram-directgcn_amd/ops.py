@@ -75,6 +75,36 @@ def _require_gpu(*ts):
             raise TypeError(f"unsupported dtype {t.dtype}")
 
 
+# Deferred bf16 gradients (train.train_step in bf16 mode with train.Adam and no GradScaler). The per-node constant's
+# gradient is the layer's dpre (protgram_directgcn.py:130-133: the constant is added to the pre-activation), which
+# the bf16 dense backward stores in bf16 for its weight gradient anyway; instead of a widened fp32 copy as
+# constant.grad (written by the backward, read by Adam: 6 B per element per step, 0.74 GB at config 5), the layer
+# backward leaves the constant's .grad None and files the bf16 dpre here, keyed by the parameter's address, and
+# train.Adam reads it directly (pg_adam_desc_t.gtype = 1; exactly widened: the same update bits). train_step
+# switches this on around its backward and optimizer step only, and empties the table after.
+_DEFER_CONST_GRAD = False
+_DEFERRED_GRADS: dict = {}
+
+
+def deferred_grad(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The bf16 gradient a layer backward filed for parameter p in this train_step (None if none)."""
+    return _DEFERRED_GRADS.get(p.data_ptr()) if _DEFERRED_GRADS else None
+
+
+def _defer_const(constant, need: bool, M: int, rows) -> bool:
+    return (_DEFER_CONST_GRAD and need and constant is not None and constant.dtype == torch.float32 and rows is None
+            and constant.dim() == 2 and constant.size(0) == M and constant.is_contiguous())
+
+
+def _file_deferred(constant, dpre) -> bool:
+    if not (_is_bf16(dpre) and dpre.is_contiguous() and dpre.shape == constant.shape):
+        return False
+    if constant.data_ptr() in _DEFERRED_GRADS:
+        raise RuntimeError("a deferred gradient was filed twice for one parameter")
+    _DEFERRED_GRADS[constant.data_ptr()] = dpre
+    return True
+
+
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -425,24 +455,34 @@ def spmm3_gated(g: CSRGraph, x: torch.Tensor, prm: dict, gate_mode: int, flags: 
     return Z
 
 
-def spmm3t_ngram_acc_bf16(g: CSRGraph, G: torch.Tensor, dX: torch.Tensor, flags: Optional[int] = None):
+def spmm3t_ngram_acc_bf16(g: CSRGraph, G: torch.Tensor, dX: torch.Tensor, flags: Optional[int] = None,
+                          src: Optional[torch.Tensor] = None):
     """dX += sum_k A_k^T G[:, kF:(k+1)F] in place for bf16 G and dX on the 4x4-block transposed n-gram kernel
     (pg_spmm3t_ngram_bf16 with accumulate: the sum in fp32, dX rounded once), or None when that kernel does not take
     the call (the caller adds instead). Used by PropagateDense in bf16 mode: dX = the identity residual's dpre + the
-    transposed propagation, one launch and one rounding where autograd ran the kernel and a bf16 add."""
+    transposed propagation, one launch and one rounding where autograd ran the kernel and a bf16 add. src: the
+    addend read from its own rows instead (dX = src + ..., pg_spmm3t_ngram_add_bf16; src is left as it was)."""
     fl = default_flags() if flags is None else flags
     if not (_is_bf16(G) and _is_bf16(dX) and G.is_contiguous() and dX.is_contiguous() and g.shared and g.symmetric
             and G.size(0) == g.n_rows and dX.size(1) * 3 == G.size(1)
             and _ngram_ok(g, dX, fl, (64, 128, 256), torch.bfloat16)):
         return None
+    if src is not None and not (_is_bf16(src) and src.is_contiguous() and src.shape == dX.shape):
+        return None
     _require_gpu(G, dX)
     _require_graph_on(g, G)
     lib, ng, F = load_library(), g.ngram, dX.size(1)
-    rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, g.n_rows, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0), 1,
-                                  fl, _stream(G))
+    if src is not None:
+        rc = lib.pg_spmm3t_ngram_add_bf16(ng.K, ng.n, g.n_rows, _p(ng.plan), _p(G), G.stride(0), F, _p(src),
+                                          src.stride(0), _p(dX), dX.stride(0), fl, _stream(G))
+        name = "pg_spmm3t_ngram_add_bf16"
+    else:
+        rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, g.n_rows, _p(ng.plan), _p(G), G.stride(0), F, _p(dX), dX.stride(0),
+                                      1, fl, _stream(G))
+        name = "pg_spmm3t_ngram_bf16"
     if rc == _lib.PG_ERR_UNSUPPORTED:
         return None
-    check(rc, "pg_spmm3t_ngram_bf16")
+    check(rc, name)
     return dX
 
 
@@ -1121,11 +1161,15 @@ class LayerDense(torch.autograd.Function):
         W_res = W_res if ctx.has_wres else None
         rows = rows if ctx.has_rows else None
         packs, ctx.packs = ctx.packs, None
+        defer = _is_bf16(dY) and _defer_const(constant, ctx.needs_input_grad[2], Z.size(0), rows)
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, rows=rows, res_x=res_x, W_res=W_res,
                                    act=ctx.act, slope=ctx.slope, need_dZ=ctx.needs_input_grad[0], packs=packs,
                                    drop_p=ctx.drop_p,
                                    dpre_f32=constant is not None and ctx.needs_input_grad[2]
-                                   and constant.dtype == torch.float32)
+                                   and constant.dtype == torch.float32 and not defer)
+        need_const = ctx.needs_input_grad[2]
+        if out is not None and defer and _file_deferred(constant, out["dpre"]):
+            need_const = False
         if out is None:  # bf16 shapes the bf16 kernels do not take: the fp32 kernels on widened copies
             out = layer_dense_backward(dY.float(), Z.float(), Y.float(), prm, ctx.gate_mode, rows=rows,
                                        res_x=None if res_x is None else res_x.float(), W_res=W_res, act=ctx.act,
@@ -1134,8 +1178,7 @@ class LayerDense(torch.autograd.Function):
                 if out[k] is not None:
                     out[k] = out[k].to(torch.bfloat16)
         grads, d_const, d_res, d_wres, d_bres = _dense_grads(out, prm, ctx.gate_mode, rows, Z, constant, res_x, W_res,
-                                                             lambda i: ctx.needs_input_grad[10 + i],
-                                                             ctx.needs_input_grad[2])
+                                                             lambda i: ctx.needs_input_grad[10 + i], need_const)
         return (out["dZ"], d_res, d_const, d_wres, d_bres, None, None, None, None, None, *grads)
 
 
@@ -1264,17 +1307,26 @@ class PropagateDense(torch.autograd.Function):
         residual's dpre (spmm3t_ngram_acc_bf16: dX = dpre + sum_k A_k^T dZ_k in fp32, rounded once) -- the autograd
         path (Propagate3 + LayerDense) ran the same kernel into a fresh buffer and added dpre in a separate bf16 pass."""
         packs, ctx.packs = ctx.packs, None
-        dpre_f32 = constant is not None and ctx.needs_input_grad[3] and constant.dtype == torch.float32
+        defer = _defer_const(constant, ctx.needs_input_grad[3], Z.size(0), None)
+        dpre_f32 = constant is not None and ctx.needs_input_grad[3] and constant.dtype == torch.float32 and not defer
         out = layer_dense_backward(dY, Z, Y, prm, ctx.gate_mode, act=ctx.act, slope=ctx.slope, packs=packs,
                                    drop_p=ctx.drop_p, dpre_f32=dpre_f32)
         if out is None:
             raise RuntimeError("PropagateDense: the bf16 dense backward refused a shape supports accepted")
+        need_const = ctx.needs_input_grad[3]
+        deferred = defer and _file_deferred(constant, out["dpre"])
+        if deferred:
+            need_const = False
         grads, d_const, d_res, _, _ = _dense_grads(out, prm, ctx.gate_mode, None, Z, constant,
                                                    Z.new_empty(0) if ctx.res else None, None,
-                                                   lambda i: ctx.needs_input_grad[8 + i], ctx.needs_input_grad[3])
+                                                   lambda i: ctx.needs_input_grad[8 + i], need_const)
         dX = None
         if ctx.needs_input_grad[0]:
-            if ctx.res:
+            if ctx.res and deferred:  # dpre stays the constant's gradient: dX = dpre + A^T dZ into a new buffer
+                dX = spmm3t_ngram_acc_bf16(ctx.g, out["dZ"], torch.empty_like(d_res), src=d_res)
+                if dX is None:
+                    dX = spmm3_t(ctx.g, out["dZ"]) + d_res
+            elif ctx.res:
                 # d_res is dpre itself; the constant's gradient (d_const) is its fp32 copy or a conversion made above
                 if d_const is not None and d_const.data_ptr() == d_res.data_ptr():
                     d_res = d_res.clone()

@@ -46,7 +46,7 @@ def prepare_capture(dev, n: int = 1 << 16) -> torch.Tensor:
     return t
 
 
-def _upload(a: np.ndarray, dev, keep: Optional[list] = None) -> torch.Tensor:
+def _upload(a: np.ndarray, dev, keep: Optional[list] = None, nptr: Optional[int] = None) -> torch.Tensor:
     """Host array (int64) -> device without a host sync (pinned staging, stream-ordered copy). `keep` receives the
     pinned staging tensor: a copy captured into a HIP graph re-reads it at every replay, so its owner must keep it
     alive. Inside a HIP-graph capture (no pinned allocation is allowed there) the table takes a slice of the arena
@@ -62,7 +62,8 @@ def _upload(a: np.ndarray, dev, keep: Optional[list] = None) -> torch.Tensor:
                                "before capturing")
         t = slot[0][slot[1]:slot[1] + n].view(a.shape)
         slot[1] += (n + 1) // 2 * 2  # 16-B aligned slices
-        _DEFERRED.append((t, np.array(a, copy=True)))
+        # nptr: the table's leading address columns (check_deferred); None: all but the last
+        _DEFERRED.append((t, np.array(a, copy=True), a.shape[1] - 1 if nptr is None and a.ndim == 2 else nptr))
         return t
     h = torch.from_numpy(a).pin_memory()
     if keep is not None:
@@ -74,26 +75,32 @@ class TensorList:
     """Device descriptors + chunk offsets for a list of fp32 tensor groups: field k of descriptor t is the data
     pointer of fields[k][t]; the last int64 is numel (of fields[0][t])."""
 
-    def __init__(self, *fields: List[torch.Tensor]):
+    def __init__(self, *fields: List[torch.Tensor], gtype: bool = False):
+        """gtype: pg_adam_desc_t's trailing gradient-type column (field 1 may then hold bf16 tensors: 1)."""
         lib = load_library()
         xs = fields[0]
         if not xs:
             raise ValueError("empty tensor list")
         dev = xs[0].device
-        for f in fields:
+        for k, f in enumerate(fields):
             for t in f:
-                if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+                ok = t.dtype == torch.float32 or (gtype and k == 1 and t.dtype == torch.bfloat16)
+                if not ok or not t.is_contiguous() or t.device != dev:
                     raise ValueError("tensors must be contiguous fp32 on one device")
-        desc = np.zeros((len(xs), len(fields) + 1), dtype=np.int64)
+        desc = np.zeros((len(xs), len(fields) + 1 + int(gtype)), dtype=np.int64)
         chunks = np.zeros(len(xs) + 1, dtype=np.int64)
         for i, x in enumerate(xs):
             for k, f in enumerate(fields):
                 desc[i, k] = f[i].data_ptr()
-            desc[i, -1] = x.numel()
+            desc[i, len(fields)] = x.numel()
+            if gtype:
+                if any(f[i].numel() != x.numel() for f in fields):
+                    raise ValueError("tensor list fields differ in size")
+                desc[i, -1] = 1 if fields[1][i].dtype == torch.bfloat16 else 0
             chunks[i + 1] = chunks[i] + lib.pg_multi_chunks(x.numel())
         self.fields = fields  # keep the tensors alive while the descriptors may be in use (dropped when cached)
         self.host = []  # the pinned staging copies (see _upload)
-        self.desc = _upload(desc, dev, self.host)
+        self.desc = _upload(desc, dev, self.host, nptr=len(fields))
         self.chunk_ptr = _upload(chunks, dev, self.host)
         self.nchunks = int(chunks[-1])
         self.partial = torch.empty(max(self.nchunks, 1), dtype=torch.float32, device=dev)
@@ -109,9 +116,9 @@ def flush_deferred() -> list:
     Returns what the captured launches read by address -- the written tensors and the TensorLists built during the
     capture, with the tensors their descriptors point to: the owner of the graph keeps them as long as the graph."""
     keep = []
-    for t, a in _DEFERRED:
+    for t, a, nptr in _DEFERRED:
         t.copy_(torch.from_numpy(a))
-        keep.append((t, a))
+        keep.append((t, a, nptr))
     _DEFERRED.clear()
     keep += _CAPTURED_LISTS
     _CAPTURED_LISTS.clear()
@@ -122,7 +129,7 @@ def flush_deferred() -> list:
 
 def check_deferred(keep: list):
     """Debug check of flush_deferred's result before a first replay: every written table reads back as built, and
-    every address in a descriptor table (all but its last column) lies inside a live allocation of the caching
+    every address in a descriptor table (its leading address columns) lies inside a live allocation of the caching
     allocator. Raises instead of letting a replay dereference a stale address."""
     live = []
     for seg in torch.cuda.memory_snapshot():
@@ -137,11 +144,11 @@ def check_deferred(keep: list):
     for item in keep:
         if not isinstance(item, tuple):
             continue
-        t, a = item
+        t, a, nptr = item
         if not torch.equal(t.cpu(), torch.from_numpy(a)):
             raise RuntimeError("a deferred descriptor table does not read back as written")
-        if a.ndim == 2:
-            for ptr in a[:, :-1].reshape(-1).tolist():
+        if a.ndim == 2 and nptr:
+            for ptr in a[:, :nptr].reshape(-1).tolist():
                 i = bisect.bisect_right(starts, ptr) - 1
                 if i < 0 or not (live[i][0] <= ptr < live[i][1]):
                     raise RuntimeError(f"descriptor address {ptr:#x} is not inside a live allocation")
@@ -256,11 +263,12 @@ class Adam(torch.optim.Optimizer):
         return ctypes.c_void_p(self._hyper[gi][0].data_ptr())
 
     def _tensor_list(self, fields) -> TensorList:
-        key = tuple((t.data_ptr(), t.numel()) for f in fields for t in f)
+        key = tuple((t.data_ptr(), t.numel(), t.dtype) for f in fields for t in f)
         tl = self._tl_cache.get(key)
         if tl is None:
-            tl = TensorList(*fields)
-            tl.fields = None  # the descriptors hold addresses only; the key guarantees they are current
+            tl = TensorList(*fields, gtype=True)  # pg_adam_desc_t: field 1 (the gradient) may be bf16
+            if not _capturing():  # a capture's lists keep their tensors (deferred bf16 gradients have no other owner)
+                tl.fields = None  # the descriptors hold addresses only; the key guarantees they are current
             if len(self._tl_cache) >= 16:
                 self._tl_cache.pop(next(iter(self._tl_cache)))
             self._tl_cache[key] = tl
@@ -323,13 +331,15 @@ class Adam(torch.optim.Optimizer):
         group_parts: List[list] = []
         for gi, group in enumerate(self.param_groups):
             group_parts.append([])
-            ps = [p for p in group["params"] if p.grad is not None]
+            ps = [p for p in group["params"] if p.grad is not None or ops.deferred_grad(p) is not None]
             if not ps:
                 continue
             fresh = None
             for p in ps:
-                if p.grad.is_sparse or p.dtype != torch.float32:
+                if (p.grad is not None and p.grad.is_sparse) or p.dtype != torch.float32:
                     raise RuntimeError("train.Adam takes dense fp32 parameters")
+                if p.grad is not None and ops.deferred_grad(p) is not None:
+                    raise RuntimeError("train.Adam: a parameter has both .grad and a deferred bf16 gradient")
                 if p.device != ps[0].device:
                     raise RuntimeError("train.Adam: the parameters of a group must share one device")
                 st = self.state[p]
@@ -345,7 +355,7 @@ class Adam(torch.optim.Optimizer):
             fi = found_inf.to(dev, dtype=torch.float32) if found_inf is not None else None
             hyper = self._hyper_ptr(gi, dev)
             for members, step in self._cohorts(ps):
-                grads = [p.grad.contiguous() for p in members]
+                grads = [p.grad.contiguous() if p.grad is not None else ops.deferred_grad(p) for p in members]
                 tl = self._tensor_list((members, grads, [self.state[p]["exp_avg"] for p in members],
                                         [self.state[p]["exp_avg_sq"] for p in members]))
                 if want_sq:
@@ -382,10 +392,26 @@ class Adam(torch.optim.Optimizer):
 HEAD_FUSED = True
 
 
+# bf16 mode with train.Adam and no GradScaler: the per-node constants' gradients stay the layers' bf16 dpre, read by
+# Adam directly (ops.deferred_grad; the parameters' .grad stay None in this step); False: fp32 .grad as usual
+DEFER_CONST_GRAD = True
+
+
 def train_step(model, data, y: torch.Tensor, optimizer, l2_lambda: float = 0.0, scaler=None, weight: float = 1.0,
                autocast: bool = True) -> torch.Tensor:
     """One step of the reference loop (trainer :91-100, or :129-140 with weight = batch nodes / total nodes).
     Returns the total loss (nll * weight + l2_lambda * sum ||p||^2) as a device scalar."""
+    defer = DEFER_CONST_GRAD and isinstance(optimizer, Adam) and not (scaler is not None and scaler.is_enabled())
+    prev = ops._DEFER_CONST_GRAD
+    ops._DEFER_CONST_GRAD = defer
+    try:
+        return _train_step(model, data, y, optimizer, l2_lambda, scaler, weight, autocast)
+    finally:
+        ops._DEFER_CONST_GRAD = prev
+        ops._DEFERRED_GRADS.clear()
+
+
+def _train_step(model, data, y, optimizer, l2_lambda, scaler, weight, autocast):
     params = [p for p in model.parameters() if p.requires_grad]
     optimizer.zero_grad(set_to_none=True)  # autograd then assigns gradients instead of adding into zeros
     use_amp = autocast and scaler is not None and scaler.is_enabled()
@@ -443,7 +469,7 @@ def _finish_step(model, params, optimizer, loss, l2_lambda, scaler, scaled, back
         add_l2_grad(params, l2_lambda, scale=scaler._scale if scaled else None)  # device-side scale: no sync
     else:  # the reference's (0 *) l2 term gives every parameter a gradient, so it is stepped
         for p in params:
-            if p.grad is None:
+            if p.grad is None and ops.deferred_grad(p) is None:
                 p.grad = torch.zeros_like(p)
     if fold:
         optimizer._l2_extra = 2.0 * l2_lambda

@@ -1759,6 +1759,49 @@ def test_train_step_bf16_fused_head_matches_framework_head(pkg, cuda):
         assert bool(((got - ref).abs() <= bound).all()), (k, float((got - ref).abs().max()), float(ref.abs().max()))
 
 
+def test_train_step_bf16_deferred_constant_grads_bit_identical(pkg, cuda):
+    """bf16 mode + train.Adam, no GradScaler: the per-node constants' gradients stay the layers' bf16 dpre, read by
+    pg_adam_f32 as bf16 (gtype 1) instead of an fp32 .grad copy (train.DEFER_CONST_GRAD). 3 training-mode steps with
+    dropout and the L2 term: losses and every parameter and Adam moment bit-identical to the fp32-.grad run. Layer 1
+    (projected residual) runs LayerDense, layer 2 (identity residual) PropagateDense, whose dX then comes from
+    pg_spmm3t_ngram_add_bf16 (dpre kept intact); the constants' .grad stay None and the table is emptied."""
+    from protgram_directgcn_amd import ops, train
+    N, s, d, c = pkg.synth.de_bruijn_edges(3)
+    g = pkg.build_propagation_csr(N, s, d, c, device=cuda)
+    x = torch.randn(N, 64, generator=torch.Generator().manual_seed(1234)).to(cuda)
+    y = (torch.arange(N, device=cuda) // 400) % 20
+    data = pkg.Data(x=x, graph=g)
+    lib = ops.load_library()
+    real = lib.pg_spmm3t_ngram_add_bf16
+    calls = []
+    runs = []
+    for defer in (False, True):
+        train.DEFER_CONST_GRAD = defer
+        try:
+            torch.manual_seed(0)
+            m = pkg.ProtGramDirectGCN([64, 256, 256], N, 20, 3, 0, 512, 0.5, True).to(cuda).train()
+            m.compute_dtype = torch.bfloat16
+            opt = train.Adam(m.parameters(), lr=1e-3)
+            lib.pg_spmm3t_ngram_add_bf16 = lambda *a: (calls.append(defer), real(*a))[1]
+            losses = [float(train.train_step(m, data, y, opt, l2_lambda=1e-7)) for _ in range(3)]
+            consts = [k for k, p in m.named_parameters() if "constant" in k]
+            assert consts
+            if defer:
+                assert all(dict(m.named_parameters())[k].grad is None for k in consts)
+                assert not ops._DEFERRED_GRADS and not ops._DEFER_CONST_GRAD
+            st = {k: (p.detach().clone(), opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone())
+                  for k, p in m.named_parameters()}
+            runs.append((losses, st))
+        finally:
+            train.DEFER_CONST_GRAD = True
+            lib.pg_spmm3t_ngram_add_bf16 = real
+    assert calls and all(calls)  # the deferred run only
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    for k, (p0, m0, v0) in runs[0][1].items():
+        p1, m1, v1 = runs[1][1][k]
+        assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1), k
+
+
 def test_train_step_fused_head_matches_framework_head(pkg, cuda):
     """train.train_step with the head in one kernel (HEAD_FUSED, the default) against the framework ops
     (HEAD_FUSED = False): 3 SGD steps with the L2 gradient (parameter updates linear in the gradients), eval mode (no

@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol(pkg):
         assert hasattr(lib, n), n
     from protgram_directgcn_amd import _lib
     assert names == set(_lib.SIGNATURES), "ctypes table out of sync with the header"
-    assert lib.pg_abi_version() == 3
+    assert lib.pg_abi_version() == 4
 
 
 def test_dgrad_kernels_have_no_packed_fp32_ops():

@@ -32,6 +32,26 @@
 
 namespace {
 
+// One row's gate partials over the C4 4-column groups of an n-tile (the per-column dots the epilogue left in T at
+// stride 4), added into ds[segment] in column order -- the order of the original serial loop, so the same bits --
+// with the LDS reads issued in groups of 8: C4 / 8 round trips per row instead of C4 dependent ones (the serial loop with its
+// early exit and division cost the resident bf16 dgrad ~70 us of its ~300 at config 5, tools/r06_dgrad_exp.sh).
+template <int C4>
+__device__ __forceinline__ void row_gate_partials(const float* Trow, int n0, int N, int F_in, float (&ds)[3]) {
+    constexpr int G = C4 < 8 ? C4 : 8;
+#pragma unroll
+    for (int c0 = 0; c0 < C4; c0 += G) {
+        float tv[G];
+#pragma unroll
+        for (int c = 0; c < G; ++c) tv[c] = Trow[4 * (c0 + c)];
+#pragma unroll
+        for (int c = 0; c < G; ++c) {
+            const int jj = n0 + 4 * (c0 + c);
+            if (jj < N && jj < 3 * F_in) ds[(jj >= F_in) + (jj >= 2 * F_in)] += tv[c];
+        }
+    }
+}
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
@@ -302,7 +322,7 @@ __global__ __launch_bounds__(64 * NW) void dgrad_kernel(DgradP p) {
             if (jj >= p.N) break;
             const int q = jj / p.F_in;
             if (q < 3) ds[q] += T[tid * TLD + 4 * c];
-        }
+        }  // (row_gate_partials spilled 16 B per lane here)
 #pragma unroll
         for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
     }
@@ -582,12 +602,7 @@ __global__ __launch_bounds__(64 * NW, 3) void dgrad_x3_kernel(DgradP p, const ui
             ds[1] = Bd[tid * 3 + 1];
             ds[2] = Bd[tid * 3 + 2];
         }
-        for (int c = 0; c < C4; ++c) {
-            const int jj = n0 + 4 * c;
-            if (jj >= p.N) break;
-            const int q = jj / p.F_in;
-            if (q < 3) ds[q] += T[tid * TLD + 4 * c];
-        }
+        row_gate_partials<C4>(&T[tid * TLD], n0, p.N, p.F_in, ds);
 #pragma unroll
         for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
     }
@@ -1597,7 +1612,7 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
             if (jj >= p.N) break;
             const int q = jj / p.F_in;
             if (q < 3) ds[q] += T[tid * TLD + 4 * c];
-        }
+        }  // (row_gate_partials spilled 16 B per lane here)
 #pragma unroll
         for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
     }
@@ -1609,6 +1624,11 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
 // n-tiles with the B k-tiles double-buffered a tile ahead (crossing n-tile boundaries) and the Z rows of each n-tile's
 // epilogue loaded during its last k-tile. Same products in the same order, same per-thread bias-dot order, same
 // epilogue: every output is bit-identical to dgrad_bf16_kernel's (PG_FLAG_DGRAD_BF16_TILED keeps that kernel).
+// diagnostics build only (-DPG_DGRAD_EXP=mask, tools/r06_dgrad_exp.sh): phases of dgrad_bf16r_kernel skipped
+#ifndef PG_DGRAD_EXP
+#define PG_DGRAD_EXP 0
+#endif
+#define GXP(bit) ((PG_DGRAD_EXP >> (bit)) & 1)
 constexpr int RB_BM = 64, RB_NW = 4, RB_FMAX = 256;
 __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
     using namespace pgbf;
@@ -1670,6 +1690,10 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
             return reinterpret_cast<const uint4*>(p.BT + (int64_t)n * p.F_out + k0 + 8 * (idx & 7));
         };
         B4 r;
+        if (GXP(1)) {
+            r.a = r.b = r.c = r.d = make_uint4(g, tid, 0u, 0u);
+            return r;
+        }
         r.a = *src(0);
         r.b = *src(1);
         r.c = *src(2);
@@ -1699,6 +1723,11 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 const int idx = tid + NT * q;
                 const int64_t m = min(m0 + (idx >> 3), mlast);
                 const int k = (t < KT ? t : 0) * BKB + 8 * (idx & 7);
+                if (GXP(5)) {
+                    ra[t][q] = make_uint4(m, k, 0u, 0u);
+                    ry[t][q] = ra[t][q];
+                    continue;
+                }
                 ra[t][q] = *reinterpret_cast<const uint4*>(p.dY + m * p.lddy + k);
                 if (p.act) ry[t][q] = *reinterpret_cast<const uint4*>(p.Y + m * p.ldy + k);
             }
@@ -1724,10 +1753,10 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 }
                 const uint4 v = pack8(d);
                 if (m < p.M) {
-                    *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
+                    if (!GXP(2)) *reinterpret_cast<uint4*>(p.dpre + m * p.ldp + k) = v;
                     float dr[8];
                     unpack8(v, dr);
-                    if (p.dpre32) {
+                    if (p.dpre32 && !GXP(2)) {
                         st4(p.dpre32 + m * p.ldp32 + k, make_float4(dr[0], dr[1], dr[2], dr[3]));
                         st4(p.dpre32 + m * p.ldp32 + k + 4, make_float4(dr[4], dr[5], dr[6], dr[7]));
                     }
@@ -1779,27 +1808,36 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 T[rl * TLD + wn * TN * 32 + jj * 32 + li] = acc[jj][r];
             }
         __syncthreads();
+        // the gate dots first: every use of the Z rows precedes this epilogue's stores, so the compiler waits for
+        // the Z loads once; with a dot after each dZ store it drained the whole memory queue (vmcnt(0): the stores
+        // and the next B k-tile) at every one of the 8 items. Same products and order: the same bits.
+        float part[ITER];
+#pragma unroll
+        for (int u = 0; u < ITER; ++u) {
+            const int rl = (tid + NT * u) / C4;
+            const float4 gv = ld4(&T[rl * TLD + 4 * c4]);
+            part[u] = m0 + rl < p.M && seg < 3 ? dot4(gv, unpack4(zv[u])) : 0.f;
+        }
 #pragma unroll
         for (int u = 0; u < ITER; ++u) {
             const int rl = (tid + NT * u) / C4;
             const int64_t mm = m0 + rl;
-            float part = 0.f;
             if (mm < p.M && seg < 4) {
                 const float4 gv = ld4(&T[rl * TLD + 4 * c4]);
                 if (seg < 3) {
                     const float sc = Sg[rl * 4 + seg];
-                    if (p.dZ)
+                    if (p.dZ && !GXP(0))
                         *reinterpret_cast<uint2*>(p.dZ + mm * p.lddz + j) =
                             pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
-                    part = dot4(gv, unpack4(zv[u]));
-                } else {
+                } else if (!GXP(0)) {
                     *reinterpret_cast<uint2*>(p.dres + mm * p.lddres + (j - 3 * p.F_in)) = pack4(gv);
                 }
             }
-            T[rl * TLD + 4 * c4] = part;
         }
+#pragma unroll
+        for (int u = 0; u < ITER; ++u) T[((tid + NT * u) / C4) * TLD + 4 * c4] = part[u];  // own slots
         __syncthreads();
-        if (tid < BM && m0 + tid < p.M) {
+        if (tid < BM && m0 + tid < p.M && !GXP(7)) {
             const int64_t m = m0 + tid;
             float ds[3] = {0.f, 0.f, 0.f};
             if (nt == 0) {
@@ -1807,16 +1845,19 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 ds[1] = Bd[tid * 3 + 1];
                 ds[2] = Bd[tid * 3 + 2];
             }
-            for (int c = 0; c < C4; ++c) {
-                const int jj = n0 + 4 * c;
-                if (jj >= p.N) break;
-                const int q = jj / p.F_in;
-                if (q < 3) ds[q] += T[tid * TLD + 4 * c];
-            }
+            row_gate_partials<C4>(&T[tid * TLD], n0, p.N, p.F_in, ds);
 #pragma unroll
             for (int q = 0; q < 3; ++q) p.dsp[((int64_t)nt * 3 + q) * p.M + m] = ds[q];
         }
         __syncthreads();  // T is read before the next n-tile's first B k-tile overwrites it
+    };
+    auto acc_sink = [&](int nt) __attribute__((always_inline)) {  // diagnostics: keep the products live
+        float t = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t += acc[jj][r];
+        if (t == 12345.f) p.dsp[nt] = t;
     };
     // tile g: MFMAs on buffer g & 1 (tile g, stashed); tile g + 2 loads into one register set while tile g + 1 goes
     // from the other to the other buffer -- after the epilogue when g ends an n-tile (even g: load S0, stash S1)
@@ -1828,9 +1869,12 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[jj][r] = 0.f;
         }
-        if (g + 2 < G) {
-            if constexpr (decltype(odd)::value) S1 = loadB(g + 2);
-            else S0 = loadB(g + 2);
+        {  // unconditional (the last steps re-read tile G - 1, unused): with a load on every path the compiler's
+           // wait before the stash below counts the 4 younger loads (vmcnt(4)) instead of draining everything,
+           // epilogue stores included (vmcnt(0)), at every k-tile
+            const int gl = g + 2 < G ? g + 2 : G - 1;
+            if constexpr (decltype(odd)::value) S1 = loadB(gl);
+            else S0 = loadB(gl);
         }
         if (kt == KT - 1) {  // this n-tile's Z rows for the epilogue
             const int j = nt * BN + 4 * c4;
@@ -1838,7 +1882,7 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
 #pragma unroll
             for (int u = 0; u < ITER; ++u) {
                 const int64_t m = min(m0 + (tid + NT * u) / C4, mlast);
-                zv[u] = zseg ? *reinterpret_cast<const uint2*>(p.Z + m * p.ldz + j) : make_uint2(0u, 0u);
+                zv[u] = zseg && !GXP(6) ? *reinterpret_cast<const uint2*>(p.Z + m * p.ldz + j) : make_uint2(m, j);
             }
         }
         const uint16_t* Bb = Bs + (g & 1) * BN * LDKB;
@@ -1852,8 +1896,10 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 b[jj] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
                                                       &Bb[(wn * TN * 32 + jj * 32 + li) * LDKB + kk * 16 + 8 * lh]));
 #pragma unroll
-            for (int jj = 0; jj < TN; ++jj)
-                acc[jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[jj], acc[jj], 0, 0, 0);
+            for (int jj = 0; jj < TN; ++jj) {
+                if (GXP(3)) acc[jj][kk] += (float)a[jj] * (float)b[jj][kk];
+                else acc[jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[jj], acc[jj], 0, 0, 0);
+            }
         }
         auto stash_next = [&]() __attribute__((always_inline)) {
             if constexpr (decltype(odd)::value) stashB(S0, (g + 1) & 1);
@@ -1864,7 +1910,8 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
             __syncthreads();
         } else {
             __syncthreads();
-            epilogue(nt);
+            if (!GXP(4)) epilogue(nt);
+            else acc_sink(nt);
             if (g + 1 < G) {
                 stash_next();
                 __syncthreads();

@@ -14,6 +14,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 
 
+def _collect(q, procs, timeout=300):
+    """The ranks' results; on the first failure the others (which may wait in a collective) are terminated."""
+    res = []
+    for _ in procs:
+        r = q.get(timeout=timeout)
+        res.append(r)
+        if not r[1]:
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            break
+    return sorted(res)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -85,6 +99,9 @@ def _worker(rank, world, port, out_q):
             if err > tol:
                 bad.append((name, err, tol))
         out_q.put((rank, not bad, str(bad[:4])))
+    except Exception as e:  # report at once (the parent would otherwise wait out its queue timeout)
+        out_q.put((rank, False, repr(e)))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -96,12 +113,12 @@ def test_sharded_training_two_ranks_one_gpu(pkg, cuda):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=300) for _ in procs)
+    res = _collect(q, procs)
+    for r in res:
+        assert r[1], f"rank {r[0]}: {r[2]}"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in res:
-        assert r[1], f"rank {r[0]}: {r[2]}"
 
 
 def _trainer_worker(rank, world, port, out_q, bf16):
@@ -149,6 +166,7 @@ def _trainer_worker(rank, world, port, out_q, bf16):
         m1.load_state_dict(ref)
         m1.compute_dtype = dt
         opt1 = train.Adam(m1.parameters(), lr=1e-3) if bf16 else torch.optim.SGD(m1.parameters(), lr=0.1)
+        train.DEFER_CONST_GRAD = False  # the comparison below reads every parameter's .grad
         rl = [float(train.train_step(m1, pkg.Data(x=x, graph=g1), y, opt1, l2_lambda=lam, scaler=None))
               for _ in range(steps)]
         bad = []
@@ -173,6 +191,9 @@ def _trainer_worker(rank, world, port, out_q, bf16):
                 if err > tol:
                     bad.append((name, err, tol))
         out_q.put((rank, not bad, str(bad[:4])))
+    except Exception as e:  # report at once (the parent would otherwise wait out its queue timeout)
+        out_q.put((rank, False, repr(e)))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -185,12 +206,12 @@ def test_sharded_trainer_two_ranks_one_gpu(pkg, cuda, bf16):
     procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, bf16)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=300) for _ in procs)
+    res = _collect(q, procs)
+    for r in res:
+        assert r[1], f"rank {r[0]}: {r[2]}"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r in res:
-        assert r[1], f"rank {r[0]}: {r[2]}"
 
 
 @pytest.mark.parametrize("n,dims", [(3, [128, 128, 128]), (3, [64, 64, 32]), (2, [32, 32, 32, 16])])

@@ -1580,9 +1580,12 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
             zv[u] = make_uint2(0u, 0u);
             if (mm[u] < p.M && seg < 3) zv[u] = *reinterpret_cast<const uint2*>(p.Z + mm[u] * p.ldz + j);
         }
+        float part[BATCH];  // the gate dots before the batch's stores: one wait for its Z loads, not one per item
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u)
+            part[u] = mm[u] < p.M && seg < 3 ? dot4(ld4(&T[rl[u] * TLD + 4 * c4]), unpack4(zv[u])) : 0.f;
 #pragma unroll
         for (int u = 0; u < BATCH; ++u) {
-            float part = 0.f;
             if (mm[u] < p.M && seg < 4) {
                 const float4 gv = ld4(&T[rl[u] * TLD + 4 * c4]);
                 if (seg < 3) {
@@ -1590,13 +1593,13 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
                     if (p.dZ)
                         *reinterpret_cast<uint2*>(p.dZ + mm[u] * p.lddz + j) =
                             pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
-                    part = dot4(gv, unpack4(zv[u]));
                 } else {
                     *reinterpret_cast<uint2*>(p.dres + mm[u] * p.lddres + (j - 3 * p.F_in)) = pack4(gv);
                 }
             }
-            T[rl[u] * TLD + 4 * c4] = part;
         }
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) T[rl[u] * TLD + 4 * c4] = part[u];  // own slots
     }
     __syncthreads();
     if (tid < BM && m0 + tid < p.M) {

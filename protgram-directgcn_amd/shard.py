@@ -1642,6 +1642,22 @@ class MiddleTrainer:
         g.replay()  # the step the capture recorded
 
     def _step(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
+        # bf16 mode with train.Adam: the owned per-node constants' gradients stay the layers' bf16 dpre, read by Adam
+        # directly (train.DEFER_CONST_GRAD, as train.train_step: no fp32 copy written by the backward, none copied
+        # into a home buffer, half the bytes read by Adam; the same update bits)
+        from . import ops
+        defer = (self._train.DEFER_CONST_GRAD and isinstance(self.opt, self._train.Adam)
+                 and self.model.compute_dtype == torch.bfloat16)
+        prev = ops._DEFER_CONST_GRAD
+        ops._DEFER_CONST_GRAD = defer
+        try:
+            return self._step_body(x_full, y_own)
+        finally:
+            ops._DEFER_CONST_GRAD = prev
+            ops._DEFERRED_GRADS.clear()
+
+    def _step_body(self, x_full: torch.Tensor, y_own: torch.Tensor) -> torch.Tensor:
+        from .ops import deferred_grad
         mp, lam, train = self.mp, self.l2_lambda, self._train
         # autograd assigns each parameter's gradient (no .grad preset: a preset one costs an add kernel per parameter
         # per step, ~0.3 ms at config 5); then one multi-tensor copy moves them into their fixed homes: the flat
@@ -1673,6 +1689,8 @@ class MiddleTrainer:
         if have:
             torch._foreach_copy_([h for _, h in have], [p.grad for p, _ in have])
         for p, h, node in homes:
+            if node and p.grad is None and deferred_grad(p) is not None:
+                continue  # Adam reads the filed bf16 gradient
             if p.grad is None and node:
                 h.zero_()  # an unused per-node parameter: its persistent buffer holds zeros (the flat one is zeroed)
             p.grad = h
@@ -1681,7 +1699,7 @@ class MiddleTrainer:
         zero = nll.new_zeros(())
         if lam:
             for p in self.node:
-                if p.requires_grad and p.grad is None:
+                if p.requires_grad and p.grad is None and deferred_grad(p) is None:
                     p.grad = torch.zeros_like(p)
             if not fused:
                 l2_rep = train.l2_sqsum(self.dense) if self.dense else zero

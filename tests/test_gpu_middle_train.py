@@ -93,6 +93,17 @@ def _worker(rank, world, port, out_q, bf16, ref_path):
         hits = []
         real = ops.spmm3_middles
         ops.spmm3_middles = lambda *a, **k: hits.append(1) or real(*a, **k)
+        # bf16: the per-node constants' gradients go to Adam as the layers' bf16 dpre (train.DEFER_CONST_GRAD), not
+        # as .grad; keep a widened copy of each as the backward files it
+        filed = {}
+        real_file = ops._file_deferred
+
+        def spy(constant, dpre):
+            ok = real_file(constant, dpre)
+            if ok:
+                filed[constant.data_ptr()] = dpre.float()
+            return ok
+        ops._file_deferred = spy
         phase("trainer built")
         loss = float(tr.step(x, y[mp_.own]))
         torch.cuda.synchronize()
@@ -108,7 +119,8 @@ def _worker(rank, world, port, out_q, bf16, ref_path):
         for name, p in m.named_parameters():
             r = rgrad[name]
             if shard._is_node_param(name, p, N):
-                gg = tr.own[int(name.split(".")[1])][name.split(".")[-1]].grad
+                leaf = tr.own[int(name.split(".")[1])][name.split(".")[-1]]
+                gg = leaf.grad if leaf.grad is not None else filed.get(leaf.data_ptr())
                 r = r[own.cpu()]
             else:
                 gg = p.grad
@@ -259,6 +271,47 @@ def test_middle_trainer_hip_graph_follows_lr_schedule(pkg, cuda, bf16):
         tr.close()
     lrs = [h["lr"][0] for h in res[0][0]]
     assert lrs[:4] == [1e-2, 1e-2, 5e-3, 2.5e-3], lrs
+    assert res[0][0] == res[1][0], res
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_middle_trainer_bf16_deferred_constant_grads_bit_identical(pkg, cuda, graphs):
+    """bf16 MiddleTrainer with train.Adam: the owned per-node constants' gradients go to Adam as the layers' bf16
+    dpre (train.DEFER_CONST_GRAD) instead of fp32 .grad copies moved into home buffers. 4 steps (eager, or captured
+    after the warm-up and replayed), training mode with the fused dropout: losses and every parameter bit-identical
+    to the run without deferral (rank 0 of 2 at 3-gram, the collectives no-ops); the constants' .grad stay None."""
+    from protgram_directgcn_amd import ops, shard, train
+    from test_gpu_configs import _labels, _model
+    n, dims = 3, [64, 256, 256]
+    N, s_, d, c = pkg.synth.de_bruijn_edges(n)
+    g = pkg.build_propagation_csr(N, s_, d, c, device=cuda)
+    x = torch.randn(N, dims[0], generator=torch.Generator().manual_seed(5)).to(cuda)
+    y = _labels(N, n).to(cuda)
+    mp_ = shard.middle_partition(g, 0, 2)
+    res = []
+    filed = []
+    real_file = ops._file_deferred
+    try:
+        for defer in (False, True):
+            train.DEFER_CONST_GRAD = defer
+            ops._file_deferred = lambda cst, dp: (filed.append(defer), real_file(cst, dp))[1]
+            torch.manual_seed(0)
+            m = _model(pkg, dims, N, n).to(cuda).train()
+            m.compute_dtype = torch.bfloat16
+            tr = shard.MiddleTrainer(m, mp_, lr=1e-2, l2_lambda=1e-3, comm=_NoComm(), graphs=graphs)
+            yo = y[mp_.own]
+            losses = [float(tr.step(x, yo)) for _ in range(4 + 3 * graphs)]
+            torch.cuda.synchronize()
+            if defer:
+                assert all(d["constant"].grad is None for d in tr.own if "constant" in d)
+                assert not ops._DEFERRED_GRADS and not ops._DEFER_CONST_GRAD
+            res.append((losses, [p.detach().clone() for p in tr.params]))
+            tr.close()
+    finally:
+        train.DEFER_CONST_GRAD = True
+        ops._file_deferred = real_file
+    assert filed and all(filed)  # filed in the deferring run only
     assert res[0][0] == res[1][0], res
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 : > gpurun_out/r06_ab_train.txt
 for i in 1 2 3; do
-  for lib in lib_head lib_new; do
+  for lib in ${LIBS:-lib_head lib_new}; do
     for a in "--fused --our-adam" "--fused --our-adam --bf16 --dims=128,256,256,256"; do
       echo -n "$lib " >> gpurun_out/r06_ab_train.txt
       PG_DIRECTGCN_LIB=$PWD/abtmp/$lib.so timeout -k 10 200 python -u tools/train_probe.py 20 $a 2>&1 | grep "train step" >> gpurun_out/r06_ab_train.txt || exit 1

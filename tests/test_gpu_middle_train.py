@@ -369,3 +369,49 @@ def test_middle_trainer_fused_dropout_matches_masked(pkg, cuda, bf16, monkeypatc
     monkeypatch.setattr(torch.nn.functional, "dropout", dropout)
     assert len(calls) == len(dims) - 1
     assert torch.equal(lp, lp_ref)
+
+
+def _fit_worker(rank, world, port, q, argv):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [REPO, os.path.join(REPO, "tools")]
+    try:
+        import fit_config5
+        rec = fit_config5.run(argv)
+        if rank == 0:
+            q.put(("ok", rec))
+    except Exception as e:  # report instead of leaving the parent to its timeout
+        q.put(("error", repr(e)[:400]))
+        raise
+
+
+@pytest.mark.timeout(600)
+def test_fit_config5_driver_two_ranks_matches_one():
+    """tools/fit_config5.py, the multi-GPU epoch loop of config 5 (train.fit around MiddleTrainer.step: the reference
+    loop's ReduceLROnPlateau + EarlyStopper, protgram_directgcn_trainer.py:76-108), on 2 gloo ranks sharing cuda:0
+    against the same loop on 1 rank: 8 epochs at 3-gram, fp32, no dropout; the same number of epochs, the same
+    learning rates, and the per-epoch losses within 1e-5 relative (the ranks' partial sums are added in another
+    order)."""
+    argv = ["--backend", "gloo", "--n", "3", "--dims", "64,64,32", "--epochs", "8", "--fp32", "--eval",
+            "--lr", "1e-2", "--l2", "1e-3"]
+    ctx = mp.get_context("spawn")
+    recs = []
+    for world in (1, 2):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_fit_worker, args=(r, world, port, q, argv)) for r in range(world)]
+        for p in procs:
+            p.start()
+        status, rec = q.get(timeout=300)
+        for p in procs:
+            p.join(timeout=120)
+        assert status == "ok", rec
+        assert all(p.exitcode == 0 for p in procs)
+        recs.append(rec)
+    (a, b) = recs
+    assert a["epochs_run"] == b["epochs_run"] == 8
+    assert [h["lr"] for h in a["history"]] == [h["lr"] for h in b["history"]]
+    for ha, hb in zip(a["history"], b["history"]):
+        assert abs(ha["loss"] - hb["loss"]) <= 1e-5 * abs(ha["loss"]), (ha, hb)
+    assert a["history"][-1]["loss"] < a["history"][0]["loss"]
+

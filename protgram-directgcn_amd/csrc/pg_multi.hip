@@ -177,21 +177,42 @@ __global__ __launch_bounds__(256) void adam_kernel(int ntens, const pg_adam_desc
     }
     if (vec) {
         const int64_t n4 = (end - beg) >> 2;
+// Non-temporal loads / stores of the streams (each byte touched once per step; PG_ADAM_NT=0 builds the cached form):
+// 0.652 -> 0.582 ms over config 5's 123M parameters, the same bits (tools/r06_adam_probe.py, profiles/r06_ab_adam_nt.txt)
+#ifndef PG_ADAM_NT
+#define PG_ADAM_NT 1
+#endif
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        auto ld = [](const float* q) {
+            if (PG_ADAM_NT) {
+                const f4v x = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(q));
+                return make_float4(x.x, x.y, x.z, x.w);
+            }
+            return *reinterpret_cast<const float4*>(q);
+        };
+        auto st = [](float* q, float4 x) {
+            if (PG_ADAM_NT) {
+                const f4v y = {x.x, x.y, x.z, x.w};
+                __builtin_nontemporal_store(y, reinterpret_cast<f4v*>(q));
+            } else {
+                *reinterpret_cast<float4*>(q) = x;
+            }
+        };
         for (int64_t k = threadIdx.x; k < n4; k += 256) {
             const int64_t i = beg + 4 * k;
-            const float4 g = gbf ? pgbf::unpack4(*reinterpret_cast<const uint2*>(gb + i))
-                                 : *reinterpret_cast<const float4*>(gf + i);
-            float4 p = *reinterpret_cast<const float4*>(t.p + i);
-            float4 m = *reinterpret_cast<const float4*>(t.m + i);
-            float4 v = *reinterpret_cast<const float4*>(t.v + i);
+            // (the bf16 gradient keeps the cached load: non-temporal 8-B loads measured 0.62 against 0.58 ms)
+            const float4 g = gbf ? pgbf::unpack4(*reinterpret_cast<const uint2*>(gb + i)) : ld(gf + i);
+            float4 p = ld(t.p + i);
+            float4 m = ld(t.m + i);
+            float4 v = ld(t.v + i);
             sq += p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
             upd(g.x, p.x, m.x, v.x);
             upd(g.y, p.y, m.y, v.y);
             upd(g.z, p.z, m.z, v.z);
             upd(g.w, p.w, m.w, v.w);
-            *reinterpret_cast<float4*>(t.p + i) = p;
-            *reinterpret_cast<float4*>(t.m + i) = m;
-            *reinterpret_cast<float4*>(t.v + i) = v;
+            st(t.p + i, p);
+            st(t.m + i, m);
+            st(t.v + i, v);
         }
         i0 = beg + 4 * n4;
     }

@@ -1632,6 +1632,38 @@ __global__ __launch_bounds__(64 * NW, 2) void dgrad_bf16_kernel(DgradB p) {
 #define PG_DGRAD_EXP 0
 #endif
 #define GXP(bit) ((PG_DGRAD_EXP >> (bit)) & 1)
+// non-temporal forms of the resident dgrad's once-touched streams (PG_DGRAD_NT bits: 0 the dY / Y loads, 1 the
+// epilogue's Z loads, 2 its dZ stores); A/B builds via tools/r06_ab_lib2.sh
+#ifndef PG_DGRAD_NT
+#define PG_DGRAD_NT 7  // all three: config 5 3.904 -> 3.875 ms (mean of 3 interleaved runs, profiles/r06_ab_train_dgrad_nt.txt)
+#endif
+typedef unsigned int pg_u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int pg_u2v __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16u(const uint16_t* q) {
+    if constexpr (NT) {
+        const pg_u4v x = __builtin_nontemporal_load(reinterpret_cast<const pg_u4v*>(q));
+        return make_uint4(x.x, x.y, x.z, x.w);
+    }
+    return *reinterpret_cast<const uint4*>(q);
+}
+template <bool NT>
+__device__ __forceinline__ uint2 ld8u(const uint16_t* q) {
+    if constexpr (NT) {
+        const pg_u2v x = __builtin_nontemporal_load(reinterpret_cast<const pg_u2v*>(q));
+        return make_uint2(x.x, x.y);
+    }
+    return *reinterpret_cast<const uint2*>(q);
+}
+template <bool NT>
+__device__ __forceinline__ void st8u(uint16_t* q, uint2 v) {
+    if constexpr (NT) {
+        const pg_u2v x = {v.x, v.y};
+        __builtin_nontemporal_store(x, reinterpret_cast<pg_u2v*>(q));
+    } else {
+        *reinterpret_cast<uint2*>(q) = v;
+    }
+}
 constexpr int RB_BM = 64, RB_NW = 4, RB_FMAX = 256;
 __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
     using namespace pgbf;
@@ -1731,8 +1763,8 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                     ry[t][q] = ra[t][q];
                     continue;
                 }
-                ra[t][q] = *reinterpret_cast<const uint4*>(p.dY + m * p.lddy + k);
-                if (p.act) ry[t][q] = *reinterpret_cast<const uint4*>(p.Y + m * p.ldy + k);
+                ra[t][q] = ld16u<(PG_DGRAD_NT & 1) != 0>(p.dY + m * p.lddy + k);
+                if (p.act) ry[t][q] = ld16u<(PG_DGRAD_NT & 1) != 0>(p.Y + m * p.ldy + k);
             }
         S0 = loadB(0);
         float bd[A_C][3];
@@ -1830,8 +1862,8 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
                 if (seg < 3) {
                     const float sc = Sg[rl * 4 + seg];
                     if (p.dZ && !GXP(0))
-                        *reinterpret_cast<uint2*>(p.dZ + mm * p.lddz + j) =
-                            pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w));
+                        st8u<(PG_DGRAD_NT & 4) != 0>(p.dZ + mm * p.lddz + j,
+                                                     pack4(make_float4(sc * gv.x, sc * gv.y, sc * gv.z, sc * gv.w)));
                 } else if (!GXP(0)) {
                     *reinterpret_cast<uint2*>(p.dres + mm * p.lddres + (j - 3 * p.F_in)) = pack4(gv);
                 }
@@ -1885,7 +1917,7 @@ __global__ __launch_bounds__(64 * RB_NW, 2) void dgrad_bf16r_kernel(DgradB p) {
 #pragma unroll
             for (int u = 0; u < ITER; ++u) {
                 const int64_t m = min(m0 + (tid + NT * u) / C4, mlast);
-                zv[u] = zseg && !GXP(6) ? *reinterpret_cast<const uint2*>(p.Z + m * p.ldz + j) : make_uint2(m, j);
+                zv[u] = zseg && !GXP(6) ? ld8u<(PG_DGRAD_NT & 2) != 0>(p.Z + m * p.ldz + j) : make_uint2(m, j);
             }
         }
         const uint16_t* Bb = Bs + (g & 1) * BN * LDKB;

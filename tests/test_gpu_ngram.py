@@ -184,9 +184,26 @@ def test_ngram_transposed_bf16(pkg, cuda, n, keep, F, kernel):
         dX = torch.randn(N, F, generator=torch.Generator().manual_seed(9)).to(cuda).to(torch.bfloat16)
         want = dX.float() + ref32
         ng = g.ngram
+        C = dX.clone()  # the addend, for the out-of-place form below
         rc = lib.pg_spmm3t_ngram_bf16(ng.K, ng.n, N, ng.plan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
                                       dX.data_ptr(), dX.stride(0), 1, fl, ops._stream(dX))
         assert rc == 0
         d = (dX.float() - want).abs()
         bad = d > 2.0 ** -7 * want.abs() + 2.0 ** -7 * ref32.abs() + 1e-6
         assert not bool(bad.any()), ("accumulate", int(bad.sum()), float(d.max()))
+        # pg_spmm3t_ngram_add_bf16: dX = C + A^T G with C read from its own rows -- the accumulate form's bits, C kept
+        # (a strided C, and C = dX in place)
+        Cw = torch.zeros(N, F + 8, dtype=torch.bfloat16, device=cuda)
+        Cw[:, :F] = C
+        out = torch.full((N, F), float("nan"), dtype=torch.bfloat16, device=cuda)
+        rc = lib.pg_spmm3t_ngram_add_bf16(ng.K, ng.n, N, ng.plan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
+                                          Cw.data_ptr(), Cw.stride(0), out.data_ptr(), out.stride(0), fl,
+                                          ops._stream(out))
+        assert rc == 0
+        assert torch.equal(out, dX) and torch.equal(Cw[:, :F], C)
+        C2 = C.clone()
+        rc = lib.pg_spmm3t_ngram_add_bf16(ng.K, ng.n, N, ng.plan.data_ptr(), Gw.data_ptr(), Gw.stride(0), F,
+                                          C2.data_ptr(), C2.stride(0), C2.data_ptr(), C2.stride(0), fl,
+                                          ops._stream(C2))
+        assert rc == 0 and torch.equal(C2, dX)
+        assert torch.equal(ops.spmm3t_ngram_acc_bf16(g, G, torch.empty_like(C), src=C), dX)

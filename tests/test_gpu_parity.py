@@ -1295,6 +1295,45 @@ def test_fused_adam_matches_torch_adam(pkg, cuda):
     assert float(o_ours.state[ps_ours[0]]["step"]) == 5.0
 
 
+def test_adam_bf16_deferred_gradient_matches_widened(pkg, cuda):
+    """pg_adam_desc_t.gtype = 1 (ABI 4): a bf16 gradient filed through ops._DEFERRED_GRADS gives, bit for bit, the update
+    of the same values widened to an fp32 .grad -- on the 16-B path, on a shape whose length is not a multiple of 4
+    (the scalar tail) and on a gradient view that is not 8-B aligned (the scalar path), with weight decay,
+    in one launch together with an fp32-gradient parameter; 3 steps."""
+    from protgram_directgcn_amd import ops, train
+    g = torch.Generator().manual_seed(5)
+    shapes = [(1000, 64), (1001,), (70003,), (33, 7)]
+    init = [torch.randn(s, generator=g).to(cuda) for s in shapes]
+    gb = [[(torch.randn(s, generator=g) * 1e-2).to(cuda).to(torch.bfloat16) for s in shapes] for _ in range(3)]
+    store = torch.zeros(70003 + 4, dtype=torch.bfloat16, device=cuda)  # a 4-B-offset view for shapes[2]
+    ps_w = [torch.nn.Parameter(t.clone()) for t in init]
+    ps_d = [torch.nn.Parameter(t.clone()) for t in init]
+    o_w = train.Adam([{"params": ps_w[:2]}, {"params": ps_w[2:], "weight_decay": 0.01}], lr=1e-3)
+    o_d = train.Adam([{"params": ps_d[:2]}, {"params": ps_d[2:], "weight_decay": 0.01}], lr=1e-3)
+    for step in gb:
+        for p, gg in zip(ps_w, step):
+            p.grad = gg.float()
+        o_w.step()
+        try:
+            for i, (p, gg) in enumerate(zip(ps_d, step)):
+                if i == 3:
+                    p.grad = gg.float()  # an fp32 gradient in the same launch
+                elif i == 2:
+                    view = store[2:2 + gg.numel()]
+                    view.copy_(gg)
+                    assert view.data_ptr() % 8 == 4
+                    ops._DEFERRED_GRADS[p.data_ptr()] = view
+                else:
+                    ops._DEFERRED_GRADS[p.data_ptr()] = gg.contiguous()
+            o_d.step()
+        finally:
+            ops._DEFERRED_GRADS.clear()
+    for a, b in zip(ps_d, ps_w):
+        assert torch.equal(a.detach(), b.detach())
+        assert torch.equal(o_d.state[a]["exp_avg"], o_w.state[b]["exp_avg"])
+        assert torch.equal(o_d.state[a]["exp_avg_sq"], o_w.state[b]["exp_avg_sq"])
+
+
 def test_adam_checkpoint_round_trip_and_skipped_params(pkg, cuda, tmp_path):
     """train.Adam against torch.optim.Adam across a checkpoint loaded with map_location='cpu' (the step
     counters come back as host tensors), with parameters whose gradient is None on some steps (torch counts

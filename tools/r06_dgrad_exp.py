@@ -16,7 +16,7 @@ pkg = load_package()
 from protgram_directgcn_amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-M, F = 160_000, 256
+M, F = int(os.environ.get("PROBE_M", 160_000)), 256
 gen = torch.Generator().manual_seed(3)
 conv = pkg.DirectGCNLayer(F, F, M, True).to(dev)
 prm = dict(zip(ops._DENSE_KEYS, (p.detach() for p in conv._dense_params())))

@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgradP p, int splits) 
     __shared__ __attribute__((aligned(16))) uint4 U[2][3][2][WX_COLS];
     __shared__ float Db[2][4][WX_BP];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, li = lane & 31, kh = lane >> 5;
-    const int n_tiles = p.N / WX_BN;
+    const int n_tiles = min(p.N, 3 * p.F_in) / WX_BN;  // the gated segments (a projected residual's: wgrad_bf16_kernel)
     int split, tile;
     wgrad_tile_of((int)blockIdx.x, (p.P / WX_BP) * n_tiles, splits, split, tile);
     if (tile < 0) return;  // whole workgroup: no barrier reached
@@ -2003,6 +2003,8 @@ struct WgradB {
     int64_t rows_per_split;
     int64_t part_stride;
     float* part;
+    int col0;           // wgrad_bf16_kernel: first output column (the projected residual's columns after the staged
+                        // kernel's 3 F_in; then no bias sums here)
 };
 
 constexpr int WRB = 32;  // rows per K step (2 MFMA k-steps)
@@ -2017,10 +2019,10 @@ __global__ __launch_bounds__(512, 4) void wgrad_bf16_kernel(WgradB p) {
     constexpr int BI = 128, BJ = 128;
     __shared__ __attribute__((aligned(16))) uint16_t At[2][BI * LDM];
     __shared__ __attribute__((aligned(16))) uint16_t Bt[2][BJ * LDM];
-    const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI;
+    const int j0 = p.col0 + blockIdx.x * BJ, i0 = blockIdx.y * BI;
     const int64_t r0 = (int64_t)blockIdx.z * p.rows_per_split;
     const int64_t rend = min(r0 + p.rows_per_split, p.M);
-    const bool do_db = blockIdx.x == 0;
+    const bool do_db = blockIdx.x == 0 && p.col0 == 0;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int wi = wave >> 1, wj = wave & 1;  // wave tile 32 (i) x 64 (j)
     const int li = lane & 31, lh = lane >> 5;
@@ -2484,7 +2486,7 @@ BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj, bool x3w = fa
     b.K = (int)((proj ? 4 : 3) * F_in);
     b.ntn = (b.K + DG_BN - 1) / DG_BN;
     if (x3w) {
-        const int64_t tiles = (F_out / WX_BP) * (b.K / WX_BN);
+        const int64_t tiles = (F_out / WX_BP) * (std::min<int64_t>(b.K, 3 * F_in) / WX_BN);
         const int64_t steps = std::max<int64_t>((M + WX_K - 1) / WX_K, 1);
         const int64_t splits = std::min<int64_t>(std::max<int64_t>((256 + tiles - 1) / tiles, 1), steps);
         b.rows_per_split = ((steps + splits - 1) / splits) * WX_K;
@@ -2499,7 +2501,8 @@ BwdPlan plan_of(int64_t M, int64_t F_in, int64_t F_out, bool proj, bool x3w = fa
     b.off_dsp = up4(2 * (int64_t)b.K * F_out);
     b.off_part = b.off_dsp + up4((int64_t)b.ntn * 3 * M);
     b.total = b.off_part + (int64_t)b.splits * b.part_stride;
-    if (!x3w && wgrad_x3_shape(F_in, F_out, proj)) b.total = std::max(b.total, plan_of(M, F_in, F_out, proj, true).total);
+    // (the bf16 backward stages the gated segments even with a projected residual)
+    if (!x3w && wgrad_x3_shape(F_in, F_out, false)) b.total = std::max(b.total, plan_of(M, F_in, F_out, proj, true).total);
     return b;
 }
 
@@ -2796,7 +2799,8 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
     const bool proj = a->W_res != nullptr;
     // the staged weight gradient (wgrad_bfs_kernel) where its tiles fit; PG_FLAG_WGRAD_BF16_TILED keeps the 128 x 128
     // tiles of wgrad_bf16_kernel
-    const bool bfs = wgrad_x3_shape(a->F_in, a->F_out, proj) && !(flags & PG_FLAG_WGRAD_BF16_TILED) &&
+    // (with a projected residual, its F_in columns then run on wgrad_bf16_kernel beside it)
+    const bool bfs = wgrad_x3_shape(a->F_in, a->F_out, false) && !(flags & PG_FLAG_WGRAD_BF16_TILED) &&
                      a->ldz % 4 == 0 && g->ldp % 4 == 0 && (reinterpret_cast<uintptr_t>(a->Z) & 7) == 0 &&
                      (reinterpret_cast<uintptr_t>(g->dpre) & 7) == 0;
     const BwdPlan pl = plan_of(a->M, a->F_in, a->F_out, proj, bfs);
@@ -2906,9 +2910,15 @@ int pg_directgcn_dense_bwd_bf16(const pg_layer_args_t* a, const float* packed, c
         w.part_stride = pl.part_stride;
         w.part = part;
         if (bfs) {
-            const int tiles = (F_out / WX_BP) * (K / WX_BN);
+            const int tiles = (F_out / WX_BP) * (3 * F_in / WX_BN);
             const unsigned nb = (unsigned)(8 * ((pl.splits + 7) / 8) * tiles);
             hipLaunchKernelGGL(wgrad_bfs_kernel, dim3(nb), dim3(512), 0, s, w, (int)pl.splits);
+            if (proj) {  // the residual's columns [3 F_in, 4 F_in): the same partial buffers, no bias sums
+                WgradB wr = w;
+                wr.col0 = 3 * F_in;
+                dim3 grid((unsigned)((F_in + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
+                hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(512), 0, s, wr);
+            }
         } else {
             dim3 grid((unsigned)((K + 127) / 128), (unsigned)((F_out + 127) / 128), (unsigned)pl.splits);
             hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(512), 0, s, w);

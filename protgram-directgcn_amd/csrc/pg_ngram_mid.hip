@@ -1101,22 +1101,23 @@ __global__ __launch_bounds__(256) void ngram_mplan_map_kernel(int64_t Kn1, int64
     }
 }
 
-// Residual pass of a mapped graph (pg_spmm3_resid_f32): one wave per listed row, all of its residual entries, the
-// three aggregates in fp32 (lane q: float4 columns q, q + 64, ...); the row's Z slices are overwritten (a node off the
-// grid) or added to (a grid node: bit 31 of its list entry). Compact CSR: entries of list position i at
-// [rowptr[i], rowptr[i + 1]), so the row id and the entry range load in parallel (no dependent rowptr read).
+// Residual pass of a mapped graph (pg_spmm3_resid_f32): LPR lanes per listed row (64 / LPR rows per wave; LPR = 16
+// for F <= 64, 32 for F <= 128, else 64), all of its residual entries, the three aggregates in fp32 (lane q: float4
+// columns q, q + LPR, ...); the row's Z slices are overwritten (a node off the grid) or added to (a grid node: bit 31
+// of its list entry). Compact CSR: entries of list position i at [rowptr[i], rowptr[i + 1]), so the row id and the
+// entry range load in parallel (no dependent rowptr read).
 __global__ __launch_bounds__(256) void ngram_resid_kernel(int64_t n_list, const int64_t* rowptr, const int* rows,
                                                           const int4* edges, const float* X, int64_t ldx, int F,
-                                                          float* Z, int64_t ldz) {
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                          float* Z, int64_t ldz, int lpr) {
     const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr;
     if (i >= n_list) return;
     const int code = rows[i];
     const bool add = code < 0;
     const int64_t row = code & 0x7fffffff;
     const int64_t e0 = rowptr[i], e1 = rowptr[i + 1];
     const int F4 = F >> 2;
-    for (int q = lane; q < F4; q += 64) {
+    for (int q = lane % lpr; q < F4; q += lpr) {
         f4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
         int64_t e = e0;
         for (; e + 4 <= e1; e += 4) {  // four gathers in flight
@@ -1275,8 +1276,11 @@ int pg_spmm3_resid_f32(int64_t n_list, const int64_t* rowptr, const int32_t* row
     PG_REQUIRE(ldx >= F && ldz >= 3 * F, "leading dimensions too small");
     if (!pg::aligned16(X) || !pg::aligned16(Z) || ldx % 4 || ldz % 4)
         return pg::set_error(PG_ERR_UNSUPPORTED, "pg_spmm3_resid_f32: needs 16-B aligned rows");
-    hipLaunchKernelGGL(ngram_resid_kernel, dim3((unsigned)((n_list + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n_list,
-                       rowptr, rows, reinterpret_cast<const int4*>(edges), X, ldx, (int)F, Z, ldz);
+    const int lpr = F <= 64 ? 16 : (F <= 128 ? 32 : 64);  // lanes per row: every lane has a float4 column
+    const int64_t per_block = 4 * (64 / lpr);
+    hipLaunchKernelGGL(ngram_resid_kernel, dim3((unsigned)((n_list + per_block - 1) / per_block)), dim3(256), 0,
+                       (hipStream_t)stream, n_list, rowptr, rows, reinterpret_cast<const int4*>(edges), X, ldx, (int)F,
+                       Z, ldz, lpr);
     return pg::check_launch("pg_spmm3_resid_f32");
 }
 

@@ -69,11 +69,13 @@ def test_fasta3_golden_layer_on_mapped_plan(pkg, cuda, monkeypatch):
     assert_close(Z, Zc, "mapped vs CSR propagation")
 
 
-@pytest.mark.parametrize("n,nseq,rare,F", [(2, 6, 0.05, 16), (3, 60, 0.01, 32), (3, 200, 0.003, 48)])
+@pytest.mark.parametrize("n,nseq,rare,F", [(2, 6, 0.05, 16), (3, 60, 0.01, 32), (3, 200, 0.003, 48),
+                                            (3, 60, 0.01, 144), (2, 6, 0.05, 256)])
 def test_padded_builder_graph_small(pkg, cuda, monkeypatch, n, nseq, rare, F):
     """Padded (' ') builder graphs with non-standard letters, built by ngram.ngram_transitions: off-grid rows,
     grid rows with residual entries, and grid slots all present; min_fill=0 forces the mapped plan on sparse grids.
-    Each adjacency against the oracle's propagate() on the same GPU-built weights; the CSR kernel bit-exact."""
+    Each adjacency against the oracle's propagate() on the same GPU-built weights; the CSR kernel bit-exact. The
+    widths cover the residual pass's lane layouts (16 lanes per row up to F = 64, 32 at 128, 64 above)."""
     from protgram_directgcn_amd import graph as gr, ngram, ops
     seqs = pkg.synth.protein_sequences(nseq, 120, seed=n * 100 + nseq, rare=rare, composition="uniform")
     tr = ngram.ngram_transitions(seqs, n, device=cuda)
